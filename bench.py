@@ -1,0 +1,206 @@
+"""Benchmark: denoising-steps/s on 8-channel 128^3 wavelet volumes (BASELINE.json
+config 2: BraTS 4-modality -> 1 conditional synthesis, 1000-step DDPM, bf16).
+
+One step = one p_sample of the i2i wavelet diffusion: the production U-Net
+(run.sh configuration, 81.5 M parameters, seeded non-zero weights) on
+[x_t (8) | cond (24)] at 128^3 subbands, then the fused IDWT->clamp->DWT ->
+posterior-mean -> +sigma*noise epilogue, noise drawn with th.randn_like like the
+reference.  Inputs are synthetic 256^3 phantoms (no datasets offline), DWT'd on
+the GPU before the timed region.
+
+Multi-GPU: sampling shards by volume ("replicas only"): each rank
+denoises its own volume, no collective on the data path; value = all ranks'
+steps / max-over-ranks time.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+`roofline` for the dominant kernel (conv3d implicit GEMM, all launches of a
+step) and `cpu_baseline` (the CPU oracle timed on this host, rank 0, N=1).
+"""
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "fast-cwdm_amd"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+F32_PEAK_TFLOPS = 157.3
+
+
+def seeded_weights(model, seed):
+    """Non-degenerate weights of the production architecture (the reference's
+    zero-init would make every ResBlock an identity)."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            if p.dim() == 1 and (".in_layers.0." in name or ".out_layers.0." in name or name.startswith("out.0.")):
+                p.copy_((1.0 if name.endswith("weight") else 0.0) + 0.1 * torch.randn(p.shape, generator=g))
+            elif p.dim() >= 2:
+                p.copy_(torch.randn(p.shape, generator=g) / math.sqrt(p[0].numel()))
+            else:
+                p.copy_(0.05 * torch.randn(p.shape, generator=g))
+
+
+def phantom_gpu(n, seed, device):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    ax = (0.75 + 0.15 * torch.rand(3, generator=g)).tolist()
+    lin = torch.linspace(-1, 1, n, device=device)
+    z, y, x = lin.view(n, 1, 1), lin.view(1, n, 1), lin.view(1, 1, n)
+    mask = (z / ax[0]) ** 2 + (y / ax[1]) ** 2 + (x / ax[2]) ** 2 <= 1.0
+    img = torch.zeros(n, n, n, device=device)
+    for _ in range(6):
+        c = ((torch.rand(3, generator=g) - 0.5) * 1.2).tolist()
+        s = float(0.15 + 0.35 * torch.rand(1, generator=g))
+        a = float(0.3 + 0.7 * torch.rand(1, generator=g))
+        img += a * torch.exp(-((z - c[0]) ** 2 + (y - c[1]) ** 2 + (x - c[2]) ** 2) / (2 * s * s))
+    img = img * mask
+    return (img / img.max()).clamp(0, 1).view(1, 1, n, n, n)
+
+
+def build(args, device):
+    from guided_diffusion import script_util
+    margs = script_util.run_sh_model_args(diffusion_steps=1000, sample_schedule="direct")
+    keys = script_util.model_and_diffusion_defaults().keys()
+    model, diffusion = script_util.create_model_and_diffusion(**{k: margs[k] for k in keys},
+                                                              compute_dtype=args.dtype)
+    diffusion.mode = "i2i"
+    seeded_weights(model, 1)
+    model.to(device)
+    return model, diffusion
+
+
+def cpu_baseline(n, threads):
+    """The oracle (PyTorch-CPU fp32 restatement of the reference path) on this
+    host: one full denoising step (U-Net forward + p_sample epilogue) at n^3."""
+    from oracle import diffusion as od, unet as ou
+    torch.set_num_threads(threads)
+    P = ou.random_params(seed=1)
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"))
+    model = ou.OracleUNet(P)
+    x = torch.randn(1, 8, n, n, n)
+    cond = torch.rand(1, 24, n, n, n)
+    noise = torch.randn(1, 8, n, n, n)
+    t = torch.tensor([999])
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        od.p_sample(tab, model, x, t, cond, noise)
+    dt = time.perf_counter() - t0
+    return dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--grid", type=int, default=128, help="subband edge (image edge = 2x)")
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-grid", type=int, default=0, help="0 = same grid as the GPU run")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+
+    model, diffusion = build(args, device)
+    n = args.grid
+    # synthetic conditioning: 3 phantoms at (2n)^3 -> Haar DWT (LLL/3) on the GPU
+    from cwdm_hip import ops
+    cond = torch.empty(1, 24, n, n, n, device=device)
+    V = n ** 3
+    for k in range(3):
+        vol = phantom_gpu(2 * n, 100 + 10 * rank + k, device)
+        ops.dwt3d(vol, lll_div3=True, out=cond[:, 8 * k:], out_strides=(V, 24 * V, 0, 1))
+    torch.manual_seed(1234 + rank)
+    x_T = torch.randn(1, 8, n, n, n, device=device)
+    T = diffusion.num_timesteps
+    total = args.warmup + args.steps
+    assert total <= T
+    loop = diffusion._native_loop(model, x_T, list(range(T))[::-1][:total + 1], cond, True)
+    for _ in range(args.warmup):
+        next(loop)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        next(loop)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt)
+
+    # roofline of the dominant kernel: per-conv hipEvents over one extra step
+    plan = model.plan
+    plan.set_profiling(True)
+    next(loop)
+    torch.cuda.synchronize()
+    conv_ms, conv_flops, n_conv = plan.profile_read()
+    plan.set_profiling(False)
+    step_flops = plan.flops(1, n, n, n)
+
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = world * args.steps / elapsed
+    peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
+    achieved = conv_flops / (conv_ms * 1e-3) / 1e12
+    res = {
+        "metric": "denoising-steps/sec on 8-ch 128^3 volumes (1000-step DDPM, i2i cWDM)",
+        "value": round(value, 4),
+        "unit": "denoising-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (seeded 256^3 phantoms -> Haar DWT; seeded non-zero weights)",
+        "config": {"workload": "config2: BraTS 3->1 conditional synthesis, 1xMI355X per replica, "
+                               f"{n}^3 subbands, 1000-step DDPM (direct linear schedule)",
+                   "model": "UNetModel run.sh (mc 64, mult 1,2,2,4,4, 2 res blocks, 81.5M params)",
+                   "global_batch": world, "seq_len": n ** 3, "parallelism": f"replicas{world}"},
+        "sampling_wallclock_s_per_volume_1000_steps": round(1000 * ms_per_step / 1000.0, 2),
+        "mfma_util_whole_step": round(step_flops * (value / world) / 1e12 / peak, 4),
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": None,
+                     "kernel": f"conv3d_kernel (all {n_conv} launches of one step; {conv_ms:.2f} ms, "
+                               f"{conv_flops / 1e12:.2f} TFLOP)"},
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        cg = args.cpu_grid or n
+        dt = cpu_baseline(cg, threads)
+        scale = (cg / n) ** 3
+        res["cpu_baseline"] = {"value": round(scale / dt, 6), "unit": "denoising-steps/s", "cores": threads,
+                               "kind": "port",
+                               "sample": f"1 oracle p_sample step (fp32 PyTorch-CPU restatement) at {cg}^3"
+                                         + ("" if cg == n else f", scaled by ({cg}/{n})^3")
+                                         + f" on {platform.processor() or platform.machine()}",
+                               "seconds": round(dt, 2)}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

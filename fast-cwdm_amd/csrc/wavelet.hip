@@ -1,0 +1,275 @@
+// Haar DWT/IDWT and the fused sampler step (HBM-bound, one 2x2x2 block per
+// thread).  Every product is rounded before the add (__fmul_rn/__fadd_rn), in
+// the stage order of the reference's matrices (DWT: H, W, D; IDWT: D, W, H),
+// so results match the oracle's elementwise restatement bit for bit.
+#include "common.hpp"
+
+namespace cwdm {
+
+namespace {
+
+constexpr float kC = 0.70710677f;  // fp32(1/sqrt(2)) -- pywt rec_lo/rec_hi
+
+__device__ __forceinline__ float mr(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float ad(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float sb(float a, float b) { return __fsub_rn(a, b); }
+
+// Analysis of a 2x2x2 block v[a][b][e] (a: D parity, b: H, e: W) into the 8
+// bands in reference order LLL, LLH, LHL, LHH, HLL, HLH, HHL, HHH.
+__device__ __forceinline__ void haar_fwd8(const float v[8], float o[8]) {
+  // stage 1: H (index bit 1)
+  float s1[8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float x0 = v[a * 4 + 0 * 2 + e], x1 = v[a * 4 + 1 * 2 + e];
+      s1[a * 4 + 0 * 2 + e] = ad(mr(kC, x0), mr(kC, x1));  // L_h
+      s1[a * 4 + 1 * 2 + e] = sb(mr(kC, x0), mr(kC, x1));  // H_h
+    }
+  // stage 2: W (bit 0)
+  float s2[8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float x0 = s1[a * 4 + b * 2 + 0], x1 = s1[a * 4 + b * 2 + 1];
+      s2[a * 4 + b * 2 + 0] = ad(mr(kC, x0), mr(kC, x1));
+      s2[a * 4 + b * 2 + 1] = sb(mr(kC, x0), mr(kC, x1));
+    }
+  // stage 3: D (bit 2); band index = (pD << 2) | (pH << 1) | pW
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float x0 = s2[0 * 4 + b * 2 + e], x1 = s2[1 * 4 + b * 2 + e];
+      o[0 * 4 + b * 2 + e] = ad(mr(kC, x0), mr(kC, x1));
+      o[1 * 4 + b * 2 + e] = sb(mr(kC, x0), mr(kC, x1));
+    }
+}
+
+// Synthesis: bands o[pD<<2|pH<<1|pW] -> block v[a<<2|b<<1|e]; D, then W, then H.
+__device__ __forceinline__ void haar_inv8(const float o[8], float v[8]) {
+  float s2[8];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float lo = o[0 * 4 + b * 2 + e], hi = o[1 * 4 + b * 2 + e];
+      s2[0 * 4 + b * 2 + e] = ad(mr(kC, lo), mr(kC, hi));
+      s2[1 * 4 + b * 2 + e] = sb(mr(kC, lo), mr(kC, hi));
+    }
+  float s1[8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float lo = s2[a * 4 + b * 2 + 0], hi = s2[a * 4 + b * 2 + 1];
+      s1[a * 4 + b * 2 + 0] = ad(mr(kC, lo), mr(kC, hi));
+      s1[a * 4 + b * 2 + 1] = sb(mr(kC, lo), mr(kC, hi));
+    }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float lo = s1[a * 4 + 0 * 2 + e], hi = s1[a * 4 + 1 * 2 + e];
+      v[a * 4 + 0 * 2 + e] = ad(mr(kC, lo), mr(kC, hi));
+      v[a * 4 + 1 * 2 + e] = sb(mr(kC, lo), mr(kC, hi));
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ float ld(const void* p, int64_t off) {
+  return Elem<T>::to_f(reinterpret_cast<const T*>(p)[off]);
+}
+template <typename T>
+__device__ __forceinline__ void st(void* p, int64_t off, float v) {
+  reinterpret_cast<T*>(p)[off] = Elem<T>::from_f(v);
+}
+
+struct S4 { int64_t k, b, c, v; };
+
+// one thread per subband voxel (b, c, i, j, k); k fastest -> the two W-adjacent
+// inputs of neighbouring threads are contiguous (float2 per (a, b) pair).
+template <typename OutT>
+__global__ void __launch_bounds__(256) dwt3d_kernel(const float* __restrict__ x, int64_t BC, int64_t d,
+                                                   int64_t h, int64_t w, void* __restrict__ out, S4 s,
+                                                   int C, int lll_div3) {
+  int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t nvox = d * h * w;
+  if (idx >= BC * nvox) return;
+  int64_t bc = idx / nvox, v = idx - bc * nvox;
+  int64_t k = v % w, j = (v / w) % h, i = v / (w * h);
+  int64_t W = 2 * w, H = 2 * h;
+  const float* base = x + bc * (nvox * 8) + ((2 * i) * H + 2 * j) * W + 2 * k;
+  float blk[8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float2 p = *reinterpret_cast<const float2*>(base + (a * H + b) * W);
+      blk[a * 4 + b * 2 + 0] = p.x;
+      blk[a * 4 + b * 2 + 1] = p.y;
+    }
+  float o[8];
+  haar_fwd8(blk, o);
+  if (lll_div3) o[0] = __fdiv_rn(o[0], 3.0f);
+  int64_t b_ = bc / C, c_ = bc - b_ * C;
+  int64_t off = b_ * s.b + c_ * s.c + v * s.v;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) st<OutT>(out, off + q * s.k, o[q]);
+}
+
+template <typename InT>
+__global__ void __launch_bounds__(256) idwt3d_kernel(const void* __restrict__ bands, S4 s, int64_t BC, int C,
+                                                    int64_t d, int64_t h, int64_t w, float* __restrict__ x,
+                                                    int lll_mul3, int clamp01) {
+  int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t nvox = d * h * w;
+  if (idx >= BC * nvox) return;
+  int64_t bc = idx / nvox, v = idx - bc * nvox;
+  int64_t k = v % w, j = (v / w) % h, i = v / (w * h);
+  int64_t b_ = bc / C, c_ = bc - b_ * C;
+  int64_t off = b_ * s.b + c_ * s.c + v * s.v;
+  float o[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = ld<InT>(bands, off + q * s.k);
+  if (lll_mul3) o[0] = mr(o[0], 3.0f);
+  float blk[8];
+  haar_inv8(o, blk);
+  int64_t W = 2 * w, H = 2 * h;
+  float* base = x + bc * (nvox * 8) + ((2 * i) * H + 2 * j) * W + 2 * k;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float2 p;
+      p.x = blk[a * 4 + b * 2 + 0];
+      p.y = blk[a * 4 + b * 2 + 1];
+      if (clamp01) {
+        p.x = fminf(fmaxf(p.x, 0.0f), 1.0f);
+        p.y = fminf(fmaxf(p.y, 0.0f), 1.0f);
+      }
+      *reinterpret_cast<float2*>(base + (a * H + b) * W) = p;
+    }
+}
+
+struct S3 { int64_t b, c, v; };
+inline S3 s3(const int64_t* p) { return p ? S3{p[0], p[1], p[2]} : S3{0, 0, 0}; }
+
+// Fused a3 + a7 + a9: one subband voxel (8 channels) per thread.
+template <typename MirT>
+__global__ void __launch_bounds__(256) sampler_kernel(cwdm_sampler_args a, S3 mo, S3 xt, S3 xp, S3 nz, S3 px,
+                                                     S3 mr_) {
+  int64_t nvox = a.d * a.h * a.w;
+  int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= a.B * nvox) return;
+  int64_t b = idx / nvox, v = idx - b * nvox;
+  int64_t t = a.t[b];
+  t = t < 0 ? 0 : (t >= a.T ? a.T - 1 : t);
+  const float* cf = a.coef + t * 8;
+  const float c1 = cf[0], c2 = cf[1], sg = cf[2];
+  float m[8], xv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    m[q] = a.model_out[b * mo.b + q * mo.c + v * mo.v];
+    xv[q] = a.x_t[b * xt.b + q * xt.c + v * xt.v];
+  }
+  if (a.mean_type == 1) {
+    // EPSILON: x0 = sqrt(1/acp) * x_t - sqrt(1/acp - 1) * eps (gaussian_diffusion.py:392-397)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) m[q] = sb(mr(cf[3], xv[q]), mr(cf[4], m[q]));
+  }
+  float pred[8];
+  if (a.clip_denoised) {
+    m[0] = mr(m[0], 3.0f);
+    float blk[8];
+    haar_inv8(m, blk);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) blk[q] = fminf(fmaxf(blk[q], 0.0f), 1.0f);
+    haar_fwd8(blk, pred);
+    pred[0] = __fdiv_rn(pred[0], 3.0f);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pred[q] = m[q];
+  }
+  const bool noisy = (t != 0) && a.noise;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float mean = ad(mr(c1, pred[q]), mr(c2, xv[q]));
+    float r = mean;
+    if (noisy) r = ad(mean, mr(sg, a.noise[b * nz.b + q * nz.c + v * nz.v]));
+    a.x_prev[b * xp.b + q * xp.c + v * xp.v] = r;
+    if (a.pred_xstart) a.pred_xstart[b * px.b + q * px.c + v * px.v] = pred[q];
+    if (a.mirror) st<MirT>(a.mirror, b * mr_.b + q * mr_.c + v * mr_.v, r);
+  }
+}
+
+}  // namespace
+
+}  // namespace cwdm
+
+using namespace cwdm;
+
+extern "C" int cwdm_haar_dwt3d(const float* x, int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
+                               void* out, int out_dtype, const int64_t* st, int lll_div3,
+                               cwdm_stream_t stream) {
+  CWDM_REQUIRE(x && out && st, CWDM_E_INVALID, "cwdm_haar_dwt3d: null pointer");
+  CWDM_REQUIRE(B > 0 && C > 0 && D > 0 && H > 0 && W > 0, CWDM_E_SHAPE, "cwdm_haar_dwt3d: empty volume");
+  CWDM_REQUIRE(D % 2 == 0 && H % 2 == 0 && W % 2 == 0, CWDM_E_SHAPE,
+               "cwdm_haar_dwt3d: D, H, W must be even (Haar single level)");
+  CWDM_REQUIRE(((uintptr_t)x & 7) == 0, CWDM_E_INVALID, "cwdm_haar_dwt3d: x must be 8-byte aligned");
+  S4 s{st[0], st[1], st[2], st[3]};
+  int64_t n = B * C * (D / 2) * (H / 2) * (W / 2);
+  dim3 grid((unsigned)ceil_div(n, 256));
+  if (out_dtype == CWDM_F32)
+    hipLaunchKernelGGL(dwt3d_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, x, B * C, D / 2, H / 2,
+                       W / 2, out, s, (int)C, lll_div3);
+  else if (out_dtype == CWDM_BF16)
+    hipLaunchKernelGGL(dwt3d_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, x, B * C, D / 2, H / 2,
+                       W / 2, out, s, (int)C, lll_div3);
+  else
+    return fail(CWDM_E_INVALID, "cwdm_haar_dwt3d: bad dtype");
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+extern "C" int cwdm_haar_idwt3d(const void* bands, int in_dtype, const int64_t* st, int64_t B, int64_t C,
+                                int64_t d, int64_t h, int64_t w, float* x, int lll_mul3, int clamp01,
+                                cwdm_stream_t stream) {
+  CWDM_REQUIRE(x && bands && st, CWDM_E_INVALID, "cwdm_haar_idwt3d: null pointer");
+  CWDM_REQUIRE(B > 0 && C > 0 && d > 0 && h > 0 && w > 0, CWDM_E_SHAPE, "cwdm_haar_idwt3d: empty volume");
+  CWDM_REQUIRE(((uintptr_t)x & 7) == 0, CWDM_E_INVALID, "cwdm_haar_idwt3d: x must be 8-byte aligned");
+  S4 s{st[0], st[1], st[2], st[3]};
+  int64_t n = B * C * d * h * w;
+  dim3 grid((unsigned)ceil_div(n, 256));
+  if (in_dtype == CWDM_F32)
+    hipLaunchKernelGGL(idwt3d_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, bands, s, B * C, (int)C, d,
+                       h, w, x, lll_mul3, clamp01);
+  else if (in_dtype == CWDM_BF16)
+    hipLaunchKernelGGL(idwt3d_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, bands, s, B * C, (int)C, d,
+                       h, w, x, lll_mul3, clamp01);
+  else
+    return fail(CWDM_E_INVALID, "cwdm_haar_idwt3d: bad dtype");
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+extern "C" int cwdm_sampler_step(const cwdm_sampler_args* a, cwdm_stream_t stream) {
+  CWDM_REQUIRE(a && a->model_out && a->x_t && a->x_prev && a->coef && a->t, CWDM_E_INVALID,
+               "cwdm_sampler_step: null pointer");
+  CWDM_REQUIRE(a->B > 0 && a->d > 0 && a->h > 0 && a->w > 0 && a->T > 0, CWDM_E_SHAPE,
+               "cwdm_sampler_step: empty shape");
+  int64_t n = a->B * a->d * a->h * a->w;
+  dim3 grid((unsigned)ceil_div(n, 256));
+  S3 mo = s3(a->mo_s), xt = s3(a->xt_s), xp = s3(a->xp_s), nz = s3(a->nz_s), px = s3(a->px_s),
+     mi = s3(a->mr_s);
+  if (a->mirror && a->mirror_dtype == CWDM_BF16)
+    hipLaunchKernelGGL(sampler_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, *a, mo, xt, xp, nz, px, mi);
+  else if (!a->mirror || a->mirror_dtype == CWDM_F32)
+    hipLaunchKernelGGL(sampler_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *a, mo, xt, xp, nz, px, mi);
+  else
+    return fail(CWDM_E_INVALID, "cwdm_sampler_step: bad mirror dtype");
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}

@@ -1,0 +1,102 @@
+"""Torch-tensor wrappers over the libcwdm C ABI (device memory + current stream).
+
+PyTorch is plumbing here: it owns device buffers and streams; every compute
+step is a libcwdm kernel.  Inputs must live on a ROCm device -- there is no CPU
+path (``_need_cuda`` raises).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import CWDM_BF16, CWDM_F32, check, lib, strides
+
+DT = {torch.float32: CWDM_F32, torch.bfloat16: CWDM_BF16}
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("fast-cwdm_amd: HIP kernels need tensors on a ROCm device "
+                               "(no CPU fallback in the product path)")
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def dwt3d(x, lll_div3=False, out=None, out_strides=None, out_dtype=None):
+    """Haar DWT of an NCDHW fp32 volume.  Returns (8, B, C, d, h, w) unless
+    ``out``/``out_strides`` (band, b, c, voxel) are given."""
+    _need_cuda(x)
+    if x.dim() != 5:
+        raise AssertionError("DWT_3D expects a 5-D (N, C, D, H, W) tensor")
+    x = x.contiguous()
+    if x.dtype != torch.float32:
+        raise TypeError("DWT_3D: fp32 input expected (the reference's filter matrices are fp32)")
+    B, C, D, H, W = x.shape
+    if out is None:
+        out = torch.empty((8, B, C, D // 2, H // 2, W // 2), device=x.device,
+                          dtype=out_dtype or torch.float32)
+        v = (D // 2) * (H // 2) * (W // 2)
+        out_strides = (B * C * v, C * v, v, 1)
+    check(lib().cwdm_haar_dwt3d(_p(x), B, C, D, H, W, _p(out), DT[out.dtype], strides(*out_strides),
+                                1 if lll_div3 else 0, _stream()), "DWT_3D")
+    return out
+
+
+def idwt3d(bands, band_strides, B, C, d, h, w, lll_mul3=False, clamp01=False, out=None):
+    """Haar IDWT.  ``bands`` is a tensor holding all 8 subbands addressed by
+    ``band_strides`` (band, b, c, voxel); returns an NCDHW fp32 volume."""
+    _need_cuda(bands)
+    if out is None:
+        out = torch.empty((B, C, 2 * d, 2 * h, 2 * w), device=bands.device, dtype=torch.float32)
+    check(lib().cwdm_haar_idwt3d(_p(bands), DT[bands.dtype], strides(*band_strides), B, C, d, h, w, _p(out),
+                                 1 if lll_mul3 else 0, 1 if clamp01 else 0, _stream()), "IDWT_3D")
+    return out
+
+
+def copy3(src, src_strides, dst, dst_strides, B, C, V):
+    _need_cuda(src, dst)
+    check(lib().cwdm_copy3(_p(src), DT[src.dtype], strides(*src_strides), _p(dst), DT[dst.dtype],
+                           strides(*dst_strides), B, C, V, _stream()), "copy3")
+    return dst
+
+
+def ncdhw_strides(t):
+    """(b, c, voxel) element strides of a contiguous NCDHW tensor."""
+    B, C = t.shape[:2]
+    v = t[0, 0].numel()
+    return (C * v, v, 1)
+
+
+def ndhwc_strides(B, C, V, c_total=None):
+    ct = C if c_total is None else c_total
+    return (V * ct, 1, ct)
+
+
+def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t, T, B, d, h, w,
+                 clip_denoised=True, pred_xstart=None, px_s=(0, 0, 0), mirror=None, mr_s=(0, 0, 0),
+                 mean_type=0):
+    """Fused process_xstart + posterior mean + noise (cwdm_sampler_step)."""
+    _need_cuda(model_out, x_t, x_prev, noise, coef, t, pred_xstart, mirror)
+    a = _lib.SamplerArgs()
+    a.model_out, a.mo_s = model_out.data_ptr(), _lib.I64x3(*mo_s)
+    a.x_t, a.xt_s = x_t.data_ptr(), _lib.I64x3(*xt_s)
+    a.x_prev, a.xp_s = x_prev.data_ptr(), _lib.I64x3(*xp_s)
+    a.noise = noise.data_ptr() if noise is not None else None
+    a.nz_s = _lib.I64x3(*nz_s)
+    a.pred_xstart = pred_xstart.data_ptr() if pred_xstart is not None else None
+    a.px_s = _lib.I64x3(*px_s)
+    a.mirror = mirror.data_ptr() if mirror is not None else None
+    a.mirror_dtype = DT[mirror.dtype] if mirror is not None else CWDM_F32
+    a.mr_s = _lib.I64x3(*mr_s)
+    a.coef, a.t = coef.data_ptr(), t.data_ptr()
+    a.T, a.B, a.d, a.h, a.w = T, B, d, h, w
+    a.clip_denoised = 1 if clip_denoised else 0
+    a.mean_type = int(mean_type)
+    check(lib().cwdm_sampler_step(ctypes.byref(a), _stream()), "sampler_step")

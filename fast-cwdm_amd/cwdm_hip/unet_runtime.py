@@ -1,0 +1,136 @@
+"""Python handle on the native U-Net plan (cwdm_unet_* in include/cwdm.h).
+
+The plan (C++) owns the topology, the parameter naming contract and the launch
+sequence; this wrapper only holds device buffers (packed weights, workspace)
+allocated through torch's caching allocator.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import CWDM_BF16, CWDM_F32, check, lib
+from .ops import _need_cuda, _stream
+
+_DTYPES = {"fp32": CWDM_F32, "float32": CWDM_F32, "bf16": CWDM_BF16, "bfloat16": CWDM_BF16}
+TORCH_DT = {CWDM_F32: torch.float32, CWDM_BF16: torch.bfloat16}
+
+
+def parse_dtype(d):
+    if isinstance(d, torch.dtype):
+        d = {torch.float32: "fp32", torch.bfloat16: "bf16"}.get(d, str(d))
+    if d not in _DTYPES:
+        raise ValueError(f"compute dtype must be fp32 or bf16, got {d!r}")
+    return _DTYPES[d]
+
+
+class UNetPlan:
+    def __init__(self, in_channels, model_channels, out_channels, num_res_blocks, channel_mult, num_groups,
+                 dtype="fp32"):
+        cfg = _lib.UNetConfig()
+        cfg.in_channels, cfg.model_channels, cfg.out_channels = in_channels, model_channels, out_channels
+        cfg.num_res_blocks, cfg.num_levels = num_res_blocks, len(channel_mult)
+        if len(channel_mult) > 8:
+            raise ValueError("at most 8 U-Net levels")
+        for i, m in enumerate(channel_mult):
+            cfg.channel_mult[i] = int(m)
+        cfg.num_groups = num_groups
+        cfg.dtype = parse_dtype(dtype)
+        self.dtype = cfg.dtype
+        self.torch_dtype = TORCH_DT[cfg.dtype]
+        self.num_levels = len(channel_mult)
+        self.in_channels, self.out_channels = in_channels, out_channels
+        h = ctypes.c_void_p()
+        check(lib().cwdm_unet_create(ctypes.byref(cfg), ctypes.byref(h)), "UNetModel")
+        self._h = h
+        self._lib = lib()
+        self.param_specs = []
+        name = ctypes.create_string_buffer(256)
+        shape = (ctypes.c_int64 * 5)()
+        nd = ctypes.c_int()
+        for i in range(lib().cwdm_unet_num_params(h)):
+            check(lib().cwdm_unet_param_info(h, i, name, 256, shape, ctypes.byref(nd)))
+            self.param_specs.append((name.value.decode(), tuple(shape[k] for k in range(nd.value))))
+        self._ws = None
+        self._ws_key = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.cwdm_unet_destroy(h)
+            self._h = None
+
+    @property
+    def packed_bytes(self):
+        return int(lib().cwdm_unet_packed_bytes(self._h))
+
+    def pack(self, params, packed=None):
+        """params: fp32 contiguous device tensors in param_specs order."""
+        if len(params) != len(self.param_specs):
+            raise ValueError("parameter count mismatch")
+        _need_cuda(*params)
+        dev = params[0].device
+        if packed is None:
+            packed = torch.empty(self.packed_bytes, dtype=torch.uint8, device=dev)
+        arr = (ctypes.c_void_p * len(params))(*[p.data_ptr() for p in params])
+        check(lib().cwdm_unet_pack(self._h, arr, ctypes.c_void_p(packed.data_ptr()), _stream()), "pack")
+        return packed
+
+    def workspace_bytes(self, B, D, H, W):
+        n = int(lib().cwdm_unet_workspace_bytes(self._h, B, D, H, W))
+        if n < 0:
+            raise AssertionError("bad grid")
+        return n
+
+    def workspace(self, B, D, H, W, device):
+        key = (B, D, H, W, str(device))
+        if self._ws_key != key:
+            self._ws = None
+            self._ws = torch.empty(self.workspace_bytes(B, D, H, W), dtype=torch.uint8, device=device)
+            self._ws_key = key
+        return self._ws
+
+    def check_grid(self, D, H, W):
+        div = 2 ** (self.num_levels - 1)
+        if D % div or H % div or W % div:
+            raise AssertionError(f"every subband edge must be divisible by {div} (got {D}x{H}x{W})")
+
+    def forward(self, packed, x_ndhwc, t_f32, out_ndhwc, B, D, H, W, ws=None):
+        _need_cuda(packed, x_ndhwc, t_f32, out_ndhwc)
+        self.check_grid(D, H, W)
+        if ws is None:
+            ws = self.workspace(B, D, H, W, x_ndhwc.device)
+        check(lib().cwdm_unet_forward(self._h, ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(x_ndhwc.data_ptr()),
+                                      ctypes.c_void_p(t_f32.data_ptr()), ctypes.c_void_p(out_ndhwc.data_ptr()),
+                                      B, D, H, W, ctypes.c_void_p(ws.data_ptr()), ws.numel(), _stream()),
+              "UNetModel.forward")
+        return out_ndhwc
+
+    def flops(self, B, D, H, W):
+        return float(lib().cwdm_unet_flops(self._h, B, D, H, W))
+
+    def trace_tensors(self, ws, B, D, H, W):
+        """Views of every block output left in the workspace (NDHWC)."""
+        out = []
+        n = lib().cwdm_unet_trace_count(self._h)
+        off, ch, lv = ctypes.c_int64(), ctypes.c_int(), ctypes.c_int()
+        es = 2 if self.dtype == CWDM_BF16 else 4
+        for i in range(n):
+            check(lib().cwdm_unet_trace_info(self._h, i, B, D, H, W, ctypes.byref(off), ctypes.byref(ch),
+                                             ctypes.byref(lv)))
+            if off.value < 0:
+                out.append(None)
+                continue
+            d, h, w = D >> lv.value, H >> lv.value, W >> lv.value
+            nbytes = B * d * h * w * ch.value * es
+            buf = ws[off.value:off.value + nbytes].view(self.torch_dtype).view(B, d, h, w, ch.value)
+            out.append(buf)
+        return out
+
+    def set_profiling(self, on):
+        check(lib().cwdm_unet_set_profiling(self._h, 1 if on else 0))
+
+    def profile_read(self):
+        ms, fl, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        check(lib().cwdm_unet_profile_read(self._h, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(n)))
+        return ms.value, fl.value, n.value

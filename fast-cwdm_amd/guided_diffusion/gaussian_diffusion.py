@@ -1,0 +1,429 @@
+"""GaussianDiffusion for the i2i wavelet path (drop-in for
+guided_diffusion/gaussian_diffusion.py of the reference).
+
+Host-side float64 tables are the reference's (:143-205).  On device:
+* the per-step tail of p_sample -- process_xstart (IDWT(LLL*3) -> clamp ->
+  DWT -> LLL/3), q_posterior_mean_variance and the noise add -- is ONE
+  kernel (cwdm_sampler_step) reading a [T][8] fp32 coefficient table, so
+  nothing syncs with the host inside the loop;
+* when the model is the native ``UNetModel`` the sampling loop keeps the
+  U-Net input resident channels-last ([x_t | cond] in one NDHWC buffer, the
+  sampler kernel writes x_{t-1} straight into it) -- the reference's per-step
+  ``th.cat([x, cond])`` and layout moves disappear;
+* DWTs of the training path write the wavelet channels straight into the
+  model-input buffer.
+Noise is drawn with ``th.randn_like`` exactly where the reference draws it, so
+a seeded run consumes the same RNG stream.
+
+Deliberate differences (DESIGN.md "reference quirks"): ``p_sample_loop``
+runs ``num_timesteps`` steps (the reference hard-codes 1000, which only works
+for T=1000, :672); i2i DDIM is implemented by spec (the reference raises,
+:752-757).
+"""
+import enum
+import math
+
+import numpy as np
+import torch as th
+
+from cwdm_hip import ops
+from DWT_IDWT.DWT_IDWT_layer import DWT_3D, IDWT_3D
+from .nn import mean_flat
+
+dwt = DWT_3D("haar")
+idwt = IDWT_3D("haar")
+
+
+def get_named_beta_schedule(schedule_name, num_diffusion_timesteps, sample_schedule="direct"):
+    """Reference :30-67 (linear direct / Fast-DDPM sampled, cosine)."""
+    if schedule_name == "linear":
+        if sample_schedule == "direct":
+            scale = 1000 / num_diffusion_timesteps
+            return np.linspace(scale * 0.0001, scale * 0.02, num_diffusion_timesteps, dtype=np.float64)
+        if sample_schedule == "sampled":
+            full_betas = np.linspace(0.0001, 0.02, 1000, dtype=np.float64)
+            full_acp = np.cumprod(1.0 - full_betas, axis=0)
+            indices = np.linspace(0, 999, num_diffusion_timesteps, dtype=int)
+            s_acp = full_acp[indices]
+            prev = np.concatenate([[1.0], s_acp[:-1]])
+            return np.clip(1.0 - s_acp / prev, 0.0001, 0.999)
+        raise NotImplementedError(f"Unknown sample_schedule: {sample_schedule}")
+    if schedule_name == "cosine":
+        return betas_for_alpha_bar(num_diffusion_timesteps,
+                                   lambda t: math.cos((t + 0.008) / 1.008 * math.pi / 2) ** 2)
+    raise NotImplementedError(f"unknown beta schedule: {schedule_name}")
+
+
+def betas_for_alpha_bar(num_diffusion_timesteps, alpha_bar, max_beta=0.999):
+    betas = []
+    for i in range(num_diffusion_timesteps):
+        t1 = i / num_diffusion_timesteps
+        t2 = (i + 1) / num_diffusion_timesteps
+        betas.append(min(1 - alpha_bar(t2) / alpha_bar(t1), max_beta))
+    return np.array(betas)
+
+
+class ModelMeanType(enum.Enum):
+    PREVIOUS_X = enum.auto()
+    START_X = enum.auto()
+    EPSILON = enum.auto()
+
+
+class ModelVarType(enum.Enum):
+    LEARNED = enum.auto()
+    FIXED_SMALL = enum.auto()
+    FIXED_LARGE = enum.auto()
+    LEARNED_RANGE = enum.auto()
+
+
+class LossType(enum.Enum):
+    MSE = enum.auto()
+    RESCALED_MSE = enum.auto()
+    KL = enum.auto()
+    RESCALED_KL = enum.auto()
+
+    def is_vb(self):
+        return self == LossType.KL or self == LossType.RESCALED_KL
+
+
+def _ncdhw(t):
+    return ops.ncdhw_strides(t)
+
+
+class GaussianDiffusion:
+    def __init__(self, *, betas, model_mean_type, model_var_type, loss_type, rescale_timesteps=False,
+                 mode="default", loss_level="image"):
+        self.model_mean_type = model_mean_type
+        self.model_var_type = model_var_type
+        self.loss_type = loss_type
+        self.rescale_timesteps = rescale_timesteps
+        self.mode = mode
+        self.loss_level = loss_level
+        betas = np.array(betas, dtype=np.float64)
+        self.betas = betas
+        assert len(betas.shape) == 1, "betas must be 1-D"
+        assert (betas > 0).all() and (betas <= 1).all()
+        self.num_timesteps = int(betas.shape[0])
+        alphas = 1.0 - betas
+        self.alphas_cumprod = np.cumprod(alphas, axis=0)
+        self.alphas_cumprod_prev = np.append(1.0, self.alphas_cumprod[:-1])
+        self.alphas_cumprod_next = np.append(self.alphas_cumprod[1:], 0.0)
+        self.sqrt_alphas_cumprod = np.sqrt(self.alphas_cumprod)
+        self.sqrt_one_minus_alphas_cumprod = np.sqrt(1.0 - self.alphas_cumprod)
+        self.log_one_minus_alphas_cumprod = np.log(1.0 - self.alphas_cumprod)
+        self.sqrt_recip_alphas_cumprod = np.sqrt(1.0 / self.alphas_cumprod)
+        self.sqrt_recipm1_alphas_cumprod = np.sqrt(1.0 / self.alphas_cumprod - 1)
+        self.posterior_variance = betas * (1.0 - self.alphas_cumprod_prev) / (1.0 - self.alphas_cumprod)
+        self.posterior_log_variance_clipped = np.log(np.append(self.posterior_variance[1], self.posterior_variance[1:]))
+        self.posterior_mean_coef1 = betas * np.sqrt(self.alphas_cumprod_prev) / (1.0 - self.alphas_cumprod)
+        self.posterior_mean_coef2 = (1.0 - self.alphas_cumprod_prev) * np.sqrt(alphas) / (1.0 - self.alphas_cumprod)
+        self._dev_cache = {}
+
+    # ---- tables -------------------------------------------------------------
+    def _fixed_variance(self):
+        if self.model_var_type == ModelVarType.FIXED_LARGE:
+            v = np.append(self.posterior_variance[1], self.betas[1:])
+            return v, np.log(v)
+        if self.model_var_type == ModelVarType.FIXED_SMALL:
+            return self.posterior_variance, self.posterior_log_variance_clipped
+        raise NotImplementedError(f"{self.model_var_type} (learned variances are not on the fast-cwdm path)")
+
+    def coef_table(self, device):
+        """[T][8] fp32 device table read by cwdm_sampler_step: coef1, coef2,
+        exp(0.5*log_var) (computed like the reference, in fp32 from the fp32
+        log-variance), sqrt(1/acp), sqrt(1/acp-1)."""
+        key = ("coef", str(device), self.model_var_type)
+        if key not in self._dev_cache:
+            _, logv = self._fixed_variance()
+            sig = th.exp(0.5 * th.from_numpy(logv).float())
+            tab = th.zeros((self.num_timesteps, 8), dtype=th.float32)
+            tab[:, 0] = th.from_numpy(self.posterior_mean_coef1).float()
+            tab[:, 1] = th.from_numpy(self.posterior_mean_coef2).float()
+            tab[:, 2] = sig
+            tab[:, 3] = th.from_numpy(self.sqrt_recip_alphas_cumprod).float()
+            tab[:, 4] = th.from_numpy(self.sqrt_recipm1_alphas_cumprod).float()
+            self._dev_cache[key] = tab.to(device)
+        return self._dev_cache[key]
+
+    def _mean_type_code(self):
+        if self.model_mean_type == ModelMeanType.START_X:
+            return 0
+        if self.model_mean_type == ModelMeanType.EPSILON:
+            return 1
+        raise NotImplementedError(f"{self.model_mean_type} is not on the fast-cwdm path")
+
+    # ---- reference API ------------------------------------------------------
+    def q_mean_variance(self, x_start, t):
+        mean = _extract_into_tensor(self.sqrt_alphas_cumprod, t, x_start.shape) * x_start
+        variance = _extract_into_tensor(1.0 - self.alphas_cumprod, t, x_start.shape)
+        log_variance = _extract_into_tensor(self.log_one_minus_alphas_cumprod, t, x_start.shape)
+        return mean, variance, log_variance
+
+    def q_sample(self, x_start, t, noise=None):
+        if noise is None:
+            noise = th.randn_like(x_start)
+        assert noise.shape == x_start.shape
+        return (_extract_into_tensor(self.sqrt_alphas_cumprod, t, x_start.shape) * x_start
+                + _extract_into_tensor(self.sqrt_one_minus_alphas_cumprod, t, x_start.shape) * noise)
+
+    def q_posterior_mean_variance(self, x_start, x_t, t):
+        assert x_start.shape == x_t.shape
+        mean = (_extract_into_tensor(self.posterior_mean_coef1, t, x_t.shape) * x_start
+                + _extract_into_tensor(self.posterior_mean_coef2, t, x_t.shape) * x_t)
+        var = _extract_into_tensor(self.posterior_variance, t, x_t.shape)
+        logv = _extract_into_tensor(self.posterior_log_variance_clipped, t, x_t.shape)
+        return mean, var, logv
+
+    def _scale_timesteps(self, t):
+        if self.rescale_timesteps:
+            return t.float() * (1000.0 / self.num_timesteps)
+        return t
+
+    def _model_timestep(self, i):
+        """The (float) timestep value the model sees for step index i."""
+        v = float(i)
+        if self.rescale_timesteps:
+            v = v * (1000.0 / self.num_timesteps)
+        return v
+
+    def _predict_xstart_from_eps(self, x_t, t, eps):
+        assert x_t.shape == eps.shape
+        return (_extract_into_tensor(self.sqrt_recip_alphas_cumprod, t, x_t.shape) * x_t
+                - _extract_into_tensor(self.sqrt_recipm1_alphas_cumprod, t, x_t.shape) * eps)
+
+    def _predict_eps_from_xstart(self, x_t, t, pred_xstart):
+        if self.mode == "segmentation":
+            x_t = x_t[:, -pred_xstart.shape[1]:, ...]
+        assert pred_xstart.shape == x_t.shape
+        return (_extract_into_tensor(self.sqrt_recip_alphas_cumprod, t, x_t.shape) * x_t - pred_xstart) / \
+            _extract_into_tensor(self.sqrt_recipm1_alphas_cumprod, t, x_t.shape)
+
+    def _check_t(self, t):
+        tmin, tmax = int(t.min()), int(t.max())
+        if tmin < 0 or tmax >= self.num_timesteps:
+            raise IndexError(f"Timesteps out of bounds: min={tmin}, max={tmax}, arr len={self.num_timesteps}")
+
+    def _epilogue(self, model_output, x, t, clip_denoised, denoised_fn, noise):
+        """cwdm_sampler_step on NCDHW tensors; returns (sample_or_mean, pred_xstart)."""
+        B, C = x.shape[:2]
+        d, h, w = x.shape[2:]
+        if clip_denoised and C != 8:
+            raise AssertionError("process_xstart needs the 8 Haar subbands (gaussian_diffusion.py:335-354)")
+        mean_type = self._mean_type_code()
+        mo = model_output.contiguous().float()
+        if denoised_fn is not None:
+            x0 = mo if mean_type == 0 else self._predict_xstart_from_eps(x, t, mo)
+            mo = denoised_fn(x0).contiguous().float()
+            mean_type = 0
+        xt = x.contiguous().float()
+        t_dev = t.to(device=x.device, dtype=th.int64).contiguous()
+        out = th.empty_like(xt)
+        pred = th.empty_like(xt)
+        nz = noise.contiguous().float() if noise is not None else None
+        s = _ncdhw(xt)
+        ops.sampler_step(mo, s, xt, s, out, s, nz, s if nz is not None else (0, 0, 0), self.coef_table(x.device),
+                         t_dev, self.num_timesteps, B, d, h, w, clip_denoised=clip_denoised, pred_xstart=pred,
+                         px_s=s, mean_type=mean_type)
+        return out, pred
+
+    def p_mean_variance(self, model, x, t, clip_denoised=True, denoised_fn=None, model_kwargs=None, cond=None):
+        if model_kwargs is None:
+            model_kwargs = {}
+        B, C = x.shape[:2]
+        assert t.shape == (B,)
+        x_cond = th.cat([x, cond], dim=1) if self.mode == "i2i" else x
+        model_output = model(x_cond, self._scale_timesteps(t), **model_kwargs)
+        self._check_t(t)
+        var, logv = self._fixed_variance()
+        model_variance = _extract_into_tensor(var, t, x.shape)
+        model_log_variance = _extract_into_tensor(logv, t, x.shape)
+        x8 = x[:, :8, ...] if self.mode == "i2i" else x
+        mean, pred = self._epilogue(model_output, x8, t, clip_denoised, denoised_fn, None)
+        assert mean.shape == model_log_variance.shape == pred.shape == x.shape
+        return {"mean": mean, "variance": model_variance, "log_variance": model_log_variance, "pred_xstart": pred}
+
+    def p_sample(self, model, x, t, clip_denoised=True, denoised_fn=None, cond_fn=None, model_kwargs=None,
+                 cond=None, noise_fn=None):
+        if cond_fn is not None:
+            raise NotImplementedError("cond_fn guidance is not on the fast-cwdm path")
+        if model_kwargs is None:
+            model_kwargs = {}
+        B = x.shape[0]
+        assert t.shape == (B,)
+        x_cond = th.cat([x, cond], dim=1) if self.mode == "i2i" else x
+        model_output = model(x_cond, self._scale_timesteps(t), **model_kwargs)
+        self._check_t(t)
+        noise = (noise_fn or th.randn_like)(x)
+        sample, pred = self._epilogue(model_output, x, t, clip_denoised, denoised_fn, noise)
+        return {"sample": sample, "pred_xstart": pred}
+
+    def p_sample_loop(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None, cond_fn=None,
+                      model_kwargs=None, device=None, progress=True, cond=None, time=None, noise_fn=None):
+        final = None
+        for sample in self.p_sample_loop_progressive(model, shape, time=time, noise=noise,
+                                                     clip_denoised=clip_denoised, denoised_fn=denoised_fn,
+                                                     cond_fn=cond_fn, model_kwargs=model_kwargs, device=device,
+                                                     progress=progress, cond=cond, noise_fn=noise_fn):
+            final = sample
+        return final["sample"]
+
+    def p_sample_loop_progressive(self, model, shape, time=None, noise=None, clip_denoised=True, denoised_fn=None,
+                                  cond_fn=None, model_kwargs=None, device=None, progress=True, cond=None,
+                                  noise_fn=None):
+        """Reference :668-719.  ``noise_fn`` (extension, default ``th.randn_like``)
+        supplies each step's noise; parity tests inject fixed noise through it."""
+        if device is None:
+            device = next(model.parameters()).device
+        assert isinstance(shape, (tuple, list))
+        img = noise if noise is not None else th.randn(*shape, device=device)
+        time = self.num_timesteps if time is None else time
+        if time > self.num_timesteps:
+            raise IndexError(f"Timesteps out of bounds: max={time - 1}, arr len={self.num_timesteps}")
+        indices = list(range(time))[::-1]
+        if progress:
+            try:
+                from tqdm.auto import tqdm
+                indices = tqdm(indices)
+            except ImportError:  # pragma: no cover
+                pass
+        unet = _native_unet(model)
+        if unet is not None and denoised_fn is None and cond_fn is None and not model_kwargs:
+            yield from self._native_loop(unet, img, indices, cond, clip_denoised, noise_fn)
+            return
+        for i in indices:
+            t = th.tensor([i] * shape[0], device=device)
+            with th.no_grad():
+                out = self.p_sample(model, img, t, clip_denoised=clip_denoised, denoised_fn=denoised_fn,
+                                    cond_fn=cond_fn, model_kwargs=model_kwargs, cond=cond, noise_fn=noise_fn)
+                yield out
+                img = out["sample"]
+
+    def _native_loop(self, unet, img, indices, cond, clip_denoised, noise_fn=None):
+        """Channels-last resident loop for the native UNetModel."""
+        dev = img.device
+        B, C, d, h, w = img.shape
+        V = d * h * w
+        cin = unet.in_channels
+        ccond = cond.shape[1] if (self.mode == "i2i" and cond is not None) else 0
+        if C + ccond != cin:
+            raise AssertionError(f"model expects {cin} input channels, got {C} + {ccond}")
+        if clip_denoised and C != 8:
+            raise AssertionError("process_xstart needs the 8 Haar subbands")
+        plan = unet.plan
+        plan.check_grid(d, h, w)
+        xin = th.empty((B, d, h, w, cin), dtype=plan.torch_dtype, device=dev)
+        img = img.contiguous().float()
+        ops.copy3(img, _ncdhw(img), xin, (V * cin, 1, cin), B, C, V)
+        if ccond:
+            cnd = cond.contiguous().float()
+            ops.copy3(cnd, _ncdhw(cnd), xin[..., C:], (V * cin, 1, cin), B, ccond, V)
+        out_nd = th.empty((B, d, h, w, C), dtype=th.float32, device=dev)
+        coef = self.coef_table(dev)
+        mean_type = self._mean_type_code()
+        s = _ncdhw(img)
+        with th.no_grad():
+            for i in indices:
+                t = th.full((B,), i, dtype=th.int64, device=dev)
+                t_model = th.full((B,), self._model_timestep(i), dtype=th.float32, device=dev)
+                unet.forward_ndhwc(xin, t_model, out_nd)
+                noise = (noise_fn or th.randn_like)(img)
+                new = th.empty_like(img)
+                pred = th.empty_like(img)
+                ops.sampler_step(out_nd, (V * C, 1, C), img, s, new, s, noise, s, coef, t, self.num_timesteps,
+                                 B, d, h, w, clip_denoised=clip_denoised, pred_xstart=pred, px_s=s,
+                                 mirror=xin, mr_s=(V * cin, 1, cin), mean_type=mean_type)
+                yield {"sample": new, "pred_xstart": pred}
+                img = new
+
+    # ---- DDIM (i2i by spec; the reference raises NotImplementedError) --------
+    def ddim_sample(self, model, x, t, t_cpu=None, t_prev=None, t_prev_cpu=None, clip_denoised=True,
+                    denoised_fn=None, cond_fn=None, model_kwargs=None, eta=0.0, sampling_steps=0, cond=None):
+        out = self.p_mean_variance(model, x, t, clip_denoised=clip_denoised, denoised_fn=denoised_fn,
+                                   model_kwargs=model_kwargs, cond=cond)
+        x8 = x[:, :8] if self.mode == "i2i" else x
+        eps = self._predict_eps_from_xstart(x8, t, out["pred_xstart"])
+        ab = _extract_into_tensor(self.alphas_cumprod, t, x8.shape)
+        abp = _extract_into_tensor(self.alphas_cumprod_prev, t, x8.shape)
+        sigma = eta * ((1 - abp) / (1 - ab)) ** 0.5 * (1 - ab / abp) ** 0.5
+        mean_pred = out["pred_xstart"] * abp ** 0.5 + (1 - abp - sigma ** 2) ** 0.5 * eps
+        return {"sample": mean_pred, "pred_xstart": out["pred_xstart"]}
+
+    def ddim_sample_loop(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None, cond_fn=None,
+                         model_kwargs=None, device=None, progress=False, eta=0.0, cond=None):
+        final = None
+        for s in self.ddim_sample_loop_progressive(model, shape, noise=noise, clip_denoised=clip_denoised,
+                                                   denoised_fn=denoised_fn, cond_fn=cond_fn,
+                                                   model_kwargs=model_kwargs, device=device, progress=progress,
+                                                   eta=eta, cond=cond):
+            final = s
+        return final["sample"]
+
+    def ddim_sample_loop_progressive(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None,
+                                     cond_fn=None, model_kwargs=None, device=None, progress=False, eta=0.0,
+                                     cond=None):
+        if device is None:
+            device = next(model.parameters()).device
+        img = noise if noise is not None else th.randn(*shape, device=device)
+        for i in list(range(self.num_timesteps))[::-1]:
+            t = th.tensor([i] * shape[0], device=device)
+            with th.no_grad():
+                out = self.ddim_sample(model, img, t, clip_denoised=clip_denoised, denoised_fn=denoised_fn,
+                                       model_kwargs=model_kwargs, eta=eta, cond=cond)
+                yield out
+                img = out["sample"]
+
+    # ---- training -----------------------------------------------------------
+    def training_losses(self, model, x_start, t, classifier=None, model_kwargs=None, noise=None, labels=None,
+                        mode="default", contr="t1n"):
+        """i2i training loss (reference :1084-1166): returns
+        (terms{"mse_wav": [8]}, model_output, model_output_idwt)."""
+        if model_kwargs is None:
+            model_kwargs = {}
+        if mode != "i2i":
+            raise NotImplementedError("training_losses: only mode='i2i' is on the fast-cwdm path")
+        order = {"t1n": ("t1n", "t1c", "t2w", "t2f"), "t1c": ("t1c", "t1n", "t2w", "t2f"),
+                 "t2w": ("t2w", "t1n", "t1c", "t2f"), "t2f": ("t2f", "t1n", "t1c", "t2w")}
+        if contr not in order:
+            raise ValueError("This contrast can't be synthesized.")
+        keys = order[contr]
+        target = x_start[keys[0]]
+        ops._need_cuda(target)
+        B, _, D, H, W = target.shape
+        d, h, w = D // 2, H // 2, W // 2
+        V = d * h * w
+        dev = target.device
+        # model input x_t | cond_dwt (B, 32, d, h, w); cond DWTs written in place with LLL/3
+        x_in = th.empty((B, 32, d, h, w), dtype=th.float32, device=dev)
+        s_in = (32 * V, V, 1)
+        for k, key in enumerate(keys[1:]):
+            src = x_start[key].contiguous().float()
+            ops.dwt3d(src, lll_div3=True, out=x_in[:, 8 + 8 * k:], out_strides=(V, s_in[0], 0, 1))
+        x0 = ops.dwt3d(target.contiguous().float(), lll_div3=True)          # (8, B, 1, d, h, w)
+        x_start_dwt = x0[:, :, 0].permute(1, 0, 2, 3, 4).contiguous()       # (B, 8, d, h, w)
+        noise_img = th.randn_like(target) if noise is None else noise
+        nz = ops.dwt3d(noise_img.contiguous().float())                      # no /3 on noise (:1143-1145)
+        noise_dwt = nz[:, :, 0].permute(1, 0, 2, 3, 4)
+        x_t = self.q_sample(x_start_dwt, t, noise=noise_dwt)
+        x_in[:, :8] = x_t
+        model_output = model(x_in, self._scale_timesteps(t), **model_kwargs)
+        mo = model_output.float().contiguous()
+        model_output_idwt = ops.idwt3d(mo.detach(), (V, 8 * V, 0, 1), B, 1, d, h, w, lll_mul3=True)
+        terms = {"mse_wav": th.mean(mean_flat((x_start_dwt - model_output) ** 2), dim=0)}
+        return terms, model_output, model_output_idwt
+
+
+def _native_unet(model):
+    from .unet import UNetModel
+    m = getattr(model, "model", model)   # unwrap respace._WrappedModel
+    return m if isinstance(m, UNetModel) else None
+
+
+def _extract_into_tensor(arr, timesteps, broadcast_shape):
+    """Reference :1246-1263 (same IndexError contract)."""
+    if timesteps.min() < 0 or timesteps.max() >= len(arr):
+        raise IndexError(f"Timesteps out of bounds: min={timesteps.min().item()}, max={timesteps.max().item()}, "
+                         f"arr len={len(arr)}")
+    res = th.from_numpy(arr).to(device=timesteps.device)[timesteps].float()
+    while len(res.shape) < len(broadcast_shape):
+        res = res[..., None]
+    return res.expand(broadcast_shape)

@@ -1,0 +1,212 @@
+/*
+ * libcwdm -- MI355X (gfx950) native kernels for the conditional wavelet
+ * diffusion hot path: 3D Haar DWT -> 3D U-Net denoiser -> IDWT.
+ *
+ * C ABI only: plain pointers (device memory unless noted), int64 sizes and
+ * strides in ELEMENTS, an optional hipStream_t.  No torch types.  The caller
+ * owns every buffer (outputs, packed weights, workspace); no entry point
+ * allocates device memory or synchronises, so every launch is legal inside
+ * hipGraph stream capture.
+ *
+ * Return value: CWDM_OK (0) or a negative CWDM_E_* code; the message is in
+ * cwdm_last_error() (thread-local).
+ *
+ * Reference interfaces each entry point replaces are cited per declaration
+ * (paths relative to tsereda/fast-cwdm).  The reference has no FFI; its seams
+ * are Python objects, which fast-cwdm_amd/ re-exposes with
+ * the reference signatures on top of this header.
+ */
+#ifndef CWDM_H_
+#define CWDM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* cwdm_stream_t; /* == hipStream_t; NULL = default stream */
+
+enum { CWDM_F32 = 0, CWDM_BF16 = 1 };
+
+enum {
+  CWDM_OK = 0,
+  CWDM_E_INVALID = -1,     /* bad argument (maps to AssertionError/ValueError) */
+  CWDM_E_SHAPE = -2,       /* shape mismatch (AssertionError in the reference) */
+  CWDM_E_HIP = -3,         /* HIP runtime error (launch) */
+  CWDM_E_WORKSPACE = -4,   /* workspace too small */
+  CWDM_E_INDEX = -5,       /* timestep out of range (IndexError in the reference) */
+  CWDM_E_UNSUPPORTED = -6  /* configuration this build does not cover */
+};
+
+int cwdm_version(void);
+const char* cwdm_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Haar wavelets.
+ *
+ * cwdm_haar_dwt3d replaces DWT_3D('haar').forward + DWTFunction_3D.forward
+ *   (DWT_IDWT/DWT_IDWT_layer.py:520-531, DWT_IDWT/DWT_IDWT_Functions.py:117-136).
+ *   x: fp32 contiguous NCDHW (B, C, D, H, W), D/H/W even.
+ *   out: band k (order LLL, LLH, LHL, LHH, HLL, HLH, HHL, HHH; letters index
+ *   D, H, W) of (b, c, voxel v = (z*h + y)*w + x) is written at
+ *   out + k*s[0] + b*s[1] + c*s[2] + v*s[3], in out_dtype.
+ *   lll_div3 != 0 divides LLL by 3 (the `LLL / 3.` of
+ *   guided_diffusion/gaussian_diffusion.py:1132,1140).
+ *
+ * cwdm_haar_idwt3d replaces IDWT_3D('haar').forward + IDWTFunction_3D.forward
+ *   (DWT_IDWT/DWT_IDWT_layer.py:624-646, DWT_IDWT/DWT_IDWT_Functions.py:161-181);
+ *   same band addressing on the input, fp32 contiguous NCDHW output.
+ *   lll_mul3 multiplies LLL by 3 first (scripts/sample.py:113), clamp01 clamps
+ *   the image to [0, 1] (guided_diffusion/gaussian_diffusion.py:351).
+ *   It is also the exact adjoint of the DWT, i.e. DWTFunction_3D.backward
+ *   (DWT_IDWT_Functions.py:138-156), and vice versa (:183-208).
+ * ------------------------------------------------------------------------- */
+int cwdm_haar_dwt3d(const float* x, int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
+                    void* out, int out_dtype, const int64_t* out_strides /* [4] host */,
+                    int lll_div3, cwdm_stream_t stream);
+int cwdm_haar_idwt3d(const void* bands, int in_dtype, const int64_t* in_strides /* [4] host */,
+                     int64_t B, int64_t C, int64_t d, int64_t h, int64_t w,
+                     float* x, int lll_mul3, int clamp01, cwdm_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused sampler step: replaces the tail of GaussianDiffusion.p_sample after
+ * the model call (and EPSILON's _predict_xstart_from_eps, :390-397) -- process_xstart (IDWT(LLL*3) -> clamp(0,1) -> DWT ->
+ * LLL/3), q_posterior_mean_variance and the noise add
+ * (guided_diffusion/gaussian_diffusion.py:335-354, :244-267, :565-573),
+ * with FIXED_LARGE variance and START_X prediction.  All 3-element stride
+ * arrays are (batch, subband channel, voxel) in elements; voxel index
+ * v = (z*h + y)*w + x over the subband grid.  coef is a device table
+ * [T][8] = {posterior_mean_coef1, posterior_mean_coef2,
+ * exp(0.5*log_variance), sqrt_recip_alphas_cumprod,
+ * sqrt_recipm1_alphas_cumprod, 0, 0, 0} in fp32 ([T][8]); t is a device
+ * int64[B] of (spaced) timestep indices.  Out-of-range t values cannot raise on device: callers
+ * validate t on the host (the reference raises IndexError in
+ * _extract_into_tensor, :1257-1259).  noise == NULL returns the posterior
+ * mean (p_mean_variance's "mean") instead of a sample.
+ * x_prev may alias x_t.  mirror (optional) receives a second copy of x_prev,
+ * e.g. the first 8 channels of the NDHWC U-Net input buffer.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  const float* model_out; int64_t mo_s[3];
+  const float* x_t;       int64_t xt_s[3];
+  float* x_prev;          int64_t xp_s[3];
+  const float* noise;     int64_t nz_s[3];
+  float* pred_xstart;     int64_t px_s[3];
+  void* mirror; int mirror_dtype; int64_t mr_s[3];
+  const float* coef;
+  const int64_t* t;
+  int64_t T, B, d, h, w;
+  int clip_denoised;
+  int mean_type;        /* 0 START_X (model predicts x0), 1 EPSILON */
+} cwdm_sampler_args;
+int cwdm_sampler_step(const cwdm_sampler_args* args, cwdm_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Strided 3-index copy with dtype conversion, (b, c, v) -> (b, c, v).  Used
+ * for NCDHW <-> NDHWC moves at the model seam (the reference's
+ * `th.cat([x, cond], dim=1)`, guided_diffusion/gaussian_diffusion.py:296-297,
+ * writes straight into the U-Net's channels-last input).
+ * ------------------------------------------------------------------------- */
+int cwdm_copy3(const void* src, int src_dtype, const int64_t* src_s /* [3] */,
+               void* dst, int dst_dtype, const int64_t* dst_s /* [3] */,
+               int64_t B, int64_t C, int64_t V, cwdm_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Conv3d implicit GEMM on MFMA (replaces nn.Conv3d inside conv_nd,
+ * guided_diffusion/nn.py:22-32, instances at guided_diffusion/unet.py:231,260,
+ * 268/271,547,724) with the ResBlock fusions of unet.py:285-311:
+ *   out = conv3x3x3( resample_A( SiLU(GN(a)) | a ) ) [+ conv1x1(b)]
+ *         + bias[b][c] [+ resample_R(res)]
+ * Activations are channels-last NDHWC in dtype; `a` may be the channel concat
+ * of two tensors (a0: a_c0 channels, then a1: a_c1 channels) -- the decoder's
+ * `th.cat([h, hs.pop()], 1)` (unet.py:796) without the copy.
+ * a_mode/res_mode: 0 same resolution, 1 nearest x2 upsample of a low-res source
+ * (Upsample, unet.py:40-70), 2 AvgPool 2x2x2 of a high-res source
+ * (Downsample, unet.py:73-100); res_mode additionally uses -1 = none.
+ * a_gn: NULL or device [B][a_c0+a_c1][2] fp32 (scale, shift) from
+ * cwdm_gn_finalize: GroupNorm32 + SiLU (nn.py:17-19, unet.py:225-229).
+ * stats: NULL or device [B][parts][cout][2] fp32 per-tile (sum, sum^2) of the
+ * stored output, for the next GroupNorm (parts from cwdm_conv3d_parts).
+ * Weights are packed once by cwdm_conv3d_pack from PyTorch OIDHW fp32.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  int dtype;
+  int64_t B, D, H, W;   /* output grid */
+  int cout;
+  const void* a0; int a_c0;
+  const void* a1; int a_c1;
+  int a_mode;
+  const float* a_gn;
+  const void* a_w;
+  const void* b0; int b_c0;   /* optional 1x1 segment (skip_connection conv) */
+  const void* b1; int b_c1;
+  const void* b_w;
+  const float* bias; int64_t bias_bstride; /* fp32 [cout] (bstride 0) or [B][bstride] */
+  const void* res; int res_mode;
+  void* out; int out_dtype;
+  float* stats;
+} cwdm_conv3d_desc;
+int64_t cwdm_conv3d_packed_bytes(int cout, int cin, int ksize, int dtype);
+int cwdm_conv3d_pack(const float* w_oidhw, int cout, int cin, int ksize, int dtype,
+                     void* packed, cwdm_stream_t stream);
+int64_t cwdm_conv3d_parts(int dtype, int64_t D, int64_t H, int64_t W, int cout);
+int cwdm_conv3d_forward(const cwdm_conv3d_desc* desc, cwdm_stream_t stream);
+
+/* GroupNorm statistics -> per-channel (scale, shift) for the consumer conv's
+ * prologue.  Channels are the concat of source 0 (c0) and source 1 (c1), each
+ * with per-tile partials from cwdm_conv3d_forward.  torch.nn.GroupNorm
+ * semantics (biased variance, eps inside the sqrt, affine). */
+int cwdm_gn_finalize(const float* stats0, int64_t parts0, int c0,
+                     const float* stats1, int64_t parts1, int c1,
+                     const float* gamma, const float* beta, int groups,
+                     int64_t B, int64_t voxels, float eps,
+                     float* scale_shift, cwdm_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * U-Net plan: the whole UNetModel.forward (guided_diffusion/unet.py:754-800)
+ * for the run.sh configuration family (no attention, resblock_updown=True,
+ * use_scale_shift_norm=False, additive_skips=False, resample_2d=False, dims=3).
+ * Topology and parameter names/shapes follow UNetModel.__init__
+ * (unet.py:482-725) so reference state_dicts load unchanged.
+ * ------------------------------------------------------------------------- */
+typedef struct cwdm_unet cwdm_unet;
+typedef struct {
+  int in_channels, model_channels, out_channels, num_res_blocks;
+  int num_levels;
+  int channel_mult[8];
+  int num_groups;
+  int dtype;          /* storage/compute dtype of activations and weights */
+} cwdm_unet_config;
+
+int cwdm_unet_create(const cwdm_unet_config* cfg, cwdm_unet** plan);
+void cwdm_unet_destroy(cwdm_unet* plan);
+int cwdm_unet_num_params(const cwdm_unet* plan);
+int cwdm_unet_param_info(const cwdm_unet* plan, int i, char* name, int name_cap,
+                         int64_t* shape /* [5] */, int* ndim);
+int64_t cwdm_unet_packed_bytes(const cwdm_unet* plan);
+/* params: host array of device pointers to fp32 contiguous tensors, state_dict order */
+int cwdm_unet_pack(const cwdm_unet* plan, const float* const* params, void* packed,
+                   cwdm_stream_t stream);
+int64_t cwdm_unet_workspace_bytes(const cwdm_unet* plan, int64_t B, int64_t D, int64_t H, int64_t W);
+/* x: NDHWC (B, D, H, W, in_channels) in plan dtype; t: device fp32[B] model timesteps;
+ * out: NDHWC fp32 (B, D, H, W, out_channels). */
+int cwdm_unet_forward(cwdm_unet* plan, const void* packed, const void* x, const float* t,
+                      float* out, int64_t B, int64_t D, int64_t H, int64_t W,
+                      void* workspace, int64_t ws_bytes, cwdm_stream_t stream);
+/* Block outputs kept in the workspace after a forward (one per entry of the
+ * topology), for layer-level parity tests. */
+int cwdm_unet_trace_count(const cwdm_unet* plan);
+int cwdm_unet_trace_info(const cwdm_unet* plan, int i, int64_t B, int64_t D, int64_t H, int64_t W,
+                         int64_t* ws_offset, int* channels, int* level);
+/* Conv FLOPs (2*MAC) of one forward at this grid. */
+double cwdm_unet_flops(const cwdm_unet* plan, int64_t B, int64_t D, int64_t H, int64_t W);
+/* Optional per-conv hipEvent timing (profiling only; adds events to the stream). */
+int cwdm_unet_set_profiling(cwdm_unet* plan, int on);
+int cwdm_unet_profile_read(cwdm_unet* plan, double* conv_ms, double* conv_flops, int* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CWDM_H_ */

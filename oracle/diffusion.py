@@ -1,0 +1,190 @@
+"""Oracle: DDPM tables, respacing and the i2i sampler/trainer math (TEST INFRASTRUCTURE ONLY).
+
+Restates guided_diffusion/gaussian_diffusion.py and respace.py of the reference:
+schedules (:30-67), coefficient tables (:143-205), q_sample (:224-242),
+q_posterior_mean_variance (:244-267), p_mean_variance in i2i mode with the
+IDWT -> clamp -> DWT projection (:269-388), p_sample (:529-574),
+p_sample_loop_progressive (:668-719), training_losses i2i (:1084-1166),
+_extract_into_tensor (:1246-1263); space_timesteps / SpacedDiffusion /
+_WrappedModel (respace.py:7-132).
+
+Randomness is injected: every function that the reference feeds from
+``th.randn_like`` takes the noise as an argument instead, so GPU and CPU runs
+can be compared on identical inputs.
+"""
+import numpy as np
+import torch
+
+from . import haar
+
+
+def beta_schedule(name, T, sample_schedule="direct"):
+    """get_named_beta_schedule (gaussian_diffusion.py:30-67), linear branch."""
+    if name != "linear":
+        raise NotImplementedError(f"unknown beta schedule: {name}")
+    if sample_schedule == "direct":
+        s = 1000.0 / T
+        return np.linspace(s * 0.0001, s * 0.02, T, dtype=np.float64)
+    if sample_schedule == "sampled":
+        full = np.linspace(0.0001, 0.02, 1000, dtype=np.float64)
+        acp = np.cumprod(1.0 - full)
+        idx = np.linspace(0, 999, T, dtype=int)
+        s_acp = acp[idx]
+        prev = np.concatenate([[1.0], s_acp[:-1]])
+        return np.clip(1.0 - s_acp / prev, 0.0001, 0.999)
+    raise NotImplementedError(f"Unknown sample_schedule: {sample_schedule}")
+
+
+def space_timesteps(T, section_counts):
+    """respace.py:7-62."""
+    if isinstance(section_counts, str):
+        if section_counts.startswith("ddim"):
+            want = int(section_counts[4:])
+            for stride in range(1, T):
+                if len(range(0, T, stride)) == want:
+                    return set(range(0, T, stride))
+            raise ValueError(f"cannot create exactly {T} steps with an integer stride")
+        section_counts = [int(v) for v in section_counts.split(",")]
+    per, extra = divmod(T, len(section_counts))
+    start, steps = 0, []
+    for i, cnt in enumerate(section_counts):
+        size = per + (1 if i < extra else 0)
+        if size < cnt:
+            raise ValueError(f"cannot divide section of {size} steps into {cnt}")
+        stride = 1 if cnt <= 1 else (size - 1) / (cnt - 1)
+        cur = 0.0
+        for _ in range(cnt):
+            steps.append(start + round(cur))
+            cur += stride
+        start += size
+    return set(steps)
+
+
+class Tables:
+    """GaussianDiffusion.__init__ float64 tables (gaussian_diffusion.py:143-205)
+    after SpacedDiffusion's beta recomputation (respace.py:74-88)."""
+
+    def __init__(self, betas, use_timesteps=None):
+        betas = np.asarray(betas, dtype=np.float64)
+        self.original_num_steps = len(betas)
+        if use_timesteps is None:
+            use_timesteps = range(len(betas))
+        use = set(use_timesteps)
+        acp_base = np.cumprod(1.0 - betas)
+        last, nb, tmap = 1.0, [], []
+        for i, a in enumerate(acp_base):
+            if i in use:
+                nb.append(1.0 - a / last)
+                last = a
+                tmap.append(i)
+        betas = np.array(nb, dtype=np.float64)
+        assert betas.ndim == 1 and (betas > 0).all() and (betas <= 1).all()
+        self.timestep_map = tmap
+        self.betas = betas
+        self.num_timesteps = len(betas)
+        alphas = 1.0 - betas
+        self.alphas_cumprod = np.cumprod(alphas)
+        self.alphas_cumprod_prev = np.append(1.0, self.alphas_cumprod[:-1])
+        self.alphas_cumprod_next = np.append(self.alphas_cumprod[1:], 0.0)
+        self.sqrt_alphas_cumprod = np.sqrt(self.alphas_cumprod)
+        self.sqrt_one_minus_alphas_cumprod = np.sqrt(1.0 - self.alphas_cumprod)
+        self.log_one_minus_alphas_cumprod = np.log(1.0 - self.alphas_cumprod)
+        self.sqrt_recip_alphas_cumprod = np.sqrt(1.0 / self.alphas_cumprod)
+        self.sqrt_recipm1_alphas_cumprod = np.sqrt(1.0 / self.alphas_cumprod - 1)
+        self.posterior_variance = betas * (1.0 - self.alphas_cumprod_prev) / (1.0 - self.alphas_cumprod)
+        self.posterior_log_variance_clipped = np.log(
+            np.append(self.posterior_variance[1], self.posterior_variance[1:]))
+        self.posterior_mean_coef1 = betas * np.sqrt(self.alphas_cumprod_prev) / (1.0 - self.alphas_cumprod)
+        self.posterior_mean_coef2 = (1.0 - self.alphas_cumprod_prev) * np.sqrt(alphas) / (1.0 - self.alphas_cumprod)
+        # FIXED_LARGE variance (gaussian_diffusion.py:320-333)
+        self.fixed_large_variance = np.append(self.posterior_variance[1], self.betas[1:])
+        self.fixed_large_log_variance = np.log(self.fixed_large_variance)
+
+
+def extract(arr, t, shape):
+    """_extract_into_tensor (gaussian_diffusion.py:1246-1263)."""
+    if t.min() < 0 or t.max() >= len(arr):
+        raise IndexError(f"Timesteps out of bounds: min={int(t.min())}, max={int(t.max())}, arr len={len(arr)}")
+    res = torch.from_numpy(arr)[t].float()
+    while res.dim() < len(shape):
+        res = res[..., None]
+    return res.expand(shape)
+
+
+def q_sample(tab, x0, t, noise):
+    return extract(tab.sqrt_alphas_cumprod, t, x0.shape) * x0 + \
+        extract(tab.sqrt_one_minus_alphas_cumprod, t, x0.shape) * noise
+
+
+def process_xstart(x):
+    """IDWT(LLL*3) -> clamp(0,1) -> DWT -> LLL/3 (gaussian_diffusion.py:335-354)."""
+    img = haar.idwt_split(x).clamp(0.0, 1.0)
+    return haar.dwt_cat(img)
+
+
+def p_mean_variance(tab, model, x, t, cond, clip_denoised=True):
+    """i2i branch with START_X and FIXED_LARGE (gaussian_diffusion.py:269-388)."""
+    B = x.shape[0]
+    assert t.shape == (B,)
+    x_cond = torch.cat([x, cond], dim=1)
+    model_t = torch.tensor(tab.timestep_map, dtype=t.dtype)[t]   # respace.py:127-132
+    out = model(x_cond, model_t)
+    var = extract(tab.fixed_large_variance, t, x.shape)
+    logvar = extract(tab.fixed_large_log_variance, t, x.shape)
+    pred = process_xstart(out) if clip_denoised else out
+    mean = extract(tab.posterior_mean_coef1, t, x.shape) * pred + \
+        extract(tab.posterior_mean_coef2, t, x.shape) * x[:, :8]
+    return {"mean": mean, "variance": var, "log_variance": logvar, "pred_xstart": pred, "model_output": out}
+
+
+def p_sample(tab, model, x, t, cond, noise, clip_denoised=True):
+    """gaussian_diffusion.py:529-574 with the step noise passed in."""
+    out = p_mean_variance(tab, model, x, t, cond, clip_denoised)
+    mask = (t != 0).float().view(-1, *([1] * (x.dim() - 1)))
+    sample = out["mean"] + mask * torch.exp(0.5 * out["log_variance"]) * noise
+    return {"sample": sample, "pred_xstart": out["pred_xstart"], "model_output": out["model_output"]}
+
+
+def p_sample_loop(tab, model, x_T, cond, step_noises, time=None, clip_denoised=True):
+    """p_sample_loop_progressive (gaussian_diffusion.py:668-719); ``time``
+    defaults to num_timesteps (the reference's default of 1000 only works
+    for T=1000)."""
+    time = tab.num_timesteps if time is None else time
+    img = x_T
+    for k, i in enumerate(range(time - 1, -1, -1)):
+        t = torch.full((x_T.shape[0],), i, dtype=torch.int64)
+        img = p_sample(tab, model, img, t, cond, step_noises[k], clip_denoised)["sample"]
+    return img
+
+
+def training_losses(tab, model, x_start, t, noise_img, contr="t1n"):
+    """i2i training_losses (gaussian_diffusion.py:1084-1166); returns
+    (terms, model_output, model_output_idwt)."""
+    order = {"t1n": ("t1n", "t1c", "t2w", "t2f"), "t1c": ("t1c", "t1n", "t2w", "t2f"),
+             "t2w": ("t2w", "t1n", "t1c", "t2f"), "t2f": ("t2f", "t1n", "t1c", "t2w")}[contr]
+    target = x_start[order[0]]
+    cond = torch.cat([haar.dwt_cat(x_start[k]) for k in order[1:]], dim=1)
+    x0 = haar.dwt_cat(target)
+    eps = torch.cat(list(haar.dwt3d(noise_img)), dim=1)
+    x_t = q_sample(tab, x0, t, eps)
+    model_t = torch.tensor(tab.timestep_map, dtype=t.dtype)[t]
+    out = model(torch.cat([x_t, cond], dim=1), model_t)
+    out_idwt = haar.idwt_split(out)
+    mse = ((x0 - out) ** 2).mean(dim=list(range(2, out.dim()))).mean(dim=0)
+    return {"mse_wav": mse}, out, out_idwt
+
+
+def ddim_sample(tab, model, x, t, cond, clip_denoised=True, eta=0.0):
+    """Spec-defined i2i DDIM step (the reference raises for
+    i2i).  Follows ddim_sample's formulas (gaussian_diffusion.py:721-784) with
+    the i2i conditioning of p_mean_variance; returns mean_pred like the
+    reference does (:784).  Parity unpinned against the reference."""
+    out = p_mean_variance(tab, model, x, t, cond, clip_denoised)
+    shape = x.shape
+    eps = (extract(tab.sqrt_recip_alphas_cumprod, t, shape) * x - out["pred_xstart"]) / \
+        extract(tab.sqrt_recipm1_alphas_cumprod, t, shape)
+    ab = extract(tab.alphas_cumprod, t, shape)
+    abp = extract(tab.alphas_cumprod_prev, t, shape)
+    sigma = eta * ((1 - abp) / (1 - ab)) ** 0.5 * (1 - ab / abp) ** 0.5
+    mean_pred = out["pred_xstart"] * abp ** 0.5 + (1 - abp - sigma ** 2) ** 0.5 * eps
+    return {"sample": mean_pred, "pred_xstart": out["pred_xstart"]}

@@ -1,0 +1,84 @@
+"""C-ABI library: loads without a GPU, exports every declared symbol, and its
+U-Net plan agrees with the oracle on names/shapes/FLOPs (no compute calls)."""
+import ctypes
+import math
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+from oracle import unet as ou
+
+
+def _header_functions():
+    text = open(os.path.join(ROOT, "include", "cwdm.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b(cwdm_[a-z0-9_]+)\s*\(", text)
+    return sorted(set(names))
+
+
+def test_library_exports_every_header_symbol():
+    from cwdm_hip import _lib
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    names = _header_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(names) == set(_lib.EXPORTED), set(names) ^ set(_lib.EXPORTED)
+
+
+def test_version_and_error_channel():
+    from cwdm_hip import _lib
+    L = _lib.lib()
+    assert L.cwdm_version() >= 1000
+    rc = L.cwdm_unet_param_info(None, 0, None, 0, None, None)
+    assert rc == _lib.E_INVALID
+    assert b"bad index" in L.cwdm_last_error()
+
+
+CFGS = [
+    dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4)),
+    dict(in_channels=32, model_channels=32, out_channels=8, num_res_blocks=1, channel_mult=(1, 2)),
+    dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=1, channel_mult=(1, 2, 4)),
+]
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_plan_param_contract_matches_oracle(cfg, dtype):
+    from cwdm_hip.unet_runtime import UNetPlan
+    plan = UNetPlan(cfg["in_channels"], cfg["model_channels"], cfg["out_channels"], cfg["num_res_blocks"],
+                    cfg["channel_mult"], 32 if cfg["model_channels"] >= 64 else 8, dtype)
+    want = ou.param_shapes(**cfg)
+    got = plan.param_specs
+    assert [n for n, _ in got] == [n for n, _ in want]
+    assert [tuple(s) for _, s in got] == [tuple(s) for _, s in want]
+    assert plan.packed_bytes > 0
+
+
+def test_production_param_count_and_flops():
+    from cwdm_hip.unet_runtime import UNetPlan
+    plan = UNetPlan(32, 64, 8, 2, (1, 2, 2, 4, 4), 32, "bf16")
+    n = sum(math.prod(s) for _, s in plan.param_specs)
+    assert n == 81_511_048
+    f = plan.flops(1, 128, 128, 128)
+    assert abs(f / 1e12 - 14.98) < 0.01
+    assert abs(plan.flops(1, 112, 112, 80) / 1e12 - 7.17) < 0.01
+    ws = plan.workspace_bytes(1, 128, 128, 128)
+    assert 1e9 < ws < 40e9
+
+
+def test_grid_divisibility_check():
+    from cwdm_hip.unet_runtime import UNetPlan
+    plan = UNetPlan(32, 64, 8, 2, (1, 2, 2, 4, 4), 32, "fp32")
+    with pytest.raises(AssertionError):
+        plan.check_grid(24, 32, 32)
+
+
+def test_conv_pack_sizes():
+    from cwdm_hip import _lib
+    L = _lib.lib()
+    assert L.cwdm_conv3d_packed_bytes(64, 64, 3, _lib.CWDM_BF16) == 27 * 64 * 64 * 2
+    assert L.cwdm_conv3d_packed_bytes(8, 64, 3, _lib.CWDM_F32) == 27 * 32 * 64 * 4   # cout padded to 32
+    assert L.cwdm_conv3d_packed_bytes(64, 24, 3, _lib.CWDM_BF16) == -1              # 24 % 16 != 0

@@ -1,0 +1,256 @@
+"""Kernel-level parity on the GPU (libcwdm through the C ABI) against the
+oracle / plain PyTorch-CPU fp32 references of the same op."""
+import ctypes
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import haar
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+# --------------------------------------------------------------------------- wavelets
+@pytest.mark.parametrize("shape", [(1, 1, 2, 2, 2), (2, 3, 8, 12, 10), (1, 1, 64, 64, 64), (2, 1, 18, 6, 4)])
+def test_dwt_idwt_bitexact_vs_oracle(shape):
+    from cwdm_hip import ops
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(shape, generator=g)
+    bands = ops.dwt3d(x.to(DEV)).cpu()
+    ref = haar.dwt3d(x)
+    for k in range(8):
+        assert torch.equal(bands[k], ref[k]), k
+    B, C, D, H, W = shape
+    v = (D // 2) * (H // 2) * (W // 2)
+    rec = ops.idwt3d(bands.to(DEV).contiguous(), (B * C * v, C * v, v, 1), B, C, D // 2, H // 2, W // 2).cpu()
+    assert torch.equal(rec, haar.idwt3d(*ref))
+    assert (rec - x).abs().max() < 1e-5
+
+
+def test_dwt_module_api_and_autograd():
+    from DWT_IDWT.DWT_IDWT_layer import DWT_3D, IDWT_3D
+    x = torch.rand(2, 1, 8, 8, 8, device=DEV, requires_grad=True)
+    bands = DWT_3D("haar")(x)
+    assert len(bands) == 8 and bands[0].shape == (2, 1, 4, 4, 4)
+    y = [torch.randn_like(b) for b in bands]
+    loss = sum((b * yy).sum() for b, yy in zip(bands, y))
+    loss.backward()
+    adj = IDWT_3D("haar")(*y)           # adjoint == inverse for Haar
+    assert torch.allclose(x.grad, adj, atol=1e-5)
+    ref = haar.dwt3d_matrix(x.detach().cpu())
+    for b, r in zip(bands, ref):
+        assert torch.allclose(b.detach().cpu(), r, atol=1e-6)
+
+
+def test_dwt_bf16_and_strided_output_into_channel_slice():
+    from cwdm_hip import ops
+    x = torch.rand(2, 1, 16, 16, 16)
+    V = 8 ** 3
+    buf = torch.zeros(2, 32, 8, 8, 8, device=DEV)
+    ops.dwt3d(x.to(DEV), lll_div3=True, out=buf[:, 8:], out_strides=(V, 32 * V, 0, 1))
+    ref = haar.dwt_cat(x)
+    assert torch.equal(buf[:, 8:16].cpu(), ref)
+    assert torch.count_nonzero(buf[:, :8]) == 0 and torch.count_nonzero(buf[:, 16:]) == 0
+    out = torch.empty(8, 2, 1, 8, 8, 8, device=DEV, dtype=torch.bfloat16)
+    ops.dwt3d(x.to(DEV), out=out, out_strides=(2 * V, V, V, 1))
+    refb = torch.stack(haar.dwt3d(x), 0).to(torch.bfloat16)
+    assert torch.equal(out.cpu(), refb)
+
+
+# --------------------------------------------------------------------------- sampler
+@pytest.mark.parametrize("clip", [True, False])
+@pytest.mark.parametrize("mean_type", [0, 1])
+def test_sampler_step_vs_oracle(clip, mean_type):
+    from oracle import diffusion as od
+    from guided_diffusion import script_util
+    d = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=(mean_type == 0), mode="i2i")
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"))
+    g = torch.Generator().manual_seed(1)
+    B, n = 3, 6
+    mo = torch.randn(B, 8, n, n, n, generator=g) * 0.5
+    x = torch.randn(B, 8, n, n, n, generator=g)
+    noise = torch.randn(B, 8, n, n, n, generator=g)
+    t = torch.tensor([0, 17, 999])
+    sample, pred = d._epilogue(mo.to(DEV), x.to(DEV), t.to(DEV), clip, None, noise.to(DEV))
+    if mean_type == 0:
+        x0 = mo
+    else:
+        x0 = od.extract(tab.sqrt_recip_alphas_cumprod, t, x.shape) * x - \
+            od.extract(tab.sqrt_recipm1_alphas_cumprod, t, x.shape) * mo
+    pref = od.process_xstart(x0) if clip else x0
+    mean = od.extract(tab.posterior_mean_coef1, t, x.shape) * pref + od.extract(tab.posterior_mean_coef2, t, x.shape) * x
+    mask = (t != 0).float().view(-1, 1, 1, 1, 1)
+    sref = mean + mask * torch.exp(0.5 * od.extract(tab.fixed_large_log_variance, t, x.shape)) * noise
+    assert rel_err(pred, pref) < 1e-6
+    assert rel_err(sample, sref) < 1e-6
+    assert torch.equal(sample[0].cpu(), mean[0]) or rel_err(sample[0], mean[0]) < 1e-6  # t = 0: no noise
+
+
+# --------------------------------------------------------------------------- conv3d
+def _conv_call(dtype, out_grid, a0, a1, amode, gn, w, bias, bvec_bstride=0, b0=None, b1=None, wb=None, res=None,
+               rmode=-1, out_f32=False, stats=True):
+    """Run cwdm_conv3d_forward on NDHWC tensors; returns (out, stats)."""
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import check, lib
+    B, D, H, W = out_grid
+    cout = w.shape[0]
+    tdt = torch.float32 if dtype == _lib.CWDM_F32 else torch.bfloat16
+    L = lib()
+
+    def pack(wt, k):
+        nbytes = L.cwdm_conv3d_packed_bytes(cout, wt.shape[1], k, dtype)
+        assert nbytes > 0
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+        check(L.cwdm_conv3d_pack(ctypes.c_void_p(wt.data_ptr()), cout, wt.shape[1], k, dtype,
+                                 ctypes.c_void_p(buf.data_ptr()), None))
+        return buf
+
+    pa = pack(w.to(DEV).contiguous(), 3)
+    pb = pack(wb.to(DEV).contiguous(), 1) if wb is not None else None
+    out = torch.empty(B, D, H, W, cout, device=DEV, dtype=torch.float32 if out_f32 else tdt)
+    parts = L.cwdm_conv3d_parts(dtype, D, H, W, cout)
+    st = torch.zeros(B, parts, cout, 2, device=DEV) if stats else None
+    d = _lib.ConvDesc()
+    d.dtype, d.B, d.D, d.H, d.W, d.cout = dtype, B, D, H, W, cout
+    d.a0, d.a_c0 = a0.data_ptr(), a0.shape[-1]
+    d.a1, d.a_c1 = (a1.data_ptr(), a1.shape[-1]) if a1 is not None else (None, 0)
+    d.a_mode = amode
+    d.a_gn = gn.data_ptr() if gn is not None else None
+    d.a_w = pa.data_ptr()
+    if wb is not None:
+        d.b0, d.b_c0 = b0.data_ptr(), b0.shape[-1]
+        d.b1, d.b_c1 = (b1.data_ptr(), b1.shape[-1]) if b1 is not None else (None, 0)
+        d.b_w = pb.data_ptr()
+    d.bias, d.bias_bstride = bias.data_ptr(), bvec_bstride
+    d.res, d.res_mode = (res.data_ptr() if res is not None else None), rmode
+    d.out, d.out_dtype = out.data_ptr(), (_lib.CWDM_F32 if out_f32 else dtype)
+    d.stats = st.data_ptr() if st is not None else None
+    check(L.cwdm_conv3d_forward(ctypes.byref(d), None))
+    torch.cuda.synchronize()
+    return out, st
+
+
+def _nd(x):  # NCDHW -> NDHWC
+    return x.permute(0, 2, 3, 4, 1).contiguous()
+
+
+def _nc(x):
+    return x.permute(0, 4, 1, 2, 3).contiguous()
+
+
+CASES = [
+    # name, B, grid(out), c0, c1, cout, amode, gn, skip1x1, rmode
+    ("plain", 1, (8, 16, 32), 32, 0, 64, 0, False, False, -1),
+    ("gn_concat_skip", 2, (8, 8, 16), 32, 16, 64, 0, True, True, -1),
+    ("down_pool_res", 1, (4, 8, 16), 64, 0, 64, 2, True, False, 2),
+    ("up_res", 1, (8, 16, 32), 32, 0, 32, 1, True, False, 1),
+    ("same_res", 1, (6, 10, 12), 64, 0, 64, 0, True, False, 0),
+    ("cout8", 2, (8, 8, 8), 64, 0, 8, 0, True, False, -1),
+    ("small_grid", 1, (4, 4, 4), 128, 128, 128, 0, True, True, -1),
+]
+
+
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_conv3d_fused_vs_torch(case, dtype_name):
+    from cwdm_hip import _lib
+    name, B, grid, c0, c1, cout, amode, use_gn, skip, rmode = case
+    dtype = _lib.CWDM_F32 if dtype_name == "fp32" else _lib.CWDM_BF16
+    tdt = torch.float32 if dtype_name == "fp32" else torch.bfloat16
+    g = torch.Generator().manual_seed(7)
+    D, H, W = grid
+    sD, sH, sW = {0: (D, H, W), 1: (D // 2, H // 2, W // 2), 2: (2 * D, 2 * H, 2 * W)}[amode]
+    cin = c0 + c1
+    a0 = torch.randn(B, c0, sD, sH, sW, generator=g)
+    a1 = torch.randn(B, c1, sD, sH, sW, generator=g) if c1 else None
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)
+    bias = torch.randn(cout, generator=g) * 0.1
+    x = torch.cat([a0, a1], 1) if c1 else a0
+    # quantise inputs to the compute dtype so both sides see the same operands
+    x = x.to(tdt).float()
+    a0q, a1q = x[:, :c0], (x[:, c0:] if c1 else None)
+    wq = w.to(tdt).float()
+    gn = None
+    if use_gn:
+        scale = 1 + 0.2 * torch.randn(B, cin, generator=g)
+        shift = 0.2 * torch.randn(B, cin, generator=g)
+        gn = torch.stack([scale, shift], -1).contiguous()
+        h = F.silu(x * scale[:, :, None, None, None] + shift[:, :, None, None, None])
+    else:
+        h = x
+    if amode == 2:
+        h = F.avg_pool3d(h, 2)
+    elif amode == 1:
+        h = F.interpolate(h, scale_factor=2, mode="nearest")
+    if dtype_name == "bf16":
+        h = h.to(tdt).float()   # the kernel stages the transformed halo in bf16
+    ref = F.conv3d(h, wq, bias, padding=1)
+    wb = b0 = b1 = None
+    if skip:
+        wb = torch.randn(cout, cin, 1, 1, 1, generator=g) / math.sqrt(cin)
+        ref = ref + F.conv3d(x, wb.to(tdt).float())
+        b0, b1 = a0q, a1q
+    res = None
+    if rmode >= 0:
+        rsh = {0: (D, H, W), 1: (D // 2, H // 2, W // 2), 2: (2 * D, 2 * H, 2 * W)}[rmode]
+        res = torch.randn(B, cout, *rsh, generator=g).to(tdt).float()
+        rr = {0: res, 1: F.interpolate(res, scale_factor=2, mode="nearest"), 2: F.avg_pool3d(res, 2)}[rmode]
+        ref = ref + rr
+    out, st = _conv_call(
+        dtype, (B, D, H, W), _nd(a0q).to(DEV, tdt), _nd(a1q).to(DEV, tdt) if c1 else None, amode,
+        gn.to(DEV) if gn is not None else None, wq.to(DEV), bias.to(DEV),
+        b0=_nd(b0).to(DEV, tdt) if skip else None, b1=_nd(b1).to(DEV, tdt) if (skip and c1) else None,
+        wb=wb.to(tdt).float().to(DEV) if skip else None, res=_nd(res).to(DEV, tdt) if res is not None else None,
+        rmode=rmode, out_f32=(cout == 8))
+    got = _nc(out.float().cpu())
+    tol = 2e-5 if dtype_name == "fp32" else 2e-2
+    assert rel_err(got, ref) < tol, name
+    # per-channel statistics of the stored (pre-rounding) output
+    s = st.sum(1).cpu()
+    ref_sum = ref.sum(dim=(2, 3, 4))
+    assert torch.allclose(s[..., 0], ref_sum, rtol=1e-3, atol=1e-2 * ref.abs().max().item() * 8)
+
+
+def test_gn_finalize_matches_group_norm():
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import check, lib
+    g = torch.Generator().manual_seed(3)
+    B, C0, C1, G = 2, 64, 32, 32
+    D = H = W = 8
+    x = torch.randn(B, C0 + C1, D, H, W, generator=g) * 2 + 0.5
+    # fake per-tile partials: split voxels into 4 parts
+    parts = 4
+    xv = x.view(B, C0 + C1, parts, -1)
+    st = torch.stack([xv.sum(-1), (xv ** 2).sum(-1)], -1).permute(0, 2, 1, 3).contiguous()  # B, P, C, 2
+    s0 = st[:, :, :C0].contiguous().to(DEV)
+    s1 = st[:, :, C0:].contiguous().to(DEV)
+    gamma = (1 + 0.1 * torch.randn(C0 + C1, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(C0 + C1, generator=g)).to(DEV)
+    out = torch.empty(B, C0 + C1, 2, device=DEV)
+    check(lib().cwdm_gn_finalize(ctypes.c_void_p(s0.data_ptr()), parts, C0, ctypes.c_void_p(s1.data_ptr()), parts, C1,
+                                 ctypes.c_void_p(gamma.data_ptr()), ctypes.c_void_p(beta.data_ptr()), G, B,
+                                 D * H * W, 1e-5, ctypes.c_void_p(out.data_ptr()), None))
+    o = out.cpu()
+    y = x * o[..., 0][:, :, None, None, None] + o[..., 1][:, :, None, None, None]
+    ref = F.group_norm(x, G, gamma.cpu(), beta.cpu(), eps=1e-5)
+    assert rel_err(y, ref) < 1e-5
+
+
+def test_copy3_layouts():
+    from cwdm_hip import ops
+    x = torch.randn(2, 24, 5, 6, 7, device=DEV)
+    V = 5 * 6 * 7
+    buf = torch.zeros(2, 5, 6, 7, 32, device=DEV, dtype=torch.bfloat16)
+    ops.copy3(x, (24 * V, V, 1), buf[..., 8:], (V * 32, 1, 32), 2, 24, V)
+    assert torch.equal(buf[..., 8:].float().cpu(), x.permute(0, 2, 3, 4, 1).to(torch.bfloat16).float().cpu())
+    back = torch.empty(2, 24, 5, 6, 7, device=DEV)
+    ops.copy3(buf[..., 8:], (V * 32, 1, 32), back, (24 * V, V, 1), 2, 24, V)
+    assert torch.equal(back.cpu(), x.to(torch.bfloat16).float().cpu())
