@@ -4,6 +4,9 @@
 // so results match the oracle's elementwise restatement bit for bit.
 #include "common.hpp"
 
+// Rounding must follow the reference stage by stage: no FMA contraction here.
+#pragma clang fp contract(off)
+
 namespace cwdm {
 
 namespace {
