@@ -40,6 +40,8 @@ struct ConvParams {
   const void* res; int rmode;
   void* out; int out_f32;
   float* stats;
+  int ksplit;       // K split factor S (1 = none)
+  float* partial;   // [S][B*D*H*W][cout] fp32 partial sums when S > 1
 };
 
 template <typename T> struct ConvTr;
@@ -97,176 +99,170 @@ struct ConvCfg {
   static_assert(BX * BY * BZ == 256, "brick must be 256 voxels");
 };
 
-// Stage one chunk of the halo (conv input) into LDS.
-template <typename T, int BX, int BY, int BZ>
-__device__ __forceinline__ void stage_halo(unsigned char* lds, const void* s0, int c0, const void* s1, int c1,
-                                           int mode, const float* gn, int ctot, int chunk, int b, int x0, int y0,
-                                           int z0, int D, int H, int W, int tid) {
-  constexpr int CK = ConvTr<T>::CK, EPQ = ConvTr<T>::EPQ;
-  constexpr int HX = BX + 2, HY = BY + 2, HV = HX * HY * (BZ + 2);
-  const int q = tid & 1;
-  const int cb = chunk * CK + q * EPQ;  // first concat channel of this thread's quad
-  const void* src;
-  int ch, csrc;
-  if (cb < c0) { src = s0; ch = cb; csrc = c0; }
-  else { src = s1; ch = cb - c0; csrc = c1; }
+// Chunk staging.  Halo (or, for the 1x1 segment, brick-interior) items are
+// (voxel, 16-byte quad) pairs, two threads per voxel.  fetch() issues every
+// global load of a chunk into registers (nothing waits), store() transforms
+// (GroupNorm scale/shift + SiLU, compile-time) and writes the swizzled LDS
+// image.  The main loop calls fetch(c+1) before the MFMAs of chunk c, so HBM
+// latency hides behind compute.  MODE: 0 same grid, 1 nearest-x2 upsample
+// (source at half resolution), 2 AvgPool2 (source at double resolution; no
+// prefetch: 8 loads per item are done inside store()).
+template <typename T, int BX, int BY, int BZ, int MODE, bool GN>
+struct Stager {
+  static constexpr int CK = ConvTr<T>::CK, EPQ = ConvTr<T>::EPQ;
+  static constexpr int HX = BX + 2, HY = BY + 2, HV = HX * HY * (BZ + 2);
+  static constexpr int NI = (HV + 127) / 128;
+  u32x4 r[NI];
+  unsigned ok;
   float sc[EPQ], sh[EPQ];
-  if (gn) {
-#pragma unroll
-    for (int e = 0; e < EPQ; ++e) {
-      sc[e] = gn[((long long)b * ctot + cb + e) * 2 + 0];
-      sh[e] = gn[((long long)b * ctot + cb + e) * 2 + 1];
-    }
+  const T* base;
+  int csrc;
+  bool seg_a;
+
+  __device__ __forceinline__ void coords(int it, bool interior, int* hv, int* hx, int* hy, int* hz) const {
+    if (interior) { *hx = it % BX + 1; *hy = (it / BX) % BY + 1; *hz = it / (BX * BY) + 1; }
+    else { *hx = it % HX; *hy = (it / HX) % HY; *hz = it / (HX * HY); }
+    *hv = (*hz * HY + *hy) * HX + *hx;
   }
-  // source grid dims
-  int SD = D, SH = H, SW = W;
-  if (mode == 1) { SD = D >> 1; SH = H >> 1; SW = W >> 1; }
-  else if (mode == 2) { SD = D << 1; SH = H << 1; SW = W << 1; }
-  const T* base = reinterpret_cast<const T*>(src) + ch;
-  for (int hv = tid >> 1; hv < HV; hv += 128) {
-    const int hx = hv % HX, hy = (hv / HX) % HY, hz = hv / (HX * HY);
-    const int ox = x0 + hx - 1, oy = y0 + hy - 1, oz = z0 + hz - 1;
-    float f[EPQ];
-    if (ox < 0 || oy < 0 || oz < 0 || ox >= W || oy >= H || oz >= D) {
+
+  __device__ __forceinline__ void fetch(const ConvParams& p, bool segA, int chunk, int b, int x0, int y0, int z0,
+                                        int tid) {
+    seg_a = segA;
+    const int q = tid & 1;
+    const int c0 = segA ? p.ac0 : p.bc0, c1 = segA ? p.ac1 : p.bc1;
+    const int cb = chunk * CK + q * EPQ;
+    const void* src;
+    int ch;
+    if (cb < c0) { src = segA ? p.a0 : p.b0; ch = cb; csrc = c0; }
+    else { src = segA ? p.a1 : p.b1; ch = cb - c0; csrc = c1; }
+    base = reinterpret_cast<const T*>(src) + ch;
+    if (GN && segA) {
+      const int ctot = c0 + c1;
 #pragma unroll
-      for (int e = 0; e < EPQ; ++e) f[e] = 0.f;
-    } else if (mode == 2) {
+      for (int e = 0; e < EPQ; ++e) {
+        sc[e] = p.agn[((long long)b * ctot + cb + e) * 2 + 0];
+        sh[e] = p.agn[((long long)b * ctot + cb + e) * 2 + 1];
+      }
+    }
+    ok = 0;
+    if (MODE == 2 && segA) return;
+    const bool interior = !segA;
+    const int n = interior ? BX * BY * BZ : HV;
+    const int md = segA ? MODE : 0;
+    const int SD = md == 1 ? p.D >> 1 : p.D, SH = md == 1 ? p.H >> 1 : p.H, SW = md == 1 ? p.W >> 1 : p.W;
 #pragma unroll
-      for (int e = 0; e < EPQ; ++e) f[e] = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int sz = 2 * oz + (k >> 2), sy = 2 * oy + ((k >> 1) & 1), sx = 2 * ox + (k & 1);
-        const long long vox = (((long long)b * SD + sz) * SH + sy) * SW + sx;
-        float g[EPQ];
-        unpack<T>(ldg16(base + vox * csrc), g);
-#pragma unroll
-        for (int e = 0; e < EPQ; ++e) {
-          float v = g[e];
-          if (gn) v = silu(v * sc[e] + sh[e]);
-          f[e] += v;
+    for (int j = 0; j < NI; ++j) {
+      const int it = (tid >> 1) + 128 * j;
+      r[j] = u32x4{0u, 0u, 0u, 0u};
+      if (it < n) {
+        int hv, hx, hy, hz;
+        coords(it, interior, &hv, &hx, &hy, &hz);
+        int ox = x0 + hx - 1, oy = y0 + hy - 1, oz = z0 + hz - 1;
+        if (ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) {
+          if (md == 1) { ox >>= 1; oy >>= 1; oz >>= 1; }
+          const long long vox = (((long long)b * SD + oz) * SH + oy) * SW + ox;
+          r[j] = ldg16(base + vox * csrc);
+          ok |= 1u << j;
         }
       }
+    }
+  }
+
+  // in-place GroupNorm+SiLU of the fetched registers (MODE 0/1 only)
+  __device__ __forceinline__ void transform() {
+    if (!(GN && seg_a) || MODE == 2) return;
 #pragma unroll
-      for (int e = 0; e < EPQ; ++e) f[e] *= 0.125f;
-    } else {
-      int sx = ox, sy = oy, sz = oz;
-      if (mode == 1) { sx >>= 1; sy >>= 1; sz >>= 1; }
-      const long long vox = (((long long)b * SD + sz) * SH + sy) * SW + sx;
-      unpack<T>(ldg16(base + vox * csrc), f);
-      if (gn) {
+    for (int j = 0; j < NI; ++j) {
+      if ((ok >> j) & 1) {
+        float f[EPQ];
+        unpack<T>(r[j], f);
 #pragma unroll
         for (int e = 0; e < EPQ; ++e) f[e] = silu(f[e] * sc[e] + sh[e]);
+        r[j] = pack<T>(f);
       }
     }
-    const int off = hv * 32 + ((q ^ ((hv >> 3) & 1)) << 4);
-    *reinterpret_cast<u32x4*>(lds + off) = pack<T>(f);
+  }
+
+  // write already-transformed registers; SWZ selects the XOR-swizzled image
+  template <bool SWZ>
+  __device__ __forceinline__ void write(unsigned char* lds, int tid) const {
+    const int q = tid & 1;
+    const bool interior = !seg_a;
+    const int n = interior ? BX * BY * BZ : HV;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int it = (tid >> 1) + 128 * j;
+      if (it < n) {
+        int hv, hx, hy, hz;
+        coords(it, interior, &hv, &hx, &hy, &hz);
+        const int off = SWZ ? hv * 32 + ((q ^ ((hv >> 3) & 1)) << 4) : hv * 32 + (q << 4);
+        *reinterpret_cast<u32x4*>(lds + off) = r[j];
+      }
+    }
+  }
+
+  template <bool SWZ>
+  __device__ __forceinline__ void store(unsigned char* lds, const ConvParams& p, int b, int x0, int y0, int z0,
+                                        int tid) const {
+    const int q = tid & 1;
+    const bool interior = !seg_a;
+    const int n = interior ? BX * BY * BZ : HV;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int it = (tid >> 1) + 128 * j;
+      if (it < n) {
+        int hv, hx, hy, hz;
+        coords(it, interior, &hv, &hx, &hy, &hz);
+        float f[EPQ];
+        if (MODE == 2 && seg_a) {
+#pragma unroll
+          for (int e = 0; e < EPQ; ++e) f[e] = 0.f;
+          const int ox = x0 + hx - 1, oy = y0 + hy - 1, oz = z0 + hz - 1;
+          if (ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) {
+            const int SD = p.D << 1, SH = p.H << 1, SW = p.W << 1;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const long long vox = (((long long)b * SD + 2 * oz + (k >> 2)) * SH + 2 * oy + ((k >> 1) & 1)) * SW +
+                                    2 * ox + (k & 1);
+              float g[EPQ];
+              unpack<T>(ldg16(base + vox * csrc), g);
+#pragma unroll
+              for (int e = 0; e < EPQ; ++e) f[e] += GN ? silu(g[e] * sc[e] + sh[e]) : g[e];
+            }
+#pragma unroll
+            for (int e = 0; e < EPQ; ++e) f[e] *= 0.125f;
+          }
+        } else {
+          unpack<T>(r[j], f);
+          if (GN && seg_a && ((ok >> j) & 1)) {
+#pragma unroll
+            for (int e = 0; e < EPQ; ++e) f[e] = silu(f[e] * sc[e] + sh[e]);
+          }
+        }
+        const int off = SWZ ? hv * 32 + ((q ^ ((hv >> 3) & 1)) << 4) : hv * 32 + (q << 4);
+        *reinterpret_cast<u32x4*>(lds + off) = pack<T>(f);
+      }
+    }
+  }
+};
+
+// weights of one chunk: a contiguous block of the packed layout copied
+// global -> LDS with LDS-DMA (no VGPRs; each wave instruction moves 1 KB).
+__device__ __forceinline__ void stage_weights(unsigned char* wl, const unsigned char* g, int bytes, int tid) {
+  const int wv = tid >> 6, lane = tid & 63;
+  for (int off = wv * 1024; off < bytes; off += 4096) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + off + lane * 16),
+                                     (__attribute__((address_space(3))) void*)(wl + off), 16, 0, 0);
   }
 }
 
-template <typename T, int BX, int BY, int BZ, int NF>
-__global__ void __launch_bounds__(256) conv3d_kernel(ConvParams p) {
-  using Cfg = ConvCfg<T, BX, BY, BZ, NF>;
-  constexpr int CK = ConvTr<T>::CK;
-  constexpr int HX = Cfg::HX, HY = Cfg::HY, NT = Cfg::NT;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[Cfg::SMEM];
-  unsigned char* halo = smem;
-  unsigned char* wl = smem + Cfg::HALO_B;
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 31, hh = lane >> 5;
-  const int ct = blockIdx.x % p.nct;
-  const int st = blockIdx.x / p.nct;
-  const int ix = st % p.tx, iy = (st / p.tx) % p.ty, iz = (st / (p.tx * p.ty)) % p.tz;
-  const int b = st / (p.tx * p.ty * p.tz);
-  const int x0 = ix * BX, y0 = iy * BY, z0 = iz * BZ;
-
-  int hbase[2];
-#pragma unroll
-  for (int mf = 0; mf < 2; ++mf) {
-    const int r = wv * 64 + mf * 32 + lr;
-    const int rx = r % BX, ry = (r / BX) % BY, rz = r / (BX * BY);
-    hbase[mf] = ((rz + 1) * HY + (ry + 1)) * HX + (rx + 1);
-  }
-
-  f32x16 acc[2][NF];
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < NF; ++n)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.f;
-
-  for (int seg = 0; seg < 2; ++seg) {
-    const void *s0, *s1, *wp;
-    int c0, c1, mode;
-    const float* gn;
-    int ntaps;
-    if (seg == 0) { s0 = p.a0; s1 = p.a1; c0 = p.ac0; c1 = p.ac1; mode = p.amode; gn = p.agn; wp = p.aw; ntaps = 27; }
-    else {
-      if (!p.bw) break;
-      s0 = p.b0; s1 = p.b1; c0 = p.bc0; c1 = p.bc1; mode = 0; gn = nullptr; wp = p.bw; ntaps = 1;
-    }
-    const int ctot = c0 + c1;
-    const int nchunks = ctot / CK;
-    for (int chunk = 0; chunk < nchunks; ++chunk) {
-      __syncthreads();
-      stage_halo<T, BX, BY, BZ>(halo, s0, c0, s1, c1, mode, gn, ctot, chunk, b, x0, y0, z0, p.D, p.H, p.W, tid);
-      {
-        const int nq = ntaps * NT * 2;
-        const unsigned char* g = reinterpret_cast<const unsigned char*>(wp) +
-                                 ((long long)ct * nchunks + chunk) * (long long)(ntaps * NT * 32);
-        for (int i = tid; i < nq; i += 256)
-          *reinterpret_cast<u32x4*>(wl + i * 16) = ldg16(g + (long long)i * 16);
-      }
-      __syncthreads();
-      for (int tap = 0; tap < ntaps; ++tap) {
-        int toff = 0;
-        if (ntaps == 27) {
-          const int dz = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dx = tap % 3 - 1;
-          toff = (dz * HY + dy) * HX + dx;
-        }
-        u32x4 bq[NF], aq[2];
-#pragma unroll
-        for (int n = 0; n < NF; ++n) {
-          const int row = n * 32 + lr;
-          bq[n] = *reinterpret_cast<const u32x4*>(wl + (tap * NT + row) * 32 + ((hh ^ ((row >> 3) & 1)) << 4));
-        }
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const int v = hbase[m] + toff;
-          aq[m] = *reinterpret_cast<const u32x4*>(halo + v * 32 + ((hh ^ ((v >> 3) & 1)) << 4));
-        }
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-          for (int n = 0; n < NF; ++n) {
-            if constexpr (sizeof(T) == 2) {
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, aq[m]),
-                                                                  __builtin_bit_cast(bf16x8, bq[n]), acc[m][n], 0, 0, 0);
-            } else {
-#pragma unroll
-              for (int s = 0; s < 4; ++s)
-                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(aq[m][s]), __uint_as_float(bq[n][s]),
-                                                                 acc[m][n], 0, 0, 0);
-            }
-          }
-      }
-    }
-  }
-
-  // ---------------- epilogue ----------------
-  __syncthreads();
-  float* E = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < NF; ++n)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = wv * 64 + m * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        E[row * Cfg::EPI_LD + n * 32 + lr] = acc[m][n][i];
-      }
-  __syncthreads();
-
+// Epilogue on one output tile held in LDS as fp32 E[ROWS][NT+4]: bias,
+// residual, store, GroupNorm partial statistics.
+template <typename T, int BX, int BY, int BZ, int NF, int ROWS>
+__device__ __forceinline__ void epilogue_rows(const ConvParams& p, float* E, int b, int st, int ct, int x0, int y0,
+                                              int z0, int tid) {
+  constexpr int NT = 32 * NF, LD = NT + 4;
+  static_assert(ROWS == BX * BY * BZ, "rows");
   constexpr int CG = NT / 8;  // 8-channel groups per row
   const int cg = tid % CG;
   const int cbase = ct * NT + cg * 8;
@@ -278,14 +274,14 @@ __global__ void __launch_bounds__(256) conv3d_kernel(ConvParams p) {
     bsq[e] = 0.f;
     bias[e] = (e < nvalid) ? p.bias[(long long)b * p.bias_bs + cbase + e] : 0.f;
   }
-  for (int u = tid; u < 256 * CG; u += 256) {
+  for (int u = tid; u < ROWS * CG; u += 256) {
     const int row = u / CG;
     const int rx = row % BX, ry = (row / BX) % BY, rz = row / (BX * BY);
     const int ox = x0 + rx, oy = y0 + ry, oz = z0 + rz;
     if (ox >= p.W || oy >= p.H || oz >= p.D || nvalid <= 0) continue;
     float v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = E[row * Cfg::EPI_LD + cg * 8 + e] + bias[e];
+    for (int e = 0; e < 8; ++e) v[e] = E[row * LD + cg * 8 + e] + bias[e];
     const long long vox = (((long long)b * p.D + oz) * p.H + oy) * p.W + ox;
     if (p.rmode >= 0) {
       const T* r = reinterpret_cast<const T*>(p.res);
@@ -306,7 +302,8 @@ __global__ void __launch_bounds__(256) conv3d_kernel(ConvParams p) {
         for (int e = 0; e < 8; ++e) rv[e] *= 0.125f;
       } else {
         long long rvx = vox;
-        if (p.rmode == 1) rvx = (((long long)b * (p.D >> 1) + (oz >> 1)) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1);
+        if (p.rmode == 1)
+          rvx = (((long long)b * (p.D >> 1) + (oz >> 1)) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (e < nvalid) rv[e] = Elem<T>::to_f(r[rvx * p.cout + cbase + e]);
@@ -337,7 +334,7 @@ __global__ void __launch_bounds__(256) conv3d_kernel(ConvParams p) {
   }
   if (p.stats) {
     __syncthreads();
-    float* R = reinterpret_cast<float*>(smem);
+    float* R = E;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       R[tid * 16 + e] = bsum[e];
@@ -360,6 +357,393 @@ __global__ void __launch_bounds__(256) conv3d_kernel(ConvParams p) {
       }
     }
   }
+}
+
+// split-K: raw fp32 partial tile -> workspace [ks][vox][cout]
+template <typename T, int BX, int BY, int BZ, int NF, int ROWS>
+__device__ __forceinline__ void write_partial(const ConvParams& p, const float* E, int ks, int b, int ct, int x0,
+                                              int y0, int z0, int tid) {
+  constexpr int NT = 32 * NF, LD = NT + 4, CG = NT / 8;
+  const long long nvox = (long long)p.B * p.D * p.H * p.W;
+  float* part = p.partial + (long long)ks * nvox * p.cout;
+  const int cg = tid % CG;
+  const int cbase = ct * NT + cg * 8;
+  const int nvalid = min(8, p.cout - cbase);
+  for (int u = tid; u < ROWS * CG; u += 256) {
+    const int row = u / CG;
+    const int rx = row % BX, ry = (row / BX) % BY, rz = row / (BX * BY);
+    const int ox = x0 + rx, oy = y0 + ry, oz = z0 + rz;
+    if (ox >= p.W || oy >= p.H || oz >= p.D || nvalid <= 0) continue;
+    const long long vox = (((long long)b * p.D + oz) * p.H + oy) * p.W + ox;
+    float* o = part + vox * p.cout + cbase;
+    if (nvalid == 8) {
+      *reinterpret_cast<float4*>(o) = *reinterpret_cast<const float4*>(E + row * LD + cg * 8);
+      *reinterpret_cast<float4*>(o + 4) = *reinterpret_cast<const float4*>(E + row * LD + cg * 8 + 4);
+    } else {
+      for (int e = 0; e < nvalid; ++e) o[e] = E[row * LD + cg * 8 + e];
+    }
+  }
+}
+
+template <typename T, int BX, int BY, int BZ>
+__device__ __forceinline__ void tile_origin(const ConvParams& p, int st, int* b, int* x0, int* y0, int* z0) {
+  const int ix = st % p.tx, iy = (st / p.tx) % p.ty, iz = (st / (p.tx * p.ty)) % p.tz;
+  *b = st / (p.tx * p.ty * p.tz);
+  *x0 = ix * BX;
+  *y0 = iy * BY;
+  *z0 = iz * BZ;
+}
+
+template <typename T, int BX, int BY, int BZ, int NF, int MODE, bool GN>
+__global__ void __launch_bounds__(256) conv3d_kernel(ConvParams p) {
+  using Cfg = ConvCfg<T, BX, BY, BZ, NF>;
+  constexpr int CK = ConvTr<T>::CK;
+  constexpr int HX = Cfg::HX, HY = Cfg::HY, NT = Cfg::NT;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[Cfg::SMEM];
+  unsigned char* halo = smem;
+  unsigned char* wl = smem + Cfg::HALO_B;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 31, hh = lane >> 5;
+  const int S = p.ksplit;
+  const int ks = blockIdx.x % S;
+  const int rest = blockIdx.x / S;
+  const int ct = rest % p.nct;
+  const int st = rest / p.nct;
+  int b, x0, y0, z0;
+  tile_origin<T, BX, BY, BZ>(p, st, &b, &x0, &y0, &z0);
+
+  int hbase[2];
+#pragma unroll
+  for (int mf = 0; mf < 2; ++mf) {
+    const int r = wv * 64 + mf * 32 + lr;
+    const int rx = r % BX, ry = (r / BX) % BY, rz = r / (BX * BY);
+    hbase[mf] = ((rz + 1) * HY + (ry + 1)) * HX + (rx + 1);
+  }
+
+  f32x16 acc[2][NF];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < NF; ++n)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.f;
+
+  const int nA = (p.ac0 + p.ac1) / CK;
+  const int nB = p.bw ? (p.bc0 + p.bc1) / CK : 0;
+  const int total = nA + nB;
+  const int per = (total + S - 1) / S;
+  const int g0 = ks * per, g1 = min(total, g0 + per);
+
+  auto wsrc = [&](int gc, int* bytes) {
+    const bool segA = gc < nA;
+    const int chunk = segA ? gc : gc - nA;
+    const int ntaps = segA ? 27 : 1;
+    const int nch = segA ? nA : nB;
+    *bytes = ntaps * NT * 32;
+    return reinterpret_cast<const unsigned char*>(segA ? p.aw : p.bw) +
+           ((long long)ct * nch + chunk) * (long long)(ntaps * NT * 32);
+  };
+
+  Stager<T, BX, BY, BZ, MODE, GN> sg;
+  if (g0 < g1) {
+    sg.fetch(p, g0 < nA, g0 < nA ? g0 : g0 - nA, b, x0, y0, z0, tid);
+    int wb;
+    const unsigned char* wsp = wsrc(g0, &wb);
+    stage_weights(wl, wsp, wb, tid);
+    sg.template store<true>(halo, p, b, x0, y0, z0, tid);
+    __syncthreads();
+  }
+  for (int gc = g0; gc < g1; ++gc) {
+    const bool segA = gc < nA;
+    const int ntaps = segA ? 27 : 1;
+    const bool has_next = gc + 1 < g1;
+    if (has_next) sg.fetch(p, gc + 1 < nA, gc + 1 < nA ? gc + 1 : gc + 1 - nA, b, x0, y0, z0, tid);
+    for (int tap = 0; tap < ntaps; ++tap) {
+      int toff = 0;
+      if (segA) {
+        const int dz = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dx = tap % 3 - 1;
+        toff = (dz * HY + dy) * HX + dx;
+      }
+      u32x4 bq[NF], aq[2];
+#pragma unroll
+      for (int n = 0; n < NF; ++n) {
+        const int row = n * 32 + lr;
+        bq[n] = *reinterpret_cast<const u32x4*>(wl + (tap * NT + row) * 32 + ((hh ^ ((row >> 3) & 1)) << 4));
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int v = hbase[m] + toff;
+        aq[m] = *reinterpret_cast<const u32x4*>(halo + v * 32 + ((hh ^ ((v >> 3) & 1)) << 4));
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < NF; ++n) {
+          if constexpr (sizeof(T) == 2) {
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, aq[m]),
+                                                                __builtin_bit_cast(bf16x8, bq[n]), acc[m][n], 0, 0, 0);
+          } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(aq[m][s]), __uint_as_float(bq[n][s]),
+                                                               acc[m][n], 0, 0, 0);
+          }
+        }
+    }
+    if (!has_next) break;
+    __syncthreads();  // every wave is done reading this chunk's halo and weights
+    int wb;
+    const unsigned char* wsp = wsrc(gc + 1, &wb);
+    stage_weights(wl, wsp, wb, tid);
+    sg.template store<true>(halo, p, b, x0, y0, z0, tid);
+    __syncthreads();
+  }
+
+  __syncthreads();
+  float* E = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < NF; ++n)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = wv * 64 + m * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        E[row * Cfg::EPI_LD + n * 32 + lr] = acc[m][n][i];
+      }
+  __syncthreads();
+  if (S == 1) {
+    epilogue_rows<T, BX, BY, BZ, NF, 256>(p, E, b, st, ct, x0, y0, z0, tid);
+    return;
+  }
+  write_partial<T, BX, BY, BZ, NF, 256>(p, E, ks, b, ct, x0, y0, z0, tid);
+}
+
+// split-K, stage 1: partial[0] += partial[1..S-1], elementwise over the whole
+// output (bandwidth-bound, every CU busy) ...
+__global__ void __launch_bounds__(256) splitk_sum_kernel(float* __restrict__ part, int S, long long n4) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4* p4 = reinterpret_cast<float4*>(part);
+  float4 a = p4[i];
+  for (int k = 1; k < S; ++k) {
+    const float4 b = p4[i + k * n4];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  p4[i] = a;
+}
+
+// ... stage 2: epilogue on the summed tile, one workgroup per (spatial tile, channel tile)
+template <typename T, int BX, int BY, int BZ, int NF>
+__global__ void __launch_bounds__(256) conv3d_reduce_kernel(ConvParams p) {
+  constexpr int ROWS = BX * BY * BZ, NT = 32 * NF, LD = NT + 4, CG = NT / 8;
+  __shared__ __attribute__((aligned(16))) float E[ROWS * LD > 256 * 16 ? ROWS * LD : 256 * 16];
+  const int tid = threadIdx.x;
+  const int ct = blockIdx.x % p.nct;
+  const int st = blockIdx.x / p.nct;
+  int b, x0, y0, z0;
+  tile_origin<T, BX, BY, BZ>(p, st, &b, &x0, &y0, &z0);
+  const int cg = tid % CG;
+  const int cbase = ct * NT + cg * 8;
+  const int nvalid = min(8, p.cout - cbase);
+  for (int u = tid; u < ROWS * CG; u += 256) {
+    const int row = u / CG;
+    const int rx = row % BX, ry = (row / BX) % BY, rz = row / (BX * BY);
+    const int ox = x0 + rx, oy = y0 + ry, oz = z0 + rz;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    if (!(ox >= p.W || oy >= p.H || oz >= p.D || nvalid <= 0)) {
+      const long long vox = (((long long)b * p.D + oz) * p.H + oy) * p.W + ox;
+      const float* src = p.partial + vox * p.cout + cbase;
+      if (nvalid == 8) {
+        float4 a = *reinterpret_cast<const float4*>(src), c = *reinterpret_cast<const float4*>(src + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+      } else {
+        for (int e = 0; e < nvalid; ++e) v[e] = src[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) E[row * LD + cg * 8 + e] = v[e];
+  }
+  __syncthreads();
+  epilogue_rows<T, BX, BY, BZ, NF, ROWS>(p, E, b, st, ct, x0, y0, z0, tid);
+}
+
+// ===========================================================================
+// Wide-grid kernel (output W >= 32): brick 32(x) x 4(y) x 4(z) = 512 rows,
+// wave w owns z-plane w = four 32-voxel x-lines = four 32-row A fragments.
+// For a fixed (dz, dx) the three dy taps read input lines y-1 .. y+4, so each
+// wave loads 6 A fragments and reuses them across the 3 dy taps (12 MFMA uses):
+// half the LDS reads of one-tap-at-a-time.  The halo image is linear (no
+// swizzle) so every (dz, line, dx) offset is an immediate; lanes of a read
+// group touch 16 consecutive voxels (2-way bank conflict, LDS stays < 40%
+// busy).  Weights are double-buffered and filled by LDS-DMA one chunk ahead;
+// the next chunk's halo is fetched into registers at the top of the chunk and
+// transformed (GN+SiLU) after the first dz slab, so HBM latency and the
+// prologue VALU both hide under the MFMAs.  One 4-wave workgroup per CU.
+// ===========================================================================
+template <typename T, int NF>
+struct WideCfg {
+  static constexpr int BX = 32, BY = 4, BZ = 4, HX = 34, HY = 6, HZ = 6, HV = HX * HY * HZ;
+  static constexpr int NT = 32 * NF;
+  static constexpr int HALO_B = HV * 32;
+  static constexpr int WB = 27 * NT * 32;
+  static constexpr int EPI_LD = NT + 4;
+  static constexpr int EPI_B = 512 * EPI_LD * 4;
+  static constexpr int MAIN_B = HALO_B + 2 * WB;
+  static constexpr int SMEM = MAIN_B > EPI_B ? MAIN_B : EPI_B;
+};
+
+__device__ __forceinline__ void mfma_acc(f32x16& acc, const u32x4& a, const u32x4& b, bf16_t*) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0,
+                                               0, 0);
+}
+__device__ __forceinline__ void mfma_acc(f32x16& acc, const u32x4& a, const u32x4& b, float*) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a[s]), __uint_as_float(b[s]), acc, 0, 0, 0);
+}
+
+template <typename T, int NF, int DZ>
+__device__ __forceinline__ void wide_slab(f32x16 (&acc)[4][NF], const unsigned char* halo_lane,
+                                          const unsigned char* w_lane) {
+  using C = WideCfg<T, NF>;
+#pragma unroll
+  for (int dx = -1; dx <= 1; ++dx) {
+    u32x4 a[6];
+#pragma unroll
+    for (int L = 0; L < 6; ++L)
+      a[L] = *reinterpret_cast<const u32x4*>(halo_lane + ((DZ * C::HY + (L - 1)) * C::HX + dx) * 32);
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      constexpr int dummy = 0;
+      (void)dummy;
+      const int tap = ((DZ + 1) * 3 + (dy + 1)) * 3 + (dx + 1);
+      u32x4 bq[NF];
+#pragma unroll
+      for (int n = 0; n < NF; ++n)
+        bq[n] = *reinterpret_cast<const u32x4*>(w_lane + (tap * C::NT + n * 32) * 32);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < NF; ++n) mfma_acc(acc[m][n], a[m + dy + 1], bq[n], (T*)nullptr);
+    }
+  }
+}
+
+template <typename T, int NF, int MODE, bool GN>
+__global__ void __launch_bounds__(256) conv3d_wide_kernel(ConvParams p) {
+  using C = WideCfg<T, NF>;
+  constexpr int CK = ConvTr<T>::CK, NT = C::NT;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[C::SMEM];
+  unsigned char* halo = smem;
+  unsigned char* wbuf0 = smem + C::HALO_B;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 31, hh = lane >> 5;
+  const int S = p.ksplit;
+  const int ks = blockIdx.x % S;
+  const int rest = blockIdx.x / S;
+  const int ct = rest % p.nct;
+  const int st = rest / p.nct;
+  int b, x0, y0, z0;
+  tile_origin<T, C::BX, C::BY, C::BZ>(p, st, &b, &x0, &y0, &z0);
+
+  // lane bases: A at (z = wv, line 0, x = lr), centre tap; B at row lr
+  const unsigned char* halo_lane = halo + (((wv + 1) * C::HY + 1) * C::HX + lr + 1) * 32 + hh * 16;
+  const int w_lane_off = lr * 32 + ((hh ^ ((lr >> 3) & 1)) << 4);
+
+  f32x16 acc[4][NF];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < NF; ++n)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.f;
+
+  const int nA = (p.ac0 + p.ac1) / CK;
+  const int nB = p.bw ? (p.bc0 + p.bc1) / CK : 0;
+  const int total = nA + nB;
+  const int per = (total + S - 1) / S;
+  const int g0 = ks * per, g1 = min(total, g0 + per);
+
+  auto wsrc = [&](int gc, int* bytes) {
+    const bool segA = gc < nA;
+    const int chunk = segA ? gc : gc - nA;
+    const int ntaps = segA ? 27 : 1;
+    const int nch = segA ? nA : nB;
+    *bytes = ntaps * NT * 32;
+    return reinterpret_cast<const unsigned char*>(segA ? p.aw : p.bw) +
+           ((long long)ct * nch + chunk) * (long long)(ntaps * NT * 32);
+  };
+
+  Stager<T, C::BX, C::BY, C::BZ, MODE, GN> sg;
+  if (g0 < g1) {
+    int wb;
+    const unsigned char* wsp = wsrc(g0, &wb);
+    stage_weights(wbuf0, wsp, wb, tid);
+    sg.fetch(p, g0 < nA, g0 < nA ? g0 : g0 - nA, b, x0, y0, z0, tid);
+    if constexpr (MODE == 2) {
+      sg.template store<false>(halo, p, b, x0, y0, z0, tid);
+    } else {
+      sg.transform();
+      sg.template write<false>(halo, tid);
+    }
+    __syncthreads();
+  }
+  for (int gc = g0; gc < g1; ++gc) {
+    const bool segA = gc < nA;
+    const bool has_next = gc + 1 < g1;
+    unsigned char* wcur = wbuf0 + ((gc - g0) & 1) * C::WB;
+    if (has_next) {
+      int wb;
+      const unsigned char* wsp = wsrc(gc + 1, &wb);
+      stage_weights(wbuf0 + ((gc + 1 - g0) & 1) * C::WB, wsp, wb, tid);
+      sg.fetch(p, gc + 1 < nA, gc + 1 < nA ? gc + 1 : gc + 1 - nA, b, x0, y0, z0, tid);
+    }
+    const unsigned char* w_lane = wcur + w_lane_off;
+    if (segA) {
+      wide_slab<T, NF, -1>(acc, halo_lane, w_lane);
+      if (has_next) sg.transform();
+      wide_slab<T, NF, 0>(acc, halo_lane, w_lane);
+      wide_slab<T, NF, 1>(acc, halo_lane, w_lane);
+    } else {
+      // 1x1 segment: centre tap only (its weights are tap 0 of the chunk)
+      u32x4 a[4], bq[NF];
+#pragma unroll
+      for (int L = 0; L < 4; ++L) a[L] = *reinterpret_cast<const u32x4*>(halo_lane + (L * C::HX) * 32);
+#pragma unroll
+      for (int n = 0; n < NF; ++n) bq[n] = *reinterpret_cast<const u32x4*>(w_lane + (n * 32) * 32);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < NF; ++n) mfma_acc(acc[m][n], a[m], bq[n], (T*)nullptr);
+      if (has_next) sg.transform();
+    }
+    if (!has_next) break;
+    __syncthreads();  // all waves done with this chunk's halo and weights
+    if constexpr (MODE == 2) sg.template store<false>(halo, p, b, x0, y0, z0, tid);
+    else sg.template write<false>(halo, tid);
+    __syncthreads();  // (drains the LDS-DMA of the next weights as well)
+  }
+
+  __syncthreads();
+  float* E = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < NF; ++n)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = wv * 128 + m * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        E[row * C::EPI_LD + n * 32 + lr] = acc[m][n][i];
+      }
+  __syncthreads();
+  if (S == 1) {
+    epilogue_rows<T, C::BX, C::BY, C::BZ, NF, 512>(p, E, b, st, ct, x0, y0, z0, tid);
+    return;
+  }
+  write_partial<T, C::BX, C::BY, C::BZ, NF, 512>(p, E, ks, b, ct, x0, y0, z0, tid);
 }
 
 // ---- weight packing: OIDHW fp32 -> [ct][chunk][tap][n][2 quads, swizzled] ----
@@ -393,7 +777,7 @@ inline int pick_nf(int cout) { return (cout % 64 == 0) ? 2 : 1; }
 struct Brick { int bx, by, bz; };
 inline Brick pick_brick(int64_t D, int64_t H, int64_t W) {
   (void)D; (void)H;
-  if (W >= 32) return {32, 4, 2};
+  if (W >= 32) return {32, 4, 4};  // conv3d_wide_kernel
   if (W >= 16) return {16, 4, 4};
   return {8, 8, 4};
 }
@@ -401,17 +785,77 @@ inline Brick pick_brick(int64_t D, int64_t H, int64_t W) {
 template <typename T, int BX, int BY, int BZ, int NF>
 int launch_conv(const ConvParams& p, hipStream_t s) {
   const long long nblk = (long long)p.B * p.tx * p.ty * p.tz * p.nct;
-  CWDM_REQUIRE(nblk < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d: grid too large");
-  hipLaunchKernelGGL((conv3d_kernel<T, BX, BY, BZ, NF>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+  CWDM_REQUIRE(nblk * p.ksplit < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d: grid too large");
+  const dim3 grid((unsigned)(nblk * p.ksplit));
+  const bool gn = p.agn != nullptr;
+  if (p.amode == 0) {
+    if (gn) hipLaunchKernelGGL((conv3d_kernel<T, BX, BY, BZ, NF, 0, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv3d_kernel<T, BX, BY, BZ, NF, 0, false>), grid, dim3(256), 0, s, p);
+  } else if (p.amode == 1) {
+    if (gn) hipLaunchKernelGGL((conv3d_kernel<T, BX, BY, BZ, NF, 1, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv3d_kernel<T, BX, BY, BZ, NF, 1, false>), grid, dim3(256), 0, s, p);
+  } else {
+    if (gn) hipLaunchKernelGGL((conv3d_kernel<T, BX, BY, BZ, NF, 2, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv3d_kernel<T, BX, BY, BZ, NF, 2, false>), grid, dim3(256), 0, s, p);
+  }
   CWDM_LAUNCHED();
+  if (p.ksplit > 1) {
+    const long long n4 = (long long)p.B * p.D * p.H * p.W * p.cout / 4;
+    hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, s, p.partial, p.ksplit, n4);
+    CWDM_LAUNCHED();
+    ConvParams q = p;
+    q.ksplit = 1;
+    hipLaunchKernelGGL((conv3d_reduce_kernel<T, BX, BY, BZ, NF>), dim3((unsigned)nblk), dim3(256), 0, s, q);
+    CWDM_LAUNCHED();
+  }
+  return CWDM_OK;
+}
+
+template <typename T, int NF>
+int launch_wide(const ConvParams& p, hipStream_t s) {
+  const long long nblk = (long long)p.B * p.tx * p.ty * p.tz * p.nct;
+  CWDM_REQUIRE(nblk * p.ksplit < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d: grid too large");
+  const dim3 grid((unsigned)(nblk * p.ksplit));
+  const bool gn = p.agn != nullptr;
+  if (p.amode == 0) {
+    if (gn) hipLaunchKernelGGL((conv3d_wide_kernel<T, NF, 0, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv3d_wide_kernel<T, NF, 0, false>), grid, dim3(256), 0, s, p);
+  } else if (p.amode == 1) {
+    if (gn) hipLaunchKernelGGL((conv3d_wide_kernel<T, NF, 1, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv3d_wide_kernel<T, NF, 1, false>), grid, dim3(256), 0, s, p);
+  } else {
+    if (gn) hipLaunchKernelGGL((conv3d_wide_kernel<T, NF, 2, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv3d_wide_kernel<T, NF, 2, false>), grid, dim3(256), 0, s, p);
+  }
+  CWDM_LAUNCHED();
+  if (p.ksplit > 1) {
+    const long long n4 = (long long)p.B * p.D * p.H * p.W * p.cout / 4;
+    hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, s, p.partial, p.ksplit, n4);
+    CWDM_LAUNCHED();
+    ConvParams q = p;
+    q.ksplit = 1;
+    hipLaunchKernelGGL((conv3d_reduce_kernel<T, 32, 4, 4, NF>), dim3((unsigned)nblk), dim3(256), 0, s, q);
+    CWDM_LAUNCHED();
+  }
   return CWDM_OK;
 }
 
 template <typename T, int NF>
 int dispatch_brick(const ConvParams& p, const Brick& br, hipStream_t s) {
+  if (br.bx == 32 && br.bz == 4) return launch_wide<T, NF>(p, s);
   if (br.bx == 32) return launch_conv<T, 32, 4, 2, NF>(p, s);
   if (br.bx == 16) return launch_conv<T, 16, 4, 4, NF>(p, s);
   return launch_conv<T, 8, 8, 4, NF>(p, s);
+}
+
+// K-split factor: small grids (the U-Net's 32^3 .. 8^3 levels) get split-K so
+// that a launch has ~768 workgroups to spread over 256 CUs.
+inline int pick_ksplit(long long nblk, int total_chunks) {
+  if (nblk >= 512 || total_chunks <= 1) return 1;
+  int S = (int)((768 + nblk - 1) / nblk);
+  if (S > total_chunks) S = total_chunks;
+  const int per = (total_chunks + S - 1) / S;
+  return (total_chunks + per - 1) / per;
 }
 
 int ck_of(int dtype) { return dtype == CWDM_BF16 ? 16 : 8; }
@@ -454,6 +898,27 @@ extern "C" int cwdm_conv3d_pack(const float* w, int cout, int cin, int ksize, in
   return CWDM_OK;
 }
 
+namespace {
+struct Plan1 { Brick br; int nf, nct, S; long long nblk; int64_t ws; };
+Plan1 plan_conv(const cwdm_conv3d_desc* d) {
+  Plan1 q;
+  q.br = pick_brick(d->D, d->H, d->W);
+  q.nf = pick_nf(d->cout);
+  q.nct = (int)ceil_div(d->cout, 32 * q.nf);
+  q.nblk = (long long)d->B * ceil_div(d->W, q.br.bx) * ceil_div(d->H, q.br.by) * ceil_div(d->D, q.br.bz) * q.nct;
+  const int ck = ck_of(d->dtype);
+  const int total = (d->a_c0 + d->a_c1) / ck + (d->b_w ? (d->b_c0 + d->b_c1) / ck : 0);
+  q.S = pick_ksplit(q.nblk, total);
+  q.ws = q.S > 1 ? (int64_t)q.S * d->B * d->D * d->H * d->W * d->cout * 4 : 0;
+  return q;
+}
+}  // namespace
+
+extern "C" int64_t cwdm_conv3d_workspace_bytes(const cwdm_conv3d_desc* d) {
+  if (!d || d->B <= 0 || d->D <= 0 || d->H <= 0 || d->W <= 0 || d->cout <= 0) return -1;
+  return plan_conv(d).ws;
+}
+
 extern "C" int64_t cwdm_conv3d_parts(int dtype, int64_t D, int64_t H, int64_t W, int cout) {
   (void)dtype; (void)cout;
   Brick br = pick_brick(D, H, W);
@@ -479,12 +944,13 @@ extern "C" int cwdm_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stre
   CWDM_REQUIRE(d->res_mode < 0 || d->res, CWDM_E_INVALID, "cwdm_conv3d_forward: residual pointer missing");
   CWDM_REQUIRE(d->out_dtype == CWDM_F32 || d->out_dtype == d->dtype, CWDM_E_INVALID,
                "cwdm_conv3d_forward: output dtype must be fp32 or the compute dtype");
-  const int nf = pick_nf(d->cout);
+  const Plan1 pl = plan_conv(d);
+  const int nf = pl.nf;
   CWDM_REQUIRE(nf == 2 || d->cout % 32 == 0 || d->cout < 32, CWDM_E_UNSUPPORTED,
                "cwdm_conv3d_forward: cout must be a multiple of 32 or below 32");
   ConvParams p{};
   p.B = (int)d->B; p.D = (int)d->D; p.H = (int)d->H; p.W = (int)d->W;
-  Brick br = pick_brick(d->D, d->H, d->W);
+  const Brick br = pl.br;
   p.tx = (int)ceil_div(d->W, br.bx); p.ty = (int)ceil_div(d->H, br.by); p.tz = (int)ceil_div(d->D, br.bz);
   p.cout = d->cout; p.nct = (int)ceil_div(d->cout, 32 * nf);
   p.a0 = d->a0; p.ac0 = d->a_c0; p.a1 = d->a1; p.ac1 = d->a_c1; p.amode = d->a_mode; p.agn = d->a_gn; p.aw = d->a_w;
@@ -493,6 +959,12 @@ extern "C" int cwdm_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stre
   p.res = d->res; p.rmode = d->res_mode;
   p.out = d->out; p.out_f32 = (d->out_dtype == CWDM_F32 && d->dtype != CWDM_F32) ? 1 : (d->dtype == CWDM_F32);
   p.stats = d->stats;
+  p.ksplit = 1;
+  p.partial = nullptr;
+  if (pl.S > 1 && d->workspace && d->ws_bytes >= pl.ws) {
+    p.ksplit = pl.S;
+    p.partial = reinterpret_cast<float*>(d->workspace);
+  }
   hipStream_t s = (hipStream_t)stream;
   if (d->dtype == CWDM_BF16)
     return nf == 2 ? dispatch_brick<bf16_t, 2>(p, br, s) : dispatch_brick<bf16_t, 1>(p, br, s);

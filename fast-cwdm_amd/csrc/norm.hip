@@ -73,3 +73,72 @@ extern "C" int cwdm_gn_finalize(const float* s0, int64_t p0, int c0, const float
   CWDM_LAUNCHED();
   return CWDM_OK;
 }
+
+// Down-ResBlock pre-pass (unet.py:286-291 with Downsample, :73-100):
+//   h = AvgPool2(SiLU(GN(x))),  x_upd = AvgPool2(x)
+// one thread per (low-res voxel, 8-channel group); the consumer conv then
+// runs at the low resolution with no prologue transform.
+namespace cwdm {
+namespace {
+template <typename T>
+__global__ void __launch_bounds__(256) gn_silu_pool_kernel(const T* __restrict__ x, int C,
+                                                          const float* __restrict__ gn, long long B, int d, int h,
+                                                          int w, T* __restrict__ oh, T* __restrict__ ox) {
+  const int G8 = C / 8;
+  const long long n = B * (long long)d * h * w * G8;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int g = (int)(i % G8);
+  long long v = i / G8;
+  const int xx = (int)(v % w), yy = (int)((v / w) % h), zz = (int)((v / ((long long)w * h)) % d);
+  const long long b = v / ((long long)w * h * d);
+  float sc[8], sh[8], ah[8], ax[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = gn[(b * C + g * 8 + e) * 2];
+    sh[e] = gn[(b * C + g * 8 + e) * 2 + 1];
+    ah[e] = 0.f;
+    ax[e] = 0.f;
+  }
+  const int H = 2 * h, W = 2 * w, D = 2 * d;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const long long src = (((b * D + 2 * zz + (k >> 2)) * H + 2 * yy + ((k >> 1) & 1)) * W + 2 * xx + (k & 1)) * C + g * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xv = Elem<T>::to_f(x[src + e]);
+      const float y = xv * sc[e] + sh[e];
+      ah[e] += y / (1.0f + __expf(-y));
+      ax[e] += xv;
+    }
+  }
+  const long long dst = v * C + g * 8;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    oh[dst + e] = Elem<T>::from_f(ah[e] * 0.125f);
+    ox[dst + e] = Elem<T>::from_f(ax[e] * 0.125f);
+  }
+}
+}  // namespace
+}  // namespace cwdm
+
+extern "C" int cwdm_gn_silu_pool(const void* x, int C, const float* gn, int64_t B, int64_t d, int64_t h, int64_t w,
+                                 int dtype, void* out_h, void* out_x, cwdm_stream_t stream) {
+  CWDM_REQUIRE(x && gn && out_h && out_x, CWDM_E_INVALID, "cwdm_gn_silu_pool: null pointer");
+  CWDM_REQUIRE(C > 0 && C % 8 == 0 && B > 0 && d > 0 && h > 0 && w > 0, CWDM_E_SHAPE,
+               "cwdm_gn_silu_pool: bad shape (channels must be a multiple of 8)");
+  const int64_t n = B * d * h * w * (C / 8);
+  dim3 grid((unsigned)ceil_div(n, 256));
+  if (dtype == CWDM_BF16)
+    hipLaunchKernelGGL(gn_silu_pool_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const bf16_t*>(x), C, gn, (long long)B, (int)d, (int)h, (int)w,
+                       reinterpret_cast<bf16_t*>(out_h), reinterpret_cast<bf16_t*>(out_x));
+  else if (dtype == CWDM_F32)
+    hipLaunchKernelGGL(gn_silu_pool_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float*>(x), C, gn, (long long)B, (int)d, (int)h, (int)w,
+                       reinterpret_cast<float*>(out_h), reinterpret_cast<float*>(out_x));
+  else
+    return fail(CWDM_E_INVALID, "cwdm_gn_silu_pool: bad dtype");
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}

@@ -59,7 +59,11 @@ struct ConvStep {
   bool stats;
 };
 
-struct Step { int kind; int idx; };  // kind 0 = gn, 1 = conv
+struct PoolStep {  // down-ResBlock pre-pass (cwdm_gn_silu_pool)
+  int src, ss_id, out_h, out_x, level_out, channels;
+};
+
+struct Step { int kind; int idx; };  // kind 0 = gn, 1 = conv, 2 = pool pre-pass
 
 }  // namespace
 
@@ -70,6 +74,7 @@ struct cwdm_unet {
   std::vector<Tensor> tensors;
   std::vector<GnStep> gns;
   std::vector<ConvStep> convs;
+  std::vector<PoolStep> pools;
   std::vector<Step> steps;
   std::vector<int> trace;         // tensor id per topology block (-1 = final output)
   std::vector<int> trace_level;
@@ -153,11 +158,24 @@ void build(cwdm_unet* u) {
     const int cin = u->tensors[x0].channels + (x1 >= 0 ? u->tensors[x1].channels : 0);
     const int lout = updown == 2 ? lin + 1 : (updown == 1 ? lin - 1 : lin);
     int g1 = gn_step(p + ".in_layers.0", x0, x1, lin);
+    int xres = x0, xrmode = updown == 2 ? 2 : (updown == 1 ? 1 : 0);
+    int a_src = x0, a_mode = updown, a_gn = g1;
+    if (updown == 2) {
+      // AvgPool(SiLU(GN(x))) and AvgPool(x) once, at the low resolution
+      PoolStep ps{};
+      ps.src = x0; ps.ss_id = g1; ps.level_out = lout; ps.channels = cin;
+      ps.out_h = new_tensor(lout, cin);
+      ps.out_x = new_tensor(lout, cin);
+      u->pools.push_back(ps);
+      u->steps.push_back({2, (int)u->pools.size() - 1});
+      a_src = ps.out_h; a_mode = 0; a_gn = -1;
+      xres = ps.out_x; xrmode = 0;
+    }
     ConvStep c1{};
     conv_params(p + ".in_layers.2", cout, cin, 3, &c1.w_p, &c1.b_p);
     c1.emb_w_p = u->add_param(p + ".emb_layers.1.weight", {cout, E});
     c1.emb_b_p = u->add_param(p + ".emb_layers.1.bias", {cout});
-    c1.a0 = x0; c1.a1 = x1; c1.amode = updown; c1.gn = g1; c1.cin_a = cin;
+    c1.a0 = a_src; c1.a1 = x1; c1.amode = a_mode; c1.gn = a_gn; c1.cin_a = cin;
     c1.sb0 = c1.sb1 = -1; c1.ws_p = c1.wsb_p = -1; c1.cin_b = 0;
     c1.bias_kind = 1; c1.bias_off = u->R;
     u->emb_rows_w.push_back(c1.emb_w_p); u->emb_rows_b.push_back(c1.emb_b_p); u->emb_rows_cb.push_back(c1.b_p);
@@ -178,8 +196,8 @@ void build(cwdm_unet* u) {
       conv_params(p + ".skip_connection", cout, cin, 1, &c2.ws_p, &c2.wsb_p);
       c2.sb0 = x0; c2.sb1 = x1; c2.cin_b = cin;
     } else {
-      c2.res = x0;
-      c2.rmode = updown == 2 ? 2 : (updown == 1 ? 1 : 0);
+      c2.res = xres;
+      c2.rmode = xrmode;
     }
     c2.bias_kind = 0; c2.cout = cout; c2.level = lout; c2.stats = true;
     int o = c2.out = new_tensor(lout, cout);
@@ -262,11 +280,30 @@ void build(cwdm_unet* u) {
 }
 
 struct Layout {
-  int64_t temb, ebias;
+  int64_t temb, ebias, split, split_bytes;
   std::vector<int64_t> t_off, s_off, s_parts;
   std::vector<int64_t> ss_off;
   int64_t total;
 };
+
+// shape-only descriptor of one conv step (pointers filled in by the forward)
+cwdm_conv3d_desc conv_shape(const cwdm_unet* u, const ConvStep& cs, int64_t B, int64_t D, int64_t H, int64_t W) {
+  cwdm_conv3d_desc d{};
+  d.dtype = u->cfg.dtype;
+  d.B = B; d.D = D >> cs.level; d.H = H >> cs.level; d.W = W >> cs.level;
+  d.cout = cs.cout;
+  d.a_c0 = u->tensors[cs.a0].channels;
+  d.a_c1 = cs.a1 >= 0 ? u->tensors[cs.a1].channels : 0;
+  d.a_mode = cs.amode;
+  if (cs.ws_p >= 0) {
+    d.b_c0 = u->tensors[cs.sb0].channels;
+    d.b_c1 = cs.sb1 >= 0 ? u->tensors[cs.sb1].channels : 0;
+    d.b_w = reinterpret_cast<const void*>(1);  // presence flag only
+  }
+  d.res_mode = cs.rmode;
+  d.out_dtype = cs.out < 0 ? CWDM_F32 : u->cfg.dtype;
+  return d;
+}
 
 Layout layout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
   Layout L;
@@ -288,6 +325,14 @@ Layout layout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
     L.s_off.push_back(take(B * parts * t.channels * 2 * 4));
   }
   for (const auto& g : u->gns) L.ss_off.push_back(take(B * (int64_t)g.channels * 2 * 4));
+  int64_t split = 0;
+  for (const auto& cs : u->convs) {
+    cwdm_conv3d_desc d = conv_shape(u, cs, B, D, H, W);
+    const int64_t n = cwdm_conv3d_workspace_bytes(&d);
+    if (n > split) split = n;
+  }
+  L.split_bytes = split;
+  L.split = take(split);
   L.total = off;
   return L;
 }
@@ -451,6 +496,15 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
     u->ev_used = 0;
   }
   for (const auto& st : u->steps) {
+    if (st.kind == 2) {
+      const auto& ps = u->pools[st.idx];
+      const int lv = ps.level_out;
+      if ((rc = cwdm_gn_silu_pool(tptr(ps.src), ps.channels, reinterpret_cast<const float*>(wb + L.ss_off[ps.ss_id]),
+                                  B, D >> lv, H >> lv, W >> lv, u->cfg.dtype, wb + L.t_off[ps.out_h],
+                                  wb + L.t_off[ps.out_x], stream)))
+        return rc;
+      continue;
+    }
     if (st.kind == 0) {
       const auto& g = u->gns[st.idx];
       const int lv = g.level;
@@ -465,13 +519,11 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
       continue;
     }
     const auto& cs = u->convs[st.idx];
-    cwdm_conv3d_desc d{};
-    d.dtype = u->cfg.dtype;
-    d.B = B; d.D = D >> cs.level; d.H = H >> cs.level; d.W = W >> cs.level;
-    d.cout = cs.cout;
-    d.a0 = tptr(cs.a0); d.a_c0 = u->tensors[cs.a0].channels;
-    d.a1 = tptr(cs.a1); d.a_c1 = cs.a1 >= 0 ? u->tensors[cs.a1].channels : 0;
-    d.a_mode = cs.amode;
+    cwdm_conv3d_desc d = conv_shape(u, cs, B, D, H, W);
+    d.a0 = tptr(cs.a0);
+    d.a1 = tptr(cs.a1);
+    d.workspace = wb + L.split;
+    d.ws_bytes = L.split_bytes;
     d.a_gn = cs.gn >= 0 ? reinterpret_cast<const float*>(wb + L.ss_off[cs.gn]) : nullptr;
     d.a_w = pk + cs.w_off;
     if (cs.ws_p >= 0) {

@@ -53,6 +53,7 @@ class ConvDesc(ctypes.Structure):
         ("res", vp), ("res_mode", ctypes.c_int),
         ("out", vp), ("out_dtype", ctypes.c_int),
         ("stats", vp),
+        ("workspace", vp), ("ws_bytes", i64),
     ]
 
 
@@ -80,8 +81,10 @@ _PROTOS = {
     "cwdm_conv3d_pack": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]),
     "cwdm_conv3d_parts": (i64, [ctypes.c_int, i64, i64, i64, ctypes.c_int]),
     "cwdm_conv3d_forward": (ctypes.c_int, [ctypes.POINTER(ConvDesc), vp]),
+    "cwdm_conv3d_workspace_bytes": (i64, [ctypes.POINTER(ConvDesc)]),
     "cwdm_gn_finalize": (ctypes.c_int, [vp, i64, ctypes.c_int, vp, i64, ctypes.c_int, vp, vp, ctypes.c_int, i64, i64,
                                         ctypes.c_float, vp, vp]),
+    "cwdm_gn_silu_pool": (ctypes.c_int, [vp, ctypes.c_int, vp, i64, i64, i64, i64, ctypes.c_int, vp, vp, vp]),
     "cwdm_unet_create": (ctypes.c_int, [ctypes.POINTER(UNetConfig), ctypes.POINTER(vp)]),
     "cwdm_unet_destroy": (None, [vp]),
     "cwdm_unet_num_params": (ctypes.c_int, [vp]),

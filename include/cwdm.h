@@ -147,11 +147,15 @@ typedef struct {
   const void* res; int res_mode;
   void* out; int out_dtype;
   float* stats;
+  void* workspace; int64_t ws_bytes; /* split-K partials for small grids (optional) */
 } cwdm_conv3d_desc;
 int64_t cwdm_conv3d_packed_bytes(int cout, int cin, int ksize, int dtype);
 int cwdm_conv3d_pack(const float* w_oidhw, int cout, int cin, int ksize, int dtype,
                      void* packed, cwdm_stream_t stream);
 int64_t cwdm_conv3d_parts(int dtype, int64_t D, int64_t H, int64_t W, int cout);
+/* Workspace that lets cwdm_conv3d_forward split K over workgroups on small
+ * grids (0 when it would not split; without it the launch runs unsplit). */
+int64_t cwdm_conv3d_workspace_bytes(const cwdm_conv3d_desc* desc);
 int cwdm_conv3d_forward(const cwdm_conv3d_desc* desc, cwdm_stream_t stream);
 
 /* GroupNorm statistics -> per-channel (scale, shift) for the consumer conv's
@@ -163,6 +167,13 @@ int cwdm_gn_finalize(const float* stats0, int64_t parts0, int c0,
                      const float* gamma, const float* beta, int groups,
                      int64_t B, int64_t voxels, float eps,
                      float* scale_shift, cwdm_stream_t stream);
+
+/* Down-ResBlock pre-pass: h = AvgPool2(SiLU(x*scale+shift)), x_upd = AvgPool2(x)
+ * (ResBlock._forward with down=True, guided_diffusion/unet.py:286-291,
+ * Downsample :73-100).  x: NDHWC high-res (B, 2d, 2h, 2w, C); outputs NDHWC
+ * (B, d, h, w, C) in dtype; gn as for cwdm_conv3d_desc.a_gn. */
+int cwdm_gn_silu_pool(const void* x, int C, const float* gn, int64_t B, int64_t d, int64_t h, int64_t w,
+                      int dtype, void* out_h, void* out_x, cwdm_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * U-Net plan: the whole UNetModel.forward (guided_diffusion/unet.py:754-800)

@@ -96,7 +96,7 @@ def test_sampler_step_vs_oracle(clip, mean_type):
 
 # --------------------------------------------------------------------------- conv3d
 def _conv_call(dtype, out_grid, a0, a1, amode, gn, w, bias, bvec_bstride=0, b0=None, b1=None, wb=None, res=None,
-               rmode=-1, out_f32=False, stats=True):
+               rmode=-1, out_f32=False, stats=True, split=True):
     """Run cwdm_conv3d_forward on NDHWC tensors; returns (out, stats)."""
     from cwdm_hip import _lib
     from cwdm_hip._lib import check, lib
@@ -133,6 +133,11 @@ def _conv_call(dtype, out_grid, a0, a1, amode, gn, w, bias, bvec_bstride=0, b0=N
     d.res, d.res_mode = (res.data_ptr() if res is not None else None), rmode
     d.out, d.out_dtype = out.data_ptr(), (_lib.CWDM_F32 if out_f32 else dtype)
     d.stats = st.data_ptr() if st is not None else None
+    nws = L.cwdm_conv3d_workspace_bytes(ctypes.byref(d))
+    ws = None
+    if nws > 0 and split:
+        ws = torch.empty(nws, dtype=torch.uint8, device=DEV)
+        d.workspace, d.ws_bytes = ws.data_ptr(), nws
     check(L.cwdm_conv3d_forward(ctypes.byref(d), None))
     torch.cuda.synchronize()
     return out, st
@@ -158,9 +163,10 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("split", [True, False], ids=["splitk", "nosplit"])
 @pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_conv3d_fused_vs_torch(case, dtype_name):
+def test_conv3d_fused_vs_torch(case, dtype_name, split):
     from cwdm_hip import _lib
     name, B, grid, c0, c1, cout, amode, use_gn, skip, rmode = case
     dtype = _lib.CWDM_F32 if dtype_name == "fp32" else _lib.CWDM_BF16
@@ -209,7 +215,7 @@ def test_conv3d_fused_vs_torch(case, dtype_name):
         gn.to(DEV) if gn is not None else None, wq.to(DEV), bias.to(DEV),
         b0=_nd(b0).to(DEV, tdt) if skip else None, b1=_nd(b1).to(DEV, tdt) if (skip and c1) else None,
         wb=wb.to(tdt).float().to(DEV) if skip else None, res=_nd(res).to(DEV, tdt) if res is not None else None,
-        rmode=rmode, out_f32=(cout == 8))
+        rmode=rmode, out_f32=(cout == 8), split=split)
     got = _nc(out.float().cpu())
     tol = 2e-5 if dtype_name == "fp32" else 2e-2
     assert rel_err(got, ref) < tol, name
@@ -254,3 +260,26 @@ def test_copy3_layouts():
     back = torch.empty(2, 24, 5, 6, 7, device=DEV)
     ops.copy3(buf[..., 8:], (V * 32, 1, 32), back, (24 * V, V, 1), 2, 24, V)
     assert torch.equal(back.cpu(), x.to(torch.bfloat16).float().cpu())
+
+
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+def test_gn_silu_pool(dtype_name):
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import check, lib
+    tdt = torch.float32 if dtype_name == "fp32" else torch.bfloat16
+    g = torch.Generator().manual_seed(9)
+    B, C, d = 2, 64, 4
+    x = torch.randn(B, C, 2 * d, 2 * d, 2 * d, generator=g).to(tdt).float()
+    scale = 1 + 0.2 * torch.randn(B, C, generator=g)
+    shift = 0.2 * torch.randn(B, C, generator=g)
+    gn = torch.stack([scale, shift], -1).contiguous().to(DEV)
+    xd = _nd(x).to(DEV, tdt)
+    oh = torch.empty(B, d, d, d, C, device=DEV, dtype=tdt)
+    ox = torch.empty_like(oh)
+    dt = _lib.CWDM_F32 if dtype_name == "fp32" else _lib.CWDM_BF16
+    check(lib().cwdm_gn_silu_pool(ctypes.c_void_p(xd.data_ptr()), C, ctypes.c_void_p(gn.data_ptr()), B, d, d, d, dt,
+                                  ctypes.c_void_p(oh.data_ptr()), ctypes.c_void_p(ox.data_ptr()), None))
+    h = F.avg_pool3d(F.silu(x * scale[:, :, None, None, None] + shift[:, :, None, None, None]), 2)
+    tol = 1e-5 if dtype_name == "fp32" else 1e-2
+    assert rel_err(_nc(oh.float().cpu()), h) < tol
+    assert rel_err(_nc(ox.float().cpu()), F.avg_pool3d(x, 2)) < tol

@@ -1,6 +1,6 @@
 import csv, sys
 sys.path.insert(0,'/root/repo/fast-cwdm_amd')
-rows=[r for r in csv.DictReader(open(sys.argv[1])) if 'conv3d_kernel' in r['Kernel_Name']]
+rows=[r for r in csv.DictReader(open(sys.argv[1])) if ('conv3d_kernel' in r['Kernel_Name'] or 'conv3d_wide_kernel' in r['Kernel_Name'])]
 # last forward = last 72 conv launches
 last=rows[-72:]
 from cwdm_hip.unet_runtime import UNetPlan
