@@ -122,6 +122,9 @@ struct Stager {
   static constexpr int NI = (HV + 127) / 128;
   u32x4 r[NI];
   unsigned ok;
+  int vox[NI];          // cached source voxel index per halo item (segment A)
+  unsigned cache_ok = 0;
+  bool cached = false;
   float sc[EPQ], sh[EPQ];
   const T* base;
   int csrc;
@@ -155,9 +158,35 @@ struct Stager {
     ok = 0;
     if (MODE == 2 && segA) return;
     const bool interior = !segA;
-    const int n = interior ? BX * BY * BZ : HV;
-    const int md = segA ? MODE : 0;
-    const int SD = md == 1 ? p.D >> 1 : p.D, SH = md == 1 ? p.H >> 1 : p.H, SW = md == 1 ? p.W >> 1 : p.W;
+    if (segA) {
+      // source voxel indices of the halo items are chunk-invariant: computed once
+      if (!cached) {
+        cache_ok = 0;
+        const int SD = MODE == 1 ? p.D >> 1 : p.D, SH = MODE == 1 ? p.H >> 1 : p.H, SW = MODE == 1 ? p.W >> 1 : p.W;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int it = (tid >> 1) + 128 * j;
+          vox[j] = 0;
+          if (it < HV) {
+            int hv, hx, hy, hz;
+            coords(it, false, &hv, &hx, &hy, &hz);
+            int ox = x0 + hx - 1, oy = y0 + hy - 1, oz = z0 + hz - 1;
+            if (ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) {
+              if (MODE == 1) { ox >>= 1; oy >>= 1; oz >>= 1; }
+              vox[j] = ((b * SD + oz) * SH + oy) * SW + ox;
+              cache_ok |= 1u << j;
+            }
+          }
+        }
+        cached = true;
+      }
+      ok = cache_ok;
+      // branch-free: out-of-volume items load voxel 0 and are zeroed later
+#pragma unroll
+      for (int j = 0; j < NI; ++j) r[j] = ldg16(base + (long long)vox[j] * csrc);
+      return;
+    }
+    const int n = BX * BY * BZ;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int it = (tid >> 1) + 128 * j;
@@ -165,11 +194,10 @@ struct Stager {
       if (it < n) {
         int hv, hx, hy, hz;
         coords(it, interior, &hv, &hx, &hy, &hz);
-        int ox = x0 + hx - 1, oy = y0 + hy - 1, oz = z0 + hz - 1;
-        if (ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) {
-          if (md == 1) { ox >>= 1; oy >>= 1; oz >>= 1; }
-          const long long vox = (((long long)b * SD + oz) * SH + oy) * SW + ox;
-          r[j] = ldg16(base + vox * csrc);
+        const int ox = x0 + hx - 1, oy = y0 + hy - 1, oz = z0 + hz - 1;
+        if (ox < p.W && oy < p.H && oz < p.D) {
+          const long long v = (((long long)b * p.D + oz) * p.H + oy) * p.W + ox;
+          r[j] = ldg16(base + v * csrc);
           ok |= 1u << j;
         }
       }
@@ -180,30 +208,32 @@ struct Stager {
   template <int J>
   __device__ __forceinline__ void transform_item() {
     if constexpr (J < NI) {
-      if (!(GN && seg_a) || MODE == 2) return;
-      if ((ok >> J) & 1) {
+      if (MODE == 2 || !seg_a) return;
+      // mask as data, not control flow: keeps the VALU stream branch-free so it
+      // can interleave with the MFMAs
+      const unsigned keep = 0u - ((ok >> J) & 1u);
+      if (GN) {
+        const float onf = __uint_as_float(keep & 0x3f800000u);  // 1.0f or 0.0f
         float f[EPQ];
         unpack<T>(r[J], f);
 #pragma unroll
-        for (int e = 0; e < EPQ; ++e) f[e] = silu(f[e] * sc[e] + sh[e]);
+        for (int e = 0; e < EPQ; ++e) f[e] = silu(f[e] * sc[e] + sh[e]) * onf;
         r[J] = pack<T>(f);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[J][k] &= keep;
       }
     }
   }
 
-  // in-place GroupNorm+SiLU of the fetched registers (MODE 0/1 only)
+  // in-place GroupNorm+SiLU (and zeroing of out-of-volume items) of the
+  // fetched registers, segment A, MODE 0/1
   __device__ __forceinline__ void transform() {
-    if (!(GN && seg_a) || MODE == 2) return;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      if ((ok >> j) & 1) {
-        float f[EPQ];
-        unpack<T>(r[j], f);
-#pragma unroll
-        for (int e = 0; e < EPQ; ++e) f[e] = silu(f[e] * sc[e] + sh[e]);
-        r[j] = pack<T>(f);
-      }
-    }
+    transform_item<0>(); transform_item<1>(); transform_item<2>(); transform_item<3>();
+    transform_item<4>(); transform_item<5>(); transform_item<6>(); transform_item<7>();
+    transform_item<8>(); transform_item<9>(); transform_item<10>(); transform_item<11>();
+    transform_item<12>(); transform_item<13>(); transform_item<14>(); transform_item<15>();
+    static_assert(NI <= 16, "transform unroll");
   }
 
   // write already-transformed registers; SWZ selects the XOR-swizzled image
@@ -257,7 +287,10 @@ struct Stager {
           }
         } else {
           unpack<T>(r[j], f);
-          if (GN && seg_a && ((ok >> j) & 1)) {
+          if (!((ok >> j) & 1)) {
+#pragma unroll
+            for (int e = 0; e < EPQ; ++e) f[e] = 0.f;  // out-of-volume (zero padding)
+          } else if (GN && seg_a) {
 #pragma unroll
             for (int e = 0; e < EPQ; ++e) f[e] = silu(f[e] * sc[e] + sh[e]);
           }
@@ -795,41 +828,49 @@ __global__ void __launch_bounds__(256) conv3d_wide_kernel(ConvParams p) {
     }
     __syncthreads();
   }
-  for (int gc = g0; gc < g1; ++gc) {
-    const bool segA = gc < nA;
-    const bool has_next = gc + 1 < g1;
-    unsigned char* wcur = wbuf0 + ((gc - g0) & 1) * C::WB;
-    if (has_next) {
-      int wb;
-      const unsigned char* wsp = wsrc(gc + 1, &wb);
-      stage_weights(wbuf0 + ((gc + 1 - g0) & 1) * C::WB, wsp, wb, tid);
-      sg.fetch(p, gc + 1 < nA, gc + 1 < nA ? gc + 1 : gc + 1 - nA, b, x0, y0, z0, tid);
-    }
-    const unsigned char* w_lane = wcur + w_lane_off;
-    if (segA) {
-      // the next chunk's GN+SiLU runs between the MFMA groups (VALU issues in
-      // the MFMA gaps of the same wave)
-      wide_slab_x<T, NF, -1>(acc, halo_lane, w_lane, &sg, has_next);
-      wide_slab_x<T, NF, 0>(acc, halo_lane, w_lane, &sg, has_next);
-      wide_slab_x<T, NF, 1>(acc, halo_lane, w_lane, &sg, has_next);
-    } else {
-      // 1x1 segment: centre tap only (its weights are tap 0 of the chunk)
-      u32x4 a[4], bq[NF];
-#pragma unroll
-      for (int L = 0; L < 4; ++L) a[L] = *reinterpret_cast<const u32x4*>(halo_lane + (L * C::HX) * 32);
-#pragma unroll
-      for (int n = 0; n < NF; ++n) bq[n] = *reinterpret_cast<const u32x4*>(w_lane + (n * 32) * 32);
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < NF; ++n) mfma_acc(acc[m][n], a[m], bq[n], (T*)nullptr);
-      if (has_next) sg.transform();
-    }
-    if (!has_next) break;
+  // staging of chunk gc+1 (LDS-DMA weights + halo registers) overlaps chunk gc's MFMAs
+  auto prefetch = [&](int gn) {
+    int wb;
+    const unsigned char* wsp = wsrc(gn, &wb);
+    stage_weights(wbuf0 + ((gn - g0) & 1) * C::WB, wsp, wb, tid);
+    sg.fetch(p, gn < nA, gn < nA ? gn : gn - nA, b, x0, y0, z0, tid);
+  };
+  auto commit = [&](bool has_next) {
     __syncthreads();  // all waves done with this chunk's halo and weights
-    if constexpr (MODE == 2) sg.template store<false>(halo, p, b, x0, y0, z0, tid);
-    else sg.template write<false>(halo, tid);
+    if (has_next) {
+      if constexpr (MODE == 2) sg.template store<false>(halo, p, b, x0, y0, z0, tid);
+      else sg.template write<false>(halo, tid);
+    }
     __syncthreads();  // (drains the LDS-DMA of the next weights as well)
+  };
+  // 3x3x3 segment: straight-line body, acc stays in the accumulator registers
+  const int gA1 = min(g1, nA);
+  for (int gc = g0; gc < gA1; ++gc) {
+    const bool has_next = gc + 1 < g1;
+    if (has_next) prefetch(gc + 1);
+    const unsigned char* w_lane = wbuf0 + ((gc - g0) & 1) * C::WB + w_lane_off;
+    // the next chunk's GN+SiLU runs between the MFMA groups (VALU issues in the
+    // MFMA gaps of the same wave)
+    wide_slab_x<T, NF, -1>(acc, halo_lane, w_lane, &sg, has_next);
+    wide_slab_x<T, NF, 0>(acc, halo_lane, w_lane, &sg, has_next);
+    wide_slab_x<T, NF, 1>(acc, halo_lane, w_lane, &sg, has_next);
+    commit(has_next);
+  }
+  // 1x1 segment (skip_connection): centre tap only, weights = tap 0 of the chunk
+  for (int gc = max(g0, nA); gc < g1; ++gc) {
+    const bool has_next = gc + 1 < g1;
+    if (has_next) prefetch(gc + 1);
+    const unsigned char* w_lane = wbuf0 + ((gc - g0) & 1) * C::WB + w_lane_off;
+    u32x4 a[4], bq[NF];
+#pragma unroll
+    for (int L = 0; L < 4; ++L) a[L] = *reinterpret_cast<const u32x4*>(halo_lane + (L * C::HX) * 32);
+#pragma unroll
+    for (int n = 0; n < NF; ++n) bq[n] = *reinterpret_cast<const u32x4*>(w_lane + (n * 32) * 32);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < NF; ++n) mfma_acc(acc[m][n], a[m], bq[n], (T*)nullptr);
+    commit(has_next);
   }
 
   __syncthreads();
