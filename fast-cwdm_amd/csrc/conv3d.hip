@@ -22,7 +22,7 @@ extern template int launch_conv<float, 8, 8, 4, 2>(const ConvParams&, hipStream_
 // ---- weight packing: OIDHW fp32 -> [ct][chunk][tap][n][2 quads, swizzled] ----
 template <typename T>
 __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, int cout, int cin, int ntaps, int NT,
-                                                   int nct, T* __restrict__ out) {
+                                                   int nct, T* __restrict__ out, int transpose) {
   constexpr int CK = ConvTr<T>::CK, EPQ = ConvTr<T>::EPQ;
   const int nch = cin / CK;
   const long long total = (long long)nct * nch * ntaps * NT * CK;
@@ -41,7 +41,12 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, 
   const int q = qp ^ ((n >> 3) & 1);
   const int co = ct * NT + n, ci = chunk * CK + q * EPQ + e;
   float v = 0.f;
-  if (co < cout) v = w[((long long)co * cin + ci) * ntaps + tap];
+  // transpose: pack the input-gradient conv of a (cin -> cout) conv, i.e. weights
+  // W'[co'=ci][ci'=co][tap] = W[co][ci][ntaps-1-tap] (w is then cin x cout OIDHW)
+  if (co < cout) {
+    if (transpose) v = w[((long long)ci * cout + co) * ntaps + (ntaps - 1 - tap)];
+    else v = w[((long long)co * cin + ci) * ntaps + tap];
+  }
   out[i] = Elem<T>::from_f(v);
 }
 
@@ -80,8 +85,22 @@ extern "C" int64_t cwdm_conv3d_packed_bytes(int cout, int cin, int ksize, int dt
   return (int64_t)nct * (cin / ck) * ntaps * NT * ck * esz;
 }
 
+static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, void* packed, int transpose,
+                     cwdm_stream_t stream);
+
 extern "C" int cwdm_conv3d_pack(const float* w, int cout, int cin, int ksize, int dtype, void* packed,
                                 cwdm_stream_t stream) {
+  return pack_impl(w, cout, cin, ksize, dtype, packed, 0, stream);
+}
+
+extern "C" int cwdm_conv3d_pack_dgrad(const float* w, int cout, int cin, int ksize, int dtype, void* packed,
+                                      cwdm_stream_t stream) {
+  // the dgrad conv maps cout channels back to cin: packed as a (cout -> cin) conv
+  return pack_impl(w, cin, cout, ksize, dtype, packed, 1, stream);
+}
+
+static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, void* packed, int transpose,
+                     cwdm_stream_t stream) {
   CWDM_REQUIRE(w && packed, CWDM_E_INVALID, "cwdm_conv3d_pack: null pointer");
   CWDM_REQUIRE(ksize == 1 || ksize == 3, CWDM_E_UNSUPPORTED, "cwdm_conv3d_pack: kernel size must be 1 or 3");
   CWDM_REQUIRE(dtype == CWDM_F32 || dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_conv3d_pack: bad dtype");
@@ -95,10 +114,10 @@ extern "C" int cwdm_conv3d_pack(const float* w, int cout, int cin, int ksize, in
   dim3 grid((unsigned)ceil_div(total, 256));
   if (dtype == CWDM_BF16)
     hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, w, cout, cin, ntaps, NT, nct,
-                       reinterpret_cast<bf16_t*>(packed));
+                       reinterpret_cast<bf16_t*>(packed), transpose);
   else
     hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, w, cout, cin, ntaps, NT, nct,
-                       reinterpret_cast<float*>(packed));
+                       reinterpret_cast<float*>(packed), transpose);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }
@@ -131,12 +150,13 @@ extern "C" int64_t cwdm_conv3d_parts(int dtype, int64_t D, int64_t H, int64_t W,
 }
 
 extern "C" int cwdm_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream) {
-  CWDM_REQUIRE(d && d->a0 && d->a_w && d->out && d->bias, CWDM_E_INVALID, "cwdm_conv3d_forward: null pointer");
+  CWDM_REQUIRE(d && d->out && (d->a_w || d->b_w), CWDM_E_INVALID, "cwdm_conv3d_forward: null pointer");
+  CWDM_REQUIRE(!d->a_w || (d->a0 && d->a_c0 > 0), CWDM_E_INVALID, "cwdm_conv3d_forward: segment A input missing");
   CWDM_REQUIRE(d->dtype == CWDM_F32 || d->dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_conv3d_forward: bad dtype");
   CWDM_REQUIRE(d->B > 0 && d->D > 0 && d->H > 0 && d->W > 0 && d->cout > 0, CWDM_E_SHAPE,
                "cwdm_conv3d_forward: empty shape");
   const int ck = ck_of(d->dtype);
-  CWDM_REQUIRE(d->a_c0 > 0 && d->a_c0 % ck == 0 && d->a_c1 % ck == 0 && (d->a_c1 == 0 || d->a1), CWDM_E_UNSUPPORTED,
+  CWDM_REQUIRE(!d->a_w || (d->a_c0 % ck == 0 && d->a_c1 % ck == 0 && (d->a_c1 == 0 || d->a1)), CWDM_E_UNSUPPORTED,
                "cwdm_conv3d_forward: segment A channels must be multiples of " + std::to_string(ck));
   if (d->b_w)
     CWDM_REQUIRE(d->b0 && d->b_c0 > 0 && d->b_c0 % ck == 0 && d->b_c1 % ck == 0 && (d->b_c1 == 0 || d->b1),
@@ -164,6 +184,13 @@ extern "C" int cwdm_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stre
   p.res = d->res; p.rmode = d->res_mode;
   p.out = d->out; p.out_f32 = (d->out_dtype == CWDM_F32 && d->dtype != CWDM_F32) ? 1 : (d->dtype == CWDM_F32);
   p.stats = d->stats;
+  p.out1 = d->out1;
+  p.out_c0 = d->out_c0;
+  p.accumulate = d->accumulate;
+  if (!d->a_w) { p.ac0 = 0; p.ac1 = 0; p.a0 = nullptr; p.a1 = nullptr; }
+  if (d->out1)
+    CWDM_REQUIRE(d->out_c0 > 0 && d->out_c0 < d->cout && d->out_c0 % (32 * nf) == 0, CWDM_E_UNSUPPORTED,
+                 "cwdm_conv3d_forward: dual-output split must be a multiple of the channel tile");
   p.ksplit = 1;
   p.partial = nullptr;
   if (pl.S > 1 && d->workspace && d->ws_bytes >= pl.ws) {

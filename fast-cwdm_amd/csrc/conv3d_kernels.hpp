@@ -43,6 +43,8 @@ struct ConvParams {
   const void* res; int rmode;
   void* out; int out_f32;
   float* stats;
+  void* out1; int out_c0;  // dual output: channels >= out_c0 go to out1 (stride cout - out_c0)
+  int accumulate;          // out += result (gradient accumulation)
   int ksplit;       // K split factor S (1 = none)
   float* partial;   // [S][B*D*H*W][cout] fp32 partial sums when S > 1
 };
@@ -328,7 +330,7 @@ __device__ __forceinline__ void epilogue_rows(const ConvParams& p, float* E, int
   for (int e = 0; e < 8; ++e) {
     bsum[e] = 0.f;
     bsq[e] = 0.f;
-    bias[e] = (e < nvalid) ? p.bias[(long long)b * p.bias_bs + cbase + e] : 0.f;
+    bias[e] = (e < nvalid && p.bias) ? p.bias[(long long)b * p.bias_bs + cbase + e] : 0.f;
   }
   // residuals of every row this thread owns are loaded first, so their HBM
   // latency overlaps (same-grid / upsampled residual, full 8-channel groups)
@@ -399,13 +401,33 @@ __device__ __forceinline__ void epilogue_rows(const ConvParams& p, float* E, int
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = rv[e] + v[e];
     }
+    // output tensor / channel stride (dual output splits the channels at out_c0)
+    void* obase = p.out;
+    int ostride = p.cout, oc = cbase;
+    if (p.out1 && cbase >= p.out_c0) {
+      obase = p.out1;
+      ostride = p.cout - p.out_c0;
+      oc = cbase - p.out_c0;
+    } else if (p.out1) {
+      ostride = p.out_c0;
+    }
     if (p.out_f32) {
-      float* o = reinterpret_cast<float*>(p.out) + vox * p.cout + cbase;
+      float* o = reinterpret_cast<float*>(obase) + vox * ostride + oc;
+      if (p.accumulate) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (e < nvalid) v[e] += o[e];
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         if (e < nvalid) o[e] = v[e];
     } else {
-      T* o = reinterpret_cast<T*>(p.out) + vox * p.cout + cbase;
+      T* o = reinterpret_cast<T*>(obase) + vox * ostride + oc;
+      if (p.accumulate) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (e < nvalid) v[e] += Elem<T>::to_f(o[e]);
+      }
       if (nvalid == 8) {
         if constexpr (sizeof(T) == 2) {
           *reinterpret_cast<u32x4*>(o) = pack<bf16_t>(v);

@@ -12,7 +12,8 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restric
                                                          const float* __restrict__ s1, long long p1, int c1,
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, int groups,
-                                                         long long voxels, float eps, float* __restrict__ out) {
+                                                         long long voxels, float eps, float* __restrict__ out,
+                                                         float* __restrict__ mean_rstd) {
   const int g = blockIdx.x, b = blockIdx.y;
   const int C = c0 + c1, cpg = C / groups;
   __shared__ double rs[256], rq[256];
@@ -47,6 +48,10 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restric
   if (var < 0) var = 0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   const float meanf = (float)mean;
+  if (mean_rstd && threadIdx.x == 0) {
+    mean_rstd[((long long)b * groups + g) * 2 + 0] = meanf;
+    mean_rstd[((long long)b * groups + g) * 2 + 1] = rstd;
+  }
   for (int ci = threadIdx.x; ci < cpg; ci += 256) {
     const int c = g * cpg + ci;
     const float sc = gamma[c] * rstd;
@@ -62,14 +67,15 @@ using namespace cwdm;
 
 extern "C" int cwdm_gn_finalize(const float* s0, int64_t p0, int c0, const float* s1, int64_t p1, int c1,
                                 const float* gamma, const float* beta, int groups, int64_t B, int64_t voxels,
-                                float eps, float* out, cwdm_stream_t stream) {
+                                float eps, float* out, float* mean_rstd, cwdm_stream_t stream) {
   CWDM_REQUIRE(s0 && gamma && beta && out, CWDM_E_INVALID, "cwdm_gn_finalize: null pointer");
   CWDM_REQUIRE(c1 == 0 || s1, CWDM_E_INVALID, "cwdm_gn_finalize: second source missing");
   CWDM_REQUIRE(groups > 0 && (c0 + c1) % groups == 0, CWDM_E_SHAPE,
                "cwdm_gn_finalize: channels must be divisible by num_groups");
   CWDM_REQUIRE(B > 0 && B < 65536 && voxels > 0, CWDM_E_SHAPE, "cwdm_gn_finalize: bad batch/voxels");
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, (unsigned)B), dim3(256), 0, (hipStream_t)stream, s0,
-                     (long long)p0, c0, s1, (long long)p1, c1, gamma, beta, groups, (long long)voxels, eps, out);
+                     (long long)p0, c0, s1, (long long)p1, c1, gamma, beta, groups, (long long)voxels, eps, out,
+                     mean_rstd);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }

@@ -282,7 +282,7 @@ void build(cwdm_unet* u) {
 struct Layout {
   int64_t temb, ebias, split, split_bytes;
   std::vector<int64_t> t_off, s_off, s_parts;
-  std::vector<int64_t> ss_off;
+  std::vector<int64_t> ss_off, mr_off;
   int64_t total;
 };
 
@@ -325,6 +325,7 @@ Layout layout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
     L.s_off.push_back(take(B * parts * t.channels * 2 * 4));
   }
   for (const auto& g : u->gns) L.ss_off.push_back(take(B * (int64_t)g.channels * 2 * 4));
+  for (size_t i = 0; i < u->gns.size(); ++i) L.mr_off.push_back(take(B * (int64_t)u->cfg.num_groups * 2 * 4));
   int64_t split = 0;
   for (const auto& cs : u->convs) {
     cwdm_conv3d_desc d = conv_shape(u, cs, B, D, H, W);
@@ -514,7 +515,7 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
                                  g.src1 >= 0 ? reinterpret_cast<const float*>(wb + L.s_off[g.src1]) : nullptr,
                                  g.src1 >= 0 ? L.s_parts[g.src1] : 0, c1, P(g.gamma_off), P(g.beta_off),
                                  u->cfg.num_groups, B, vox, 1e-5f, reinterpret_cast<float*>(wb + L.ss_off[g.ss_id]),
-                                 stream)))
+                                 reinterpret_cast<float*>(wb + L.mr_off[g.ss_id]), stream)))
         return rc;
       continue;
     }

@@ -54,6 +54,8 @@ class ConvDesc(ctypes.Structure):
         ("out", vp), ("out_dtype", ctypes.c_int),
         ("stats", vp),
         ("workspace", vp), ("ws_bytes", i64),
+        ("out1", vp), ("out_c0", ctypes.c_int),
+        ("accumulate", ctypes.c_int),
     ]
 
 
@@ -79,11 +81,12 @@ _PROTOS = {
                                   i64, i64, i64, vp]),
     "cwdm_conv3d_packed_bytes": (i64, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "cwdm_conv3d_pack": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]),
+    "cwdm_conv3d_pack_dgrad": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]),
     "cwdm_conv3d_parts": (i64, [ctypes.c_int, i64, i64, i64, ctypes.c_int]),
     "cwdm_conv3d_forward": (ctypes.c_int, [ctypes.POINTER(ConvDesc), vp]),
     "cwdm_conv3d_workspace_bytes": (i64, [ctypes.POINTER(ConvDesc)]),
     "cwdm_gn_finalize": (ctypes.c_int, [vp, i64, ctypes.c_int, vp, i64, ctypes.c_int, vp, vp, ctypes.c_int, i64, i64,
-                                        ctypes.c_float, vp, vp]),
+                                        ctypes.c_float, vp, vp, vp]),
     "cwdm_gn_silu_pool": (ctypes.c_int, [vp, ctypes.c_int, vp, i64, i64, i64, i64, ctypes.c_int, vp, vp, vp]),
     "cwdm_unet_create": (ctypes.c_int, [ctypes.POINTER(UNetConfig), ctypes.POINTER(vp)]),
     "cwdm_unet_destroy": (None, [vp]),

@@ -130,6 +130,8 @@ int cwdm_copy3(const void* src, int src_dtype, const int64_t* src_s /* [3] */,
  * stats: NULL or device [B][parts][cout][2] fp32 per-tile (sum, sum^2) of the
  * stored output, for the next GroupNorm (parts from cwdm_conv3d_parts).
  * Weights are packed once by cwdm_conv3d_pack from PyTorch OIDHW fp32.
+ * a_w may be NULL when b_w is set (a pure 1x1 conv, e.g. the skip dgrad);
+ * bias may be NULL (zero).
  * ------------------------------------------------------------------------- */
 typedef struct {
   int dtype;
@@ -148,10 +150,18 @@ typedef struct {
   void* out; int out_dtype;
   float* stats;
   void* workspace; int64_t ws_bytes; /* split-K partials for small grids (optional) */
+  void* out1; int out_c0;   /* optional second output: channels >= out_c0 (the two halves of a
+                               concat input's gradient) */
+  int accumulate;           /* out += result instead of out = result */
 } cwdm_conv3d_desc;
 int64_t cwdm_conv3d_packed_bytes(int cout, int cin, int ksize, int dtype);
 int cwdm_conv3d_pack(const float* w_oidhw, int cout, int cin, int ksize, int dtype,
                      void* packed, cwdm_stream_t stream);
+/* Packs the input-gradient (dgrad) conv of a (cin -> cout) conv: a (cout -> cin)
+ * conv with spatially flipped, transposed weights (the backward of Conv3d's
+ * input, stride 1, pad 1).  Size: cwdm_conv3d_packed_bytes(cin, cout, ksize, dtype). */
+int cwdm_conv3d_pack_dgrad(const float* w_oidhw, int cout, int cin, int ksize, int dtype,
+                           void* packed, cwdm_stream_t stream);
 int64_t cwdm_conv3d_parts(int dtype, int64_t D, int64_t H, int64_t W, int cout);
 /* Workspace that lets cwdm_conv3d_forward split K over workgroups on small
  * grids (0 when it would not split; without it the launch runs unsplit). */
@@ -166,7 +176,8 @@ int cwdm_gn_finalize(const float* stats0, int64_t parts0, int c0,
                      const float* stats1, int64_t parts1, int c1,
                      const float* gamma, const float* beta, int groups,
                      int64_t B, int64_t voxels, float eps,
-                     float* scale_shift, cwdm_stream_t stream);
+                     float* scale_shift, float* mean_rstd /* optional [B][groups][2] */,
+                     cwdm_stream_t stream);
 
 /* Down-ResBlock pre-pass: h = AvgPool2(SiLU(x*scale+shift)), x_upd = AvgPool2(x)
  * (ResBlock._forward with down=True, guided_diffusion/unet.py:286-291,

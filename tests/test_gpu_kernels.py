@@ -243,7 +243,7 @@ def test_gn_finalize_matches_group_norm():
     out = torch.empty(B, C0 + C1, 2, device=DEV)
     check(lib().cwdm_gn_finalize(ctypes.c_void_p(s0.data_ptr()), parts, C0, ctypes.c_void_p(s1.data_ptr()), parts, C1,
                                  ctypes.c_void_p(gamma.data_ptr()), ctypes.c_void_p(beta.data_ptr()), G, B,
-                                 D * H * W, 1e-5, ctypes.c_void_p(out.data_ptr()), None))
+                                 D * H * W, 1e-5, ctypes.c_void_p(out.data_ptr()), None, None))
     o = out.cpu()
     y = x * o[..., 0][:, :, None, None, None] + o[..., 1][:, :, None, None, None]
     ref = F.group_norm(x, G, gamma.cpu(), beta.cpu(), eps=1e-5)
