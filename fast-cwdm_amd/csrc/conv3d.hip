@@ -22,7 +22,7 @@ extern template int launch_conv<float, 8, 8, 4, 2>(const ConvParams&, hipStream_
 // ---- weight packing: OIDHW fp32 -> [ct][chunk][tap][n][2 quads, swizzled] ----
 template <typename T>
 __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, int cout, int cin, int ntaps, int NT,
-                                                   int nct, T* __restrict__ out, int transpose) {
+                                                   int nct, T* __restrict__ out, int transpose, int cin_real) {
   constexpr int CK = ConvTr<T>::CK, EPQ = ConvTr<T>::EPQ;
   const int nch = cin / CK;
   const long long total = (long long)nct * nch * ntaps * NT * CK;
@@ -43,7 +43,7 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, 
   float v = 0.f;
   // transpose: pack the input-gradient conv of a (cin -> cout) conv, i.e. weights
   // W'[co'=ci][ci'=co][tap] = W[co][ci][ntaps-1-tap] (w is then cin x cout OIDHW)
-  if (co < cout) {
+  if (co < cout && ci < cin_real) {
     if (transpose) v = w[((long long)ci * cout + co) * ntaps + (ntaps - 1 - tap)];
     else v = w[((long long)co * cin + ci) * ntaps + tap];
   }
@@ -96,6 +96,8 @@ extern "C" int cwdm_conv3d_pack(const float* w, int cout, int cin, int ksize, in
 extern "C" int cwdm_conv3d_pack_dgrad(const float* w, int cout, int cin, int ksize, int dtype, void* packed,
                                       cwdm_stream_t stream) {
   // the dgrad conv maps cout channels back to cin: packed as a (cout -> cin) conv
+  // (its input channels are padded with zeros up to the chunk size, e.g. the
+  // 8-channel output head)
   return pack_impl(w, cin, cout, ksize, dtype, packed, 1, stream);
 }
 
@@ -105,6 +107,8 @@ static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, vo
   CWDM_REQUIRE(ksize == 1 || ksize == 3, CWDM_E_UNSUPPORTED, "cwdm_conv3d_pack: kernel size must be 1 or 3");
   CWDM_REQUIRE(dtype == CWDM_F32 || dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_conv3d_pack: bad dtype");
   const int ck = ck_of(dtype);
+  const int cin_real = cin;
+  if (transpose) cin = (int)ceil_div(cin, ck) * ck;
   CWDM_REQUIRE(cin % ck == 0, CWDM_E_UNSUPPORTED,
                "cwdm_conv3d_pack: input channels must be a multiple of " + std::to_string(ck));
   const int NT = 32 * pick_nf(cout);
@@ -114,10 +118,10 @@ static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, vo
   dim3 grid((unsigned)ceil_div(total, 256));
   if (dtype == CWDM_BF16)
     hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, w, cout, cin, ntaps, NT, nct,
-                       reinterpret_cast<bf16_t*>(packed), transpose);
+                       reinterpret_cast<bf16_t*>(packed), transpose, cin_real);
   else
     hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, w, cout, cin, ntaps, NT, nct,
-                       reinterpret_cast<float*>(packed), transpose);
+                       reinterpret_cast<float*>(packed), transpose, cin_real);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }
@@ -189,8 +193,8 @@ extern "C" int cwdm_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stre
   p.accumulate = d->accumulate;
   if (!d->a_w) { p.ac0 = 0; p.ac1 = 0; p.a0 = nullptr; p.a1 = nullptr; }
   if (d->out1)
-    CWDM_REQUIRE(d->out_c0 > 0 && d->out_c0 < d->cout && d->out_c0 % (32 * nf) == 0, CWDM_E_UNSUPPORTED,
-                 "cwdm_conv3d_forward: dual-output split must be a multiple of the channel tile");
+    CWDM_REQUIRE(d->out_c0 > 0 && d->out_c0 < d->cout && d->out_c0 % 8 == 0, CWDM_E_UNSUPPORTED,
+                 "cwdm_conv3d_forward: dual-output split must be a multiple of 8 channels");
   p.ksplit = 1;
   p.partial = nullptr;
   if (pl.S > 1 && d->workspace && d->ws_bytes >= pl.ws) {

@@ -1,0 +1,570 @@
+// Backward kernels of the U-Net ResBlock path besides the convolutions
+// (training, guided_diffusion/train_util.py:396-462 -> loss.backward()):
+//   * SiLU(GroupNorm(x)) backward (nn.py:17-19, :93-100) with the adjoint of
+//     the resampling that followed it in the forward (upsample / AvgPool2),
+//     in three passes: per-block channel partials of (sum dz, sum dz*xhat),
+//     an fp64 finalize into per-(b, c) affine coefficients + dgamma/dbeta,
+//     and an elementwise apply that recomputes dz;
+//   * the residual-path resample adjoint, per-channel sums (bias and emb
+//     gradients), the timestep-embedding MLP / emb-projection backward;
+//   * the AdamW step (torch.optim.AdamW, train_util.py:111).
+#include <cmath>
+#include <type_traits>
+
+#include "common.hpp"
+
+namespace cwdm {
+namespace {
+
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+
+template <typename T> __device__ __forceinline__ void load8(const T* p, float* f);
+template <> __device__ __forceinline__ void load8<float>(const float* p, float* f) {
+  const u4 a = *reinterpret_cast<const u4*>(p), b = *reinterpret_cast<const u4*>(p + 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { f[i] = __uint_as_float(a[i]); f[4 + i] = __uint_as_float(b[i]); }
+}
+template <> __device__ __forceinline__ void load8<bf16_t>(const bf16_t* p, float* f) {
+  const u4 a = *reinterpret_cast<const u4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(a[i] << 16); f[2 * i + 1] = __uint_as_float(a[i] & 0xffff0000u); }
+}
+template <typename T> __device__ __forceinline__ void store8(T* p, const float* f);
+template <> __device__ __forceinline__ void store8<float>(float* p, const float* f) {
+  u4 a, b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { a[i] = __float_as_uint(f[i]); b[i] = __float_as_uint(f[4 + i]); }
+  *reinterpret_cast<u4*>(p) = a;
+  *reinterpret_cast<u4*>(p + 4) = b;
+}
+template <> __device__ __forceinline__ void store8<bf16_t>(bf16_t* p, const float* f) {
+  u4 a;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[i] = (unsigned)f2bf(f[2 * i]) | ((unsigned)f2bf(f[2 * i + 1]) << 16);
+  *reinterpret_cast<u4*>(p) = a;
+}
+
+// gradient of the SiLU output at voxel (z, y, x) of the GN grid, channels [c, c+8).
+// MODE is a template parameter: with a runtime three-way branch here the
+// gfx950 compiler (ROCm 7.2 clang) dropped the channel offset on the MODE-2
+// path of resample_add (an undefined register in the address -> aperture
+// violation), so every caller is instantiated per mode.
+template <typename T, int MODE>
+__device__ __forceinline__ void load_du(const T* du, int C, int c, int b, int z, int y, int x, int d, int h, int w,
+                                        float* f) {
+  constexpr int mode = MODE;
+  if constexpr (mode == 0) {
+    load8<T>(du + ((((long long)b * d + z) * h + y) * w + x) * C + c, f);
+  } else if constexpr (mode == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = 0.f;
+    const int D2 = 2 * d, H2 = 2 * h, W2 = 2 * w;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float g[8];
+      load8<T>(du + ((((long long)b * D2 + 2 * z + (k >> 2)) * H2 + 2 * y + ((k >> 1) & 1)) * W2 + 2 * x + (k & 1)) * C + c,
+               g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] += g[e];
+    }
+  } else {
+    load8<T>(du + ((((long long)b * (d >> 1) + (z >> 1)) * (h >> 1) + (y >> 1)) * (w >> 1) + (x >> 1)) * C + c, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] *= 0.125f;
+  }
+}
+
+// d/dz SiLU(z) * du
+__device__ __forceinline__ float dsilu(float z, float du) {
+  const float s = 1.0f / (1.0f + expf(-z));
+  return du * (s * (1.0f + z * (1.0f - s)));
+}
+
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) gn_bwd_reduce_kernel(const T* __restrict__ x0, int c0, const T* __restrict__ x1,
+                                                           int c1, const T* __restrict__ du,
+                                                           const float* __restrict__ ss,
+                                                           const float* __restrict__ mr, int groups, int d, int h,
+                                                           int w, long long vpb, float* __restrict__ part) {
+  __shared__ float red[256 * 16];
+  const int C = c0 + c1, ncg = C >> 3, nslots = 256 / ncg;
+  const int b = blockIdx.y, blk = blockIdx.x, nblk = gridDim.x;
+  const int cg = threadIdx.x % ncg, slot = threadIdx.x / ncg;
+  const long long V = (long long)d * h * w;
+  const int c = cg * 8, cpg = C / groups;
+  float A[8], Bs[8], sc[8], sh[8], mu[8], rs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    A[e] = 0.f; Bs[e] = 0.f;
+    sc[e] = ss[((long long)b * C + c + e) * 2];
+    sh[e] = ss[((long long)b * C + c + e) * 2 + 1];
+    const int g = (c + e) / cpg;
+    mu[e] = mr[((long long)b * groups + g) * 2];
+    rs[e] = mr[((long long)b * groups + g) * 2 + 1];
+  }
+  const T* xs = c < c0 ? x0 : x1;
+  const int xc = c < c0 ? c0 : c1, xo = c < c0 ? c : c - c0;
+  if (slot < nslots) {
+    const long long v0 = blk * vpb, v1 = v0 + vpb < V ? v0 + vpb : V;
+    for (long long v = v0 + slot; v < v1; v += nslots) {
+      const int x = (int)(v % w), y = (int)((v / w) % h), z = (int)(v / ((long long)w * h));
+      float xv[8], g[8];
+      load8<T>(xs + ((long long)b * V + v) * xc + xo, xv);
+      load_du<T, MODE>(du, C, c, b, z, y, x, d, h, w, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dz = dsilu(xv[e] * sc[e] + sh[e], g[e]);
+        A[e] += dz;
+        Bs[e] += dz * ((xv[e] - mu[e]) * rs[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[threadIdx.x * 16 + e] = slot < nslots ? A[e] : 0.f;
+    red[threadIdx.x * 16 + 8 + e] = slot < nslots ? Bs[e] : 0.f;
+  }
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < C; cc += 256) {
+    const int g8 = cc >> 3, e = cc & 7;
+    float sa = 0.f, sb = 0.f;
+    for (int s = 0; s < nslots; ++s) {
+      sa += red[(s * ncg + g8) * 16 + e];
+      sb += red[(s * ncg + g8) * 16 + 8 + e];
+    }
+    part[(((long long)b * nblk + blk) * C + cc) * 2] = sa;
+    part[(((long long)b * nblk + blk) * C + cc) * 2 + 1] = sb;
+  }
+}
+
+__global__ void __launch_bounds__(512) gn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C,
+                                                             int B, const float* __restrict__ gamma,
+                                                             const float* __restrict__ mr, int groups,
+                                                             long long V, float* __restrict__ coef,
+                                                             float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ double sA[1024], sB[1024], s1[256], s2[256];
+  const int cpg = C / groups;
+  double dg[2] = {0.0, 0.0}, db[2] = {0.0, 0.0};
+  for (int b = 0; b < B; ++b) {
+    for (int k = 0; k < 2; ++k) {
+      const int c = threadIdx.x + 512 * k;
+      if (c < C) {
+        double a = 0.0, bb = 0.0;
+        for (int i = 0; i < nblk; ++i) {
+          a += (double)part[(((long long)b * nblk + i) * C + c) * 2];
+          bb += (double)part[(((long long)b * nblk + i) * C + c) * 2 + 1];
+        }
+        sA[c] = a; sB[c] = bb;
+        dg[k] += bb; db[k] += a;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < groups) {
+      const int g = threadIdx.x;
+      double a = 0.0, bb = 0.0;
+      for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+        a += (double)gamma[c] * sA[c];
+        bb += (double)gamma[c] * sB[c];
+      }
+      s1[g] = a; s2[g] = bb;
+    }
+    __syncthreads();
+    const double N = (double)cpg * (double)V;
+    for (int c = threadIdx.x; c < C; c += 512) {
+      const int g = c / cpg;
+      const double mu = mr[((long long)b * groups + g) * 2], rs = mr[((long long)b * groups + g) * 2 + 1];
+      const double k1 = rs * gamma[c];
+      const double k2 = -rs * rs * s2[g] / N;
+      const double k3 = -rs * s1[g] / N + rs * rs * s2[g] * mu / N;
+      coef[((long long)b * C + c) * 4 + 0] = (float)k1;
+      coef[((long long)b * C + c) * 4 + 1] = (float)k2;
+      coef[((long long)b * C + c) * 4 + 2] = (float)k3;
+    }
+    __syncthreads();
+  }
+  for (int k = 0; k < 2; ++k) {
+    const int c = threadIdx.x + 512 * k;
+    if (c < C) {
+      dgamma[c] = (float)dg[k];
+      dbeta[c] = (float)db[k];
+    }
+  }
+}
+
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__ x0, int c0, const T* __restrict__ x1,
+                                                          int c1, const T* __restrict__ du,
+                                                          const float* __restrict__ ss,
+                                                          const float* __restrict__ coef, int d, int h, int w,
+                                                          T* __restrict__ dx0, int acc0, T* __restrict__ dx1,
+                                                          int acc1) {
+  const int C = c0 + c1, ncg = C >> 3;
+  const long long V = (long long)d * h * w;
+  const int b = blockIdx.y;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= V * ncg) return;
+  const int cg = (int)(i % ncg);
+  const long long v = i / ncg;
+  const int c = cg * 8;
+  const int x = (int)(v % w), y = (int)((v / w) % h), z = (int)(v / ((long long)w * h));
+  const bool first = c < c0;
+  const T* xs = first ? x0 : x1;
+  T* dx = first ? dx0 : dx1;
+  const int xc = first ? c0 : c1, xo = first ? c : c - c0;
+  const int acc = first ? acc0 : acc1;
+  float xv[8], g[8], o[8];
+  load8<T>(xs + ((long long)b * V + v) * xc + xo, xv);
+  load_du<T, MODE>(du, C, c, b, z, y, x, d, h, w, g);
+  if (acc) load8<T>(dx + ((long long)b * V + v) * xc + xo, o);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const long long bc = (long long)b * C + c + e;
+    const float dz = dsilu(xv[e] * ss[bc * 2] + ss[bc * 2 + 1], g[e]);
+    const float r = coef[bc * 4] * dz + coef[bc * 4 + 1] * xv[e] + coef[bc * 4 + 2];
+    o[e] = acc ? o[e] + r : r;
+  }
+  store8<T>(dx + ((long long)b * V + v) * xc + xo, o);
+}
+
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) resample_add_kernel(T* __restrict__ dst, const T* __restrict__ src, int C,
+                                                          int d, int h, int w, int acc) {
+  const int ncg = C >> 3;
+  const long long V = (long long)d * h * w;
+  const int b = blockIdx.y;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= V * ncg) return;
+  const int c = (int)(i % ncg) * 8;
+  const long long v = i / ncg;
+  const int x = (int)(v % w), y = (int)((v / w) % h), z = (int)(v / ((long long)w * h));
+  float g[8], o[8];
+  load_du<T, MODE>(src, C, c, b, z, y, x, d, h, w, g);
+  T* p = dst + ((long long)b * V + v) * C + c;
+  if (acc) {
+    load8<T>(p, o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] += g[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = g[e];
+  }
+  store8<T>(p, o);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) channel_sum_kernel(const T* __restrict__ src, long long V, int C, int cs,
+                                                         long long vpb, float* __restrict__ out_bc,
+                                                         long long bc_stride, float* __restrict__ out_c,
+                                                         float* __restrict__ out_c2) {
+  __shared__ float red[256 * 8];
+  const int ncg = (C + 7) >> 3, nslots = 256 / ncg;
+  const int b = blockIdx.y, blk = blockIdx.x;
+  const int cg = threadIdx.x % ncg, slot = threadIdx.x / ncg;
+  float a[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = 0.f;
+  if (slot < nslots) {
+    const long long v0 = blk * vpb, v1 = v0 + vpb < V ? v0 + vpb : V;
+    for (long long v = v0 + slot; v < v1; v += nslots) {
+      float f[8];
+      load8<T>(src + ((long long)b * V + v) * cs + cg * 8, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += f[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = slot < nslots ? a[e] : 0.f;
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int k = 0; k < nslots; ++k) s += red[(k * ncg + (c >> 3)) * 8 + (c & 7)];
+    if (out_bc) atomicAdd(out_bc + (long long)b * bc_stride + c, s);
+    if (out_c) atomicAdd(out_c + c, s);
+    if (out_c2) atomicAdd(out_c2 + c, s);
+  }
+}
+
+__global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long long n,
+                                                   float decay, float w1, float b2, float w2, float neg_step,
+                                                   float bc2_sqrt, float eps) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gi = g[i];
+    float pi = p[i] * decay;
+    const float mi = m[i] + w1 * (gi - m[i]);
+    const float vi = v[i] * b2 + w2 * (gi * gi);
+    const float den = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi + neg_step * (mi / den);
+    p[i] = pi; m[i] = mi; v[i] = vi;
+  }
+}
+
+__device__ __forceinline__ float silu_ref(float v) { return v / (1.0f + expf(-v)); }
+__device__ __forceinline__ float dsilu_ref(float z) {
+  const float s = 1.0f / (1.0f + expf(-z));
+  return s * (1.0f + z * (1.0f - s));
+}
+
+// emb projection of one ResBlock (rows [0, n) of the block; dEb stride R)
+__global__ void __launch_bounds__(256) emb_bwd_w_kernel(const float* __restrict__ dEb, int R, int n, int B,
+                                                       const float* __restrict__ temb, int E,
+                                                       float* __restrict__ dw, float* __restrict__ db,
+                                                       float* __restrict__ dcb) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)n * E) return;
+  const int r = (int)(i / E), e = (int)(i % E);
+  float s = 0.f, sb = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float g = dEb[(long long)b * R + r];
+    s += g * silu_ref(temb[(long long)b * E + e]);
+    sb += g;
+  }
+  dw[i] = s;
+  if (e == 0) {
+    db[r] = sb;
+    if (dcb) dcb[r] = sb;
+  }
+}
+
+__global__ void __launch_bounds__(256) emb_bwd_x_kernel(const float* __restrict__ dEb, int R, int n,
+                                                       const float* __restrict__ W, int E,
+                                                       float* __restrict__ dsil) {
+  const int b = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= E) return;
+  float s = 0.f;
+  for (int r = 0; r < n; ++r) s += W[(long long)r * E + e] * dEb[(long long)b * R + r];
+  dsil[(long long)b * E + e] += s;
+}
+
+// time_embed MLP backward (unet.py:534-539): one workgroup, batch looped.
+__global__ void __launch_bounds__(256) temb_bwd_kernel(const float* __restrict__ t, int B, int mc,
+                                                      const float* __restrict__ w1, const float* __restrict__ b1,
+                                                      const float* __restrict__ w2,
+                                                      const float* __restrict__ temb,
+                                                      const float* __restrict__ dsil, float* __restrict__ dw1,
+                                                      float* __restrict__ db1, float* __restrict__ dw2,
+                                                      float* __restrict__ db2) {
+  extern __shared__ float sm[];
+  const int E = 4 * mc, half = mc / 2;
+  float* sinb = sm;                 // [B][mc]
+  float* hid = sinb + B * mc;       // [B][E] pre-activation of layer 1
+  float* dt = hid + B * E;          // [B][E] gradient of temb
+  float* dh = dt + B * E;           // [B][E] gradient of the layer-1 pre-activation
+  for (int b = 0; b < B; ++b) {
+    const float tv = t[b];
+    for (int k = threadIdx.x; k < half; k += blockDim.x) {
+      const float fr = expf(__fdiv_rn(__fmul_rn(-9.210340371976184f, (float)k), (float)half));
+      const float a = __fmul_rn(tv, fr);
+      sinb[b * mc + k] = cosf(a);
+      sinb[b * mc + k + half] = sinf(a);
+    }
+    if ((mc & 1) && threadIdx.x == 0) sinb[b * mc + mc - 1] = 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < B * E; i += blockDim.x) {
+    const int b = i / E, o = i % E;
+    float acc = b1[o];
+    for (int k = 0; k < mc; ++k) acc += w1[(long long)o * mc + k] * sinb[b * mc + k];
+    hid[i] = acc;
+    dt[i] = dsil[i] * dsilu_ref(temb[i]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < B * E; i += blockDim.x) {
+    const int b = i / E, k = i % E;
+    float s = 0.f;
+    for (int o = 0; o < E; ++o) s += w2[(long long)o * E + k] * dt[b * E + o];
+    dh[i] = s * dsilu_ref(hid[i]);
+  }
+  __syncthreads();
+  for (long long i = threadIdx.x; i < (long long)E * E; i += blockDim.x) {
+    const int o = (int)(i / E), k = (int)(i % E);
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dt[b * E + o] * silu_ref(hid[b * E + k]);
+    dw2[i] = s;
+  }
+  for (long long i = threadIdx.x; i < (long long)E * mc; i += blockDim.x) {
+    const int o = (int)(i / mc), k = (int)(i % mc);
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dh[b * E + o] * sinb[b * mc + k];
+    dw1[i] = s;
+  }
+  for (int o = threadIdx.x; o < E; o += blockDim.x) {
+    float s2 = 0.f, s1 = 0.f;
+    for (int b = 0; b < B; ++b) { s2 += dt[b * E + o]; s1 += dh[b * E + o]; }
+    db2[o] = s2;
+    db1[o] = s1;
+  }
+}
+
+template <typename F>
+int dispatch_mode(int mode, F&& f) {
+  if (mode == 0) return f(std::integral_constant<int, 0>{});
+  if (mode == 1) return f(std::integral_constant<int, 1>{});
+  return f(std::integral_constant<int, 2>{});
+}
+
+long long gn_bwd_blocks(int C, long long V) {
+  (void)C;
+  long long nb = ceil_div(V, 512);
+  if (nb > 1024) nb = 1024;
+  if (nb < 1) nb = 1;
+  return nb;
+}
+
+}  // namespace
+
+int launch_emb_bwd(const float* dEb, int R, int n, int B, const float* temb, int E, const float* W, float* dw,
+                   float* db, float* dcb, float* dsil, hipStream_t s) {
+  hipLaunchKernelGGL(emb_bwd_w_kernel, dim3((unsigned)ceil_div((long long)n * E, 256)), dim3(256), 0, s, dEb, R, n,
+                     B, temb, E, dw, db, dcb);
+  CWDM_LAUNCHED();
+  hipLaunchKernelGGL(emb_bwd_x_kernel, dim3((unsigned)ceil_div(E, 256), B), dim3(256), 0, s, dEb, R, n, W, E, dsil);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+int launch_temb_bwd(const float* t, int B, int mc, const float* w1, const float* b1, const float* w2,
+                    const float* temb, const float* dsil, float* dw1, float* db1, float* dw2, float* db2,
+                    hipStream_t s) {
+  const int E = 4 * mc;
+  const size_t sm = (size_t)(B * mc + 3 * B * E) * sizeof(float);
+  CWDM_REQUIRE(sm <= 64 * 1024, CWDM_E_SHAPE, "time_embed backward: batch too large for one workgroup");
+  hipLaunchKernelGGL(temb_bwd_kernel, dim3(1), dim3(256), sm, s, t, B, mc, w1, b1, w2, temb, dsil, dw1, db1, dw2,
+                     db2);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+}  // namespace cwdm
+
+using namespace cwdm;
+
+extern "C" int64_t cwdm_gn_silu_bwd_workspace_bytes(int C, int64_t B, int64_t d, int64_t h, int64_t w) {
+  if (C <= 0 || B <= 0 || d <= 0 || h <= 0 || w <= 0) return -1;
+  const long long nb = gn_bwd_blocks(C, d * h * w);
+  const int64_t part = B * nb * C * 2 * 4;
+  return (part + 255) / 256 * 256 + B * (int64_t)C * 4 * 4;
+}
+
+extern "C" int cwdm_gn_silu_bwd(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode,
+                                const float* ss, const float* mr, const float* gamma, int groups, int64_t B,
+                                int64_t d, int64_t h, int64_t w, int dtype, void* dx0, int acc0, void* dx1, int acc1,
+                                float* dgamma, float* dbeta, void* ws, int64_t ws_bytes, cwdm_stream_t stream) {
+  CWDM_REQUIRE(x0 && du && ss && mr && gamma && dx0 && dgamma && dbeta && ws, CWDM_E_INVALID,
+               "cwdm_gn_silu_bwd: null pointer");
+  CWDM_REQUIRE(c1 == 0 || (x1 && dx1), CWDM_E_INVALID, "cwdm_gn_silu_bwd: second source missing");
+  const int C = c0 + c1;
+  CWDM_REQUIRE(c0 % 8 == 0 && c1 % 8 == 0 && C <= 1024 && C / 8 <= 256, CWDM_E_UNSUPPORTED,
+               "cwdm_gn_silu_bwd: channels must be multiples of 8, at most 1024");
+  CWDM_REQUIRE(groups > 0 && groups <= 256 && C % groups == 0, CWDM_E_SHAPE, "cwdm_gn_silu_bwd: bad groups");
+  CWDM_REQUIRE(du_mode >= 0 && du_mode <= 2, CWDM_E_INVALID, "cwdm_gn_silu_bwd: bad du_mode");
+  CWDM_REQUIRE(du_mode != 2 || (d % 2 == 0 && h % 2 == 0 && w % 2 == 0), CWDM_E_SHAPE,
+               "cwdm_gn_silu_bwd: pooled grid must be even");
+  CWDM_REQUIRE(dtype == CWDM_F32 || dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_gn_silu_bwd: bad dtype");
+  CWDM_REQUIRE(B > 0 && B < 65536 && d > 0 && h > 0 && w > 0, CWDM_E_SHAPE, "cwdm_gn_silu_bwd: empty grid");
+  CWDM_REQUIRE(ws_bytes >= cwdm_gn_silu_bwd_workspace_bytes(C, B, d, h, w), CWDM_E_WORKSPACE,
+               "cwdm_gn_silu_bwd: workspace too small");
+  const long long V = d * h * w;
+  const long long nb = gn_bwd_blocks(C, V);
+  const long long vpb = ceil_div(V, nb);
+  float* part = reinterpret_cast<float*>(ws);
+  float* coef = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(ws) + (B * nb * C * 2 * 4 + 255) / 256 * 256);
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if ((rc = dispatch_mode(du_mode, [&](auto M) -> int {
+         constexpr int MD = decltype(M)::value;
+         if (dtype == CWDM_BF16)
+           hipLaunchKernelGGL((gn_bwd_reduce_kernel<bf16_t, MD>), dim3((unsigned)nb, (unsigned)B), dim3(256), 0, s,
+                              (const bf16_t*)x0, c0, (const bf16_t*)x1, c1, (const bf16_t*)du, ss, mr, groups, (int)d,
+                              (int)h, (int)w, vpb, part);
+         else
+           hipLaunchKernelGGL((gn_bwd_reduce_kernel<float, MD>), dim3((unsigned)nb, (unsigned)B), dim3(256), 0, s,
+                              (const float*)x0, c0, (const float*)x1, c1, (const float*)du, ss, mr, groups, (int)d,
+                              (int)h, (int)w, vpb, part);
+         CWDM_LAUNCHED();
+         return CWDM_OK;
+       })))
+    return rc;
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(512), 0, s, part, (int)nb, C, (int)B, gamma, mr, groups, V,
+                     coef, dgamma, dbeta);
+  CWDM_LAUNCHED();
+  dim3 grid((unsigned)ceil_div(V * (C / 8), 256), (unsigned)B);
+  return dispatch_mode(du_mode, [&](auto M) -> int {
+    constexpr int MD = decltype(M)::value;
+    if (dtype == CWDM_BF16)
+      hipLaunchKernelGGL((gn_bwd_apply_kernel<bf16_t, MD>), grid, dim3(256), 0, s, (const bf16_t*)x0, c0,
+                         (const bf16_t*)x1, c1, (const bf16_t*)du, ss, coef, (int)d, (int)h, (int)w, (bf16_t*)dx0, acc0,
+                         (bf16_t*)dx1, acc1);
+    else
+      hipLaunchKernelGGL((gn_bwd_apply_kernel<float, MD>), grid, dim3(256), 0, s, (const float*)x0, c0,
+                         (const float*)x1, c1, (const float*)du, ss, coef, (int)d, (int)h, (int)w, (float*)dx0, acc0,
+                         (float*)dx1, acc1);
+    CWDM_LAUNCHED();
+    return CWDM_OK;
+  });
+}
+
+extern "C" int cwdm_resample_add(void* dst, const void* src, int C, int64_t B, int64_t d, int64_t h, int64_t w,
+                                 int mode, int accumulate, int dtype, cwdm_stream_t stream) {
+  CWDM_REQUIRE(dst && src, CWDM_E_INVALID, "cwdm_resample_add: null pointer");
+  CWDM_REQUIRE(C > 0 && C % 8 == 0, CWDM_E_UNSUPPORTED, "cwdm_resample_add: channels must be a multiple of 8");
+  CWDM_REQUIRE(mode >= 0 && mode <= 2, CWDM_E_INVALID, "cwdm_resample_add: bad mode");
+  CWDM_REQUIRE(mode != 2 || (d % 2 == 0 && h % 2 == 0 && w % 2 == 0), CWDM_E_SHAPE, "cwdm_resample_add: odd grid");
+  CWDM_REQUIRE(B > 0 && B < 65536 && d > 0 && h > 0 && w > 0, CWDM_E_SHAPE, "cwdm_resample_add: empty grid");
+  const long long V = d * h * w;
+  dim3 grid((unsigned)ceil_div(V * (C / 8), 256), (unsigned)B);
+  hipStream_t s = (hipStream_t)stream;
+  return dispatch_mode(mode, [&](auto M) -> int {
+    constexpr int MD = decltype(M)::value;
+    if (dtype == CWDM_BF16)
+      hipLaunchKernelGGL((resample_add_kernel<bf16_t, MD>), grid, dim3(256), 0, s, (bf16_t*)dst, (const bf16_t*)src, C,
+                         (int)d, (int)h, (int)w, accumulate);
+    else
+      hipLaunchKernelGGL((resample_add_kernel<float, MD>), grid, dim3(256), 0, s, (float*)dst, (const float*)src, C,
+                         (int)d, (int)h, (int)w, accumulate);
+    CWDM_LAUNCHED();
+    return CWDM_OK;
+  });
+}
+
+extern "C" int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V, int C, int cs, float* out_bc,
+                                int64_t bc_stride, float* out_c, float* out_c2, cwdm_stream_t stream) {
+  CWDM_REQUIRE(src, CWDM_E_INVALID, "cwdm_channel_sum: null pointer");
+  CWDM_REQUIRE(C > 0 && cs >= ((C + 7) / 8) * 8 && cs % 8 == 0 && cs <= 2048, CWDM_E_UNSUPPORTED,
+               "cwdm_channel_sum: stride must be a multiple of 8 covering C (<= 2048)");
+  CWDM_REQUIRE(B > 0 && B < 65536 && V > 0, CWDM_E_SHAPE, "cwdm_channel_sum: empty input");
+  long long nb = ceil_div(V, 2048);
+  if (nb > 512) nb = 512;
+  const long long vpb = ceil_div(V, nb);
+  dim3 grid((unsigned)nb, (unsigned)B);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == CWDM_BF16)
+    hipLaunchKernelGGL(channel_sum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)src, (long long)V, C, cs, vpb,
+                       out_bc, (long long)bc_stride, out_c, out_c2);
+  else
+    hipLaunchKernelGGL(channel_sum_kernel<float>, grid, dim3(256), 0, s, (const float*)src, (long long)V, C, cs, vpb,
+                       out_bc, (long long)bc_stride, out_c, out_c2);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+extern "C" int cwdm_adamw(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
+                          double beta2, double eps, double weight_decay, int64_t step, cwdm_stream_t stream) {
+  CWDM_REQUIRE(p && g && m && v, CWDM_E_INVALID, "cwdm_adamw: null pointer");
+  CWDM_REQUIRE(n >= 0 && step >= 1, CWDM_E_INVALID, "cwdm_adamw: bad size/step");
+  if (n == 0) return CWDM_OK;
+  // scalars as torch computes them (Python doubles, cast to float at the kernel)
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  const float decay = (float)(1.0 - lr * weight_decay);
+  const float neg_step = (float)(-(lr / bc1));
+  const float bc2s = (float)std::sqrt(bc2);
+  long long blocks = ceil_div(n, 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long long)n,
+                     decay, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), neg_step, bc2s, (float)eps);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}

@@ -5,6 +5,7 @@
 // GroupNorm-finalize and fused conv launches on one stream.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -18,6 +19,11 @@ int launch_time_embed(const float* t, int B, int mc, const float* w1, const floa
 int launch_emb_proj(const float* temb, int B, int E, const float* W, const float* bias, int R, float* out,
                     hipStream_t s);
 int launch_vec_add(const float* a, const float* b, float* out, int64_t n, hipStream_t s);
+int launch_emb_bwd(const float* dEb, int R, int n, int B, const float* temb, int E, const float* W, float* dw,
+                   float* db, float* dcb, float* dsil, hipStream_t s);
+int launch_temb_bwd(const float* t, int B, int mc, const float* w1, const float* b1, const float* w2,
+                    const float* temb, const float* dsil, float* dw1, float* db1, float* dw2, float* db2,
+                    hipStream_t s);
 }  // namespace cwdm
 
 using namespace cwdm;
@@ -65,6 +71,15 @@ struct PoolStep {  // down-ResBlock pre-pass (cwdm_gn_silu_pool)
 
 struct Step { int kind; int idx; };  // kind 0 = gn, 1 = conv, 2 = pool pre-pass
 
+// one ResBlock, for the backward (reverse order) and the gradient segments
+struct Block {
+  int g1, pool, c1, g2, c2;   // step indices (pool = -1 unless down)
+  int x0, x1;                 // input tensors (x1 = -1 unless decoder concat)
+  int updown;                 // 0 none, 1 up, 2 down
+  int p_begin, p_end;         // parameter index range
+  int emb_k;                  // index into emb_rows_*
+};
+
 }  // namespace
 
 struct cwdm_unet {
@@ -83,6 +98,13 @@ struct cwdm_unet {
   std::vector<int> emb_rows_w, emb_rows_b, emb_rows_cb;  // per res block: emb weight/bias param, conv1 bias param
   std::vector<int> emb_rows_off, emb_rows_n;
   int te_w1, te_b1, te_w2, te_b2;
+  std::vector<Block> blocks;
+  int head_g = -1, head_c = -1, head_p_begin = 0;
+  std::vector<int64_t> goff;      // flat gradient offset (elements) per parameter
+  int64_t grad_numel = 0;
+  std::vector<int64_t> dg_off, dgs_off;  // packed dgrad weights per conv (-1 none)
+  int64_t packed_bwd_bytes = 0;
+  std::vector<char> ginit;        // backward: gradient buffer of tensor written yet
   int64_t off_te_w1, off_te_b1, off_te_w2, off_te_b2, off_emb_w, off_emb_b;
   int64_t packed_bytes = 0;
   // profiling
@@ -154,10 +176,14 @@ void build(cwdm_unet* u) {
 
   // ResBlock (unet.py:185-311): returns output tensor
   auto resblock = [&](const std::string& p, int x0, int x1, int cout, int updown /*0 none 1 up 2 down*/) {
+    Block blk{};
+    blk.p_begin = (int)u->params.size();
+    blk.x0 = x0; blk.x1 = x1; blk.updown = updown; blk.pool = -1;
     const int lin = u->tensors[x0].level;
     const int cin = u->tensors[x0].channels + (x1 >= 0 ? u->tensors[x1].channels : 0);
     const int lout = updown == 2 ? lin + 1 : (updown == 1 ? lin - 1 : lin);
     int g1 = gn_step(p + ".in_layers.0", x0, x1, lin);
+    blk.g1 = g1;
     int xres = x0, xrmode = updown == 2 ? 2 : (updown == 1 ? 1 : 0);
     int a_src = x0, a_mode = updown, a_gn = g1;
     if (updown == 2) {
@@ -168,6 +194,7 @@ void build(cwdm_unet* u) {
       ps.out_x = new_tensor(lout, cin);
       u->pools.push_back(ps);
       u->steps.push_back({2, (int)u->pools.size() - 1});
+      blk.pool = (int)u->pools.size() - 1;
       a_src = ps.out_h; a_mode = 0; a_gn = -1;
       xres = ps.out_x; xrmode = 0;
     }
@@ -179,14 +206,17 @@ void build(cwdm_unet* u) {
     c1.sb0 = c1.sb1 = -1; c1.ws_p = c1.wsb_p = -1; c1.cin_b = 0;
     c1.bias_kind = 1; c1.bias_off = u->R;
     u->emb_rows_w.push_back(c1.emb_w_p); u->emb_rows_b.push_back(c1.emb_b_p); u->emb_rows_cb.push_back(c1.b_p);
+    blk.emb_k = (int)u->emb_rows_off.size();
     u->emb_rows_off.push_back(u->R); u->emb_rows_n.push_back(cout);
     u->R += cout;
     c1.res = -1; c1.rmode = -1; c1.cout = cout; c1.level = lout; c1.stats = true;
     int h1 = c1.out = new_tensor(lout, cout);
     u->convs.push_back(c1);
+    blk.c1 = (int)u->convs.size() - 1;
     u->steps.push_back({1, (int)u->convs.size() - 1});
 
     int g2 = gn_step(p + ".out_layers.0", h1, -1, lout);
+    blk.g2 = g2;
     ConvStep c2{};
     conv_params(p + ".out_layers.3", cout, cout, 3, &c2.w_p, &c2.b_p);
     c2.a0 = h1; c2.a1 = -1; c2.amode = 0; c2.gn = g2; c2.cin_a = cout;
@@ -203,6 +233,9 @@ void build(cwdm_unet* u) {
     int o = c2.out = new_tensor(lout, cout);
     u->convs.push_back(c2);
     u->steps.push_back({1, (int)u->convs.size() - 1});
+    blk.c2 = (int)u->convs.size() - 1;
+    blk.p_end = (int)u->params.size();
+    u->blocks.push_back(blk);
     return o;
   };
 
@@ -247,7 +280,9 @@ void build(cwdm_unet* u) {
     }
   }
   // out head
+  u->head_p_begin = (int)u->params.size();
   int g = gn_step("out.0", h, -1, 0);
+  u->head_g = g;
   ConvStep co{};
   conv_params("out.2", c.out_channels, ch, 3, &co.w_p, &co.b_p);
   co.a0 = h; co.a1 = -1; co.amode = 0; co.gn = g; co.cin_a = ch;
@@ -255,6 +290,7 @@ void build(cwdm_unet* u) {
   co.bias_kind = 0; co.res = -1; co.rmode = -1; co.cout = c.out_channels; co.level = 0; co.stats = false;
   co.out = -1;
   u->convs.push_back(co);
+  u->head_c = (int)u->convs.size() - 1;
   u->steps.push_back({1, (int)u->convs.size() - 1});
   u->trace.push_back(-1); u->trace_level.push_back(0);
 
@@ -277,6 +313,22 @@ void build(cwdm_unet* u) {
     gs.beta_off = take((int64_t)gs.channels * 4);
   }
   u->packed_bytes = off;
+
+  // flat gradient layout (state_dict order, contiguous)
+  int64_t go = 0;
+  for (const auto& pr : u->params) { u->goff.push_back(go); go += pr.numel(); }
+  u->grad_numel = go;
+  // packed dgrad weights (every conv but conv_in, whose input needs no gradient)
+  const int ck = c.dtype == CWDM_BF16 ? 16 : 8;
+  int64_t bo = 0;
+  auto takeb = [&](int64_t bytes) { int64_t o = bo; bo = align_up(bo + bytes); return o; };
+  for (size_t i = 0; i < u->convs.size(); ++i) {
+    const auto& cs = u->convs[i];
+    const int cpad = (int)((cs.cout + ck - 1) / ck * ck);
+    u->dg_off.push_back(i == 0 ? -1 : takeb(cwdm_conv3d_packed_bytes(cs.cin_a, cpad, 3, c.dtype)));
+    u->dgs_off.push_back(cs.ws_p >= 0 ? takeb(cwdm_conv3d_packed_bytes(cs.cin_b, cpad, 1, c.dtype)) : -1);
+  }
+  u->packed_bwd_bytes = bo;
 }
 
 struct Layout {
@@ -581,5 +633,319 @@ extern "C" int cwdm_unet_profile_read(cwdm_unet* u, double* ms, double* flops, i
   if (ms) *ms = tot;
   if (flops) *flops = fl;
   if (n) *n = u->ev_used;
+  return CWDM_OK;
+}
+
+// ============================================================================
+// Backward (training): the reverse of the launch list above, as torch autograd
+// differentiates UNetModel.forward inside TrainLoop.forward_backward
+// (guided_diffusion/train_util.py:396-462).  Per ResBlock, in reverse:
+//   conv2: bias grad (channel sums), wgrad (input = SiLU(GN2(h1)) recomputed
+//          in the staging), skip 1x1 wgrad + dgrad or residual adjoint,
+//          dgrad (flipped/transposed weights, same implicit-GEMM kernel)
+//   GN2:   SiLU/GroupNorm backward -> dh1
+//   conv1: emb-projection grads (per-batch channel sums), wgrad, dgrad
+//   GN1:   SiLU/GroupNorm backward with the up/down resample adjoint -> dx
+// Gradient buffers live in grad_ws (one per forward tensor, compute dtype);
+// the first writer of a buffer stores, later writers accumulate.
+// ============================================================================
+namespace {
+
+struct GLayout {
+  std::vector<int64_t> g_off;
+  int64_t tmp, dout, deb, dsil, gnws, gnws_bytes, split, split_bytes, total;
+};
+
+int ckpad(const cwdm_unet* u, int c) {
+  const int ck = u->cfg.dtype == CWDM_BF16 ? 16 : 8;
+  return (c + ck - 1) / ck * ck;
+}
+
+// dgrad conv of conv step i as a forward conv descriptor (shape only)
+cwdm_conv3d_desc dgrad_shape(const cwdm_unet* u, int i, int64_t B, int64_t D, int64_t H, int64_t W) {
+  const auto& cs = u->convs[i];
+  cwdm_conv3d_desc d{};
+  d.dtype = u->cfg.dtype;
+  d.B = B; d.D = D >> cs.level; d.H = H >> cs.level; d.W = W >> cs.level;
+  d.cout = cs.cin_a;
+  d.a_c0 = ckpad(u, cs.cout);
+  d.a_mode = 0;
+  d.a_w = reinterpret_cast<const void*>(1);
+  d.res_mode = -1;
+  d.out_dtype = u->cfg.dtype;
+  return d;
+}
+
+GLayout glayout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
+  GLayout G;
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) { int64_t o = off; off = align_up(off + bytes); return o; };
+  const int es = esize(u->cfg.dtype);
+  for (size_t i = 0; i < u->tensors.size(); ++i) {
+    const auto& t = u->tensors[i];
+    if ((int)i == u->input_tensor) { G.g_off.push_back(-1); continue; }
+    G.g_off.push_back(take(B * (D >> t.level) * (H >> t.level) * (W >> t.level) * t.channels * es));
+  }
+  int64_t tmp = 0, split = 0, gnws = 0;
+  for (size_t i = 1; i < u->convs.size(); ++i) {
+    const auto& cs = u->convs[i];
+    const int64_t v = B * (D >> cs.level) * (H >> cs.level) * (W >> cs.level);
+    tmp = std::max(tmp, v * cs.cin_a * es);
+    cwdm_conv3d_desc d = dgrad_shape(u, (int)i, B, D, H, W);
+    split = std::max(split, (int64_t)cwdm_conv3d_workspace_bytes(&d));
+  }
+  for (const auto& g : u->gns) {
+    const int lv = g.level;
+    gnws = std::max(gnws, cwdm_gn_silu_bwd_workspace_bytes(g.channels, B, D >> lv, H >> lv, W >> lv));
+  }
+  G.tmp = take(tmp);
+  G.dout = take(B * D * H * W * ckpad(u, u->cfg.out_channels) * es);
+  G.deb = take(B * (int64_t)u->R * 4);
+  G.dsil = take(B * (int64_t)u->E * 4);
+  G.gnws_bytes = gnws;
+  G.gnws = take(gnws);
+  G.split_bytes = split;
+  G.split = take(split);
+  G.total = off;
+  return G;
+}
+
+}  // namespace
+
+extern "C" int64_t cwdm_unet_packed_bwd_bytes(const cwdm_unet* u) { return u ? u->packed_bwd_bytes : -1; }
+
+extern "C" int cwdm_unet_pack_bwd(const cwdm_unet* u, const float* const* P, void* packed_bwd, cwdm_stream_t stream) {
+  CWDM_REQUIRE(u && P && packed_bwd, CWDM_E_INVALID, "cwdm_unet_pack_bwd: null pointer");
+  auto* base = reinterpret_cast<unsigned char*>(packed_bwd);
+  int rc;
+  for (size_t i = 0; i < u->convs.size(); ++i) {
+    const auto& cs = u->convs[i];
+    if (u->dg_off[i] >= 0 &&
+        (rc = cwdm_conv3d_pack_dgrad(P[cs.w_p], cs.cout, cs.cin_a, 3, u->cfg.dtype, base + u->dg_off[i], stream)))
+      return rc;
+    if (u->dgs_off[i] >= 0 &&
+        (rc = cwdm_conv3d_pack_dgrad(P[cs.ws_p], cs.cout, cs.cin_b, 1, u->cfg.dtype, base + u->dgs_off[i], stream)))
+      return rc;
+  }
+  return CWDM_OK;
+}
+
+extern "C" int64_t cwdm_unet_grad_workspace_bytes(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
+  if (!u || B <= 0 || D <= 0 || H <= 0 || W <= 0) return -1;
+  return glayout(u, B, D, H, W).total;
+}
+
+extern "C" int cwdm_unet_backward_segments(const cwdm_unet* u) { return u ? (int)u->blocks.size() + 2 : -1; }
+
+extern "C" int cwdm_unet_segment_range(const cwdm_unet* u, int seg, int64_t* off, int64_t* n) {
+  CWDM_REQUIRE(u && seg >= 0 && seg < (int)u->blocks.size() + 2, CWDM_E_INVALID, "cwdm_unet_segment_range: bad seg");
+  const int nb = (int)u->blocks.size();
+  int pb, pe;
+  if (seg == 0) { pb = u->head_p_begin; pe = (int)u->params.size(); }
+  else if (seg <= nb) { const auto& b = u->blocks[nb - seg]; pb = b.p_begin; pe = b.p_end; }
+  else { pb = 0; pe = u->blocks[0].p_begin; }
+  const int64_t o = u->goff[pb];
+  const int64_t e = pe < (int)u->params.size() ? u->goff[pe] : u->grad_numel;
+  if (off) *off = o;
+  if (n) *n = e - o;
+  return CWDM_OK;
+}
+
+extern "C" double cwdm_unet_backward_flops(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
+  if (!u) return -1;
+  double f = 0;
+  for (size_t i = 0; i < u->convs.size(); ++i) {
+    const auto& cs = u->convs[i];
+    const double v = (double)B * (D >> cs.level) * (H >> cs.level) * (W >> cs.level);
+    const double fwd = 2.0 * v * cs.cout * (27.0 * cs.cin_a + cs.cin_b);
+    f += i == 0 ? fwd : 2 * fwd;  // wgrad (+ dgrad)
+  }
+  return f;
+}
+
+extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* packed_bwd, const void* x,
+                                  const float* t, const float* dout, float* grads, int64_t B, int64_t D, int64_t H,
+                                  int64_t W, const void* ws, int64_t ws_bytes, void* gws, int64_t gws_bytes,
+                                  int seg_begin, int seg_end, cwdm_stream_t stream) {
+  CWDM_REQUIRE(u && packed && packed_bwd && x && t && dout && grads && ws && gws, CWDM_E_INVALID,
+               "cwdm_unet_backward: null pointer");
+  const int nseg = (int)u->blocks.size() + 2;
+  CWDM_REQUIRE(0 <= seg_begin && seg_begin <= seg_end && seg_end <= nseg, CWDM_E_INVALID,
+               "cwdm_unet_backward: bad segment range");
+  CWDM_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0, CWDM_E_SHAPE, "cwdm_unet_backward: empty grid");
+  const int64_t div = int64_t(1) << (u->cfg.num_levels - 1);
+  CWDM_REQUIRE(D % div == 0 && H % div == 0 && W % div == 0, CWDM_E_SHAPE,
+               "cwdm_unet_backward: every subband edge must be divisible by " + std::to_string(div));
+  Layout L = layout(u, B, D, H, W);
+  GLayout G = glayout(u, B, D, H, W);
+  CWDM_REQUIRE(ws_bytes >= L.total, CWDM_E_WORKSPACE, "cwdm_unet_backward: forward workspace too small");
+  CWDM_REQUIRE(gws_bytes >= G.total, CWDM_E_WORKSPACE,
+               "cwdm_unet_backward: grad workspace too small (need " + std::to_string(G.total) + " bytes)");
+  CWDM_REQUIRE(seg_begin == 0 || (int)u->ginit.size() == (int)u->tensors.size(), CWDM_E_INVALID,
+               "cwdm_unet_backward: segment 0 must run first");
+  hipStream_t s = (hipStream_t)stream;
+  const int dt = u->cfg.dtype;
+  const int es = esize(dt);
+  auto* pk = reinterpret_cast<const unsigned char*>(packed);
+  auto* pb = reinterpret_cast<const unsigned char*>(packed_bwd);
+  auto* wb = reinterpret_cast<const unsigned char*>(ws);
+  auto* gb = reinterpret_cast<unsigned char*>(gws);
+  auto P = [&](int64_t off) { return reinterpret_cast<const float*>(pk + off); };
+  auto GR = [&](int pi) { return grads + u->goff[pi]; };
+  auto act = [&](int id) -> const void* {
+    if (id < 0) return nullptr;
+    if (id == u->input_tensor) return x;
+    return wb + L.t_off[id];
+  };
+  auto grd = [&](int id) -> void* { return id < 0 ? nullptr : gb + G.g_off[id]; };
+  auto vox = [&](int lv) { return (D >> lv) * (H >> lv) * (W >> lv); };
+  const float* temb = reinterpret_cast<const float*>(wb + L.temb);
+  float* deb = reinterpret_cast<float*>(gb + G.deb);
+  float* dsil = reinterpret_cast<float*>(gb + G.dsil);
+  void* tmp = gb + G.tmp;
+  int rc;
+
+  // first writer stores, later writers accumulate
+  auto take_acc = [&](int id) -> int {
+    if (id < 0) return 0;
+    const int a = u->ginit[id] ? 1 : 0;
+    u->ginit[id] = 1;
+    return a;
+  };
+  auto ss_of = [&](int g) { return reinterpret_cast<const float*>(wb + L.ss_off[g]); };
+  auto mr_of = [&](int g) { return reinterpret_cast<const float*>(wb + L.mr_off[g]); };
+
+  auto wgrad = [&](int level, int ksize, const void* u0, int uc0, const void* u1, int uc1, int umode,
+                   const float* ugn, const void* dy, int dy_cs, int cout, float* dw) -> int {
+    cwdm_wgrad_desc d{};
+    d.dtype = dt; d.B = B; d.D = D >> level; d.H = H >> level; d.W = W >> level; d.ksize = ksize;
+    d.u0 = u0; d.u_c0 = uc0; d.u1 = u1; d.u_c1 = uc1; d.u_mode = umode; d.u_gn = ugn;
+    d.dy = dy; d.dy_cs = dy_cs; d.cout = cout; d.dw = dw;
+    return cwdm_conv3d_wgrad(&d, stream);
+  };
+  auto dgrad = [&](int ci, const void* dy) -> int {
+    cwdm_conv3d_desc d = dgrad_shape(u, ci, B, D, H, W);
+    d.a0 = dy;
+    d.a_w = pb + u->dg_off[ci];
+    d.out = tmp;
+    d.workspace = gb + G.split;
+    d.ws_bytes = G.split_bytes;
+    return cwdm_conv3d_forward(&d, stream);
+  };
+  auto gn_bwd = [&](int gi, int x0, int x1, int du_mode) -> int {
+    const auto& g = u->gns[gi];
+    const int lv = g.level;
+    const int c0 = u->tensors[x0].channels, c1 = x1 >= 0 ? u->tensors[x1].channels : 0;
+    const int a0 = take_acc(x0), a1 = take_acc(x1);
+    return cwdm_gn_silu_bwd(act(x0), c0, act(x1), c1, tmp, du_mode, ss_of(gi), mr_of(gi), P(g.gamma_off),
+                            u->cfg.num_groups, B, D >> lv, H >> lv, W >> lv, dt, grd(x0), a0, grd(x1), a1,
+                            GR(g.gamma_p), GR(g.beta_p), gb + G.gnws, G.gnws_bytes, stream);
+  };
+
+  for (int seg = seg_begin; seg < seg_end; ++seg) {
+    const int nb = (int)u->blocks.size();
+    if (seg == 0) {
+      u->ginit.assign(u->tensors.size(), 0);
+      CWDM_HIP(hipMemsetAsync(grads, 0, u->grad_numel * 4, s));
+      CWDM_HIP(hipMemsetAsync(deb, 0, B * (int64_t)u->R * 4, s));
+      CWDM_HIP(hipMemsetAsync(dsil, 0, B * (int64_t)u->E * 4, s));
+      // output head: dout -> padded compute-dtype buffer
+      const int oc = u->cfg.out_channels, ocp = ckpad(u, oc);
+      const int64_t V0 = D * H * W;
+      void* d16 = gb + G.dout;
+      CWDM_HIP(hipMemsetAsync(d16, 0, B * V0 * ocp * es, s));
+      const int64_t ss_[3] = {V0 * oc, 1, oc}, ds_[3] = {V0 * ocp, 1, ocp};
+      if ((rc = cwdm_copy3(dout, CWDM_F32, ss_, d16, dt, ds_, B, oc, V0, stream))) return rc;
+      const auto& co = u->convs[u->head_c];
+      const auto& hg = u->gns[u->head_g];
+      if ((rc = cwdm_channel_sum(d16, dt, B, V0, oc, ocp, nullptr, 0, GR(co.b_p), nullptr, stream))) return rc;
+      if ((rc = wgrad(0, 3, act(co.a0), co.cin_a, nullptr, 0, 0, ss_of(u->head_g), d16, ocp, oc, GR(co.w_p))))
+        return rc;
+      if ((rc = dgrad(u->head_c, d16))) return rc;
+      if ((rc = gn_bwd(u->head_g, hg.src0, -1, 0))) return rc;
+      continue;
+    }
+    if (seg <= nb) {
+      const Block& bk = u->blocks[nb - seg];
+      const auto& c1 = u->convs[bk.c1];
+      const auto& c2 = u->convs[bk.c2];
+      const int lout = c2.level;
+      const int64_t Vo = vox(lout);
+      const int o = c2.out, h1 = c1.out;
+      const int cout = c2.cout;
+      // ---- conv2 (+ skip / residual)
+      if ((rc = cwdm_channel_sum(grd(o), dt, B, Vo, cout, cout, nullptr, 0, GR(c2.b_p),
+                                 c2.wsb_p >= 0 ? GR(c2.wsb_p) : nullptr, stream)))
+        return rc;
+      if ((rc = wgrad(lout, 3, act(h1), cout, nullptr, 0, 0, ss_of(bk.g2), grd(o), cout, cout, GR(c2.w_p))))
+        return rc;
+      if (c2.ws_p >= 0) {
+        const int c0 = u->tensors[c2.sb0].channels, cc1 = c2.sb1 >= 0 ? u->tensors[c2.sb1].channels : 0;
+        if ((rc = wgrad(lout, 1, act(c2.sb0), c0, act(c2.sb1), cc1, 0, nullptr, grd(o), cout, cout, GR(c2.ws_p))))
+          return rc;
+        // 1x1 dgrad into dx0 / dx1 (dual output); equalise the store/accumulate state
+        int a0 = take_acc(c2.sb0), a1 = c2.sb1 >= 0 ? take_acc(c2.sb1) : a0;
+        if (a0 != a1) {
+          const int zid = a0 ? c2.sb1 : c2.sb0;
+          const auto& zt = u->tensors[zid];
+          CWDM_HIP(hipMemsetAsync(grd(zid), 0, B * vox(zt.level) * zt.channels * es, s));
+          a0 = a1 = 1;
+        }
+        cwdm_conv3d_desc d{};
+        d.dtype = dt; d.B = B; d.D = D >> lout; d.H = H >> lout; d.W = W >> lout;
+        d.cout = c0 + cc1;
+        d.b0 = grd(o); d.b_c0 = cout; d.b_w = pb + u->dgs_off[bk.c2];
+        d.res_mode = -1;
+        d.out = grd(c2.sb0); d.out_dtype = dt;
+        if (c2.sb1 >= 0) { d.out1 = grd(c2.sb1); d.out_c0 = c0; }
+        d.accumulate = a0;
+        d.workspace = gb + G.split; d.ws_bytes = G.split_bytes;
+        if ((rc = cwdm_conv3d_forward(&d, stream))) return rc;
+      } else {
+        // identity residual (possibly through the block's resampling)
+        const int xt = bk.x0;
+        const int lx = u->tensors[xt].level;
+        const int mode = bk.updown == 2 ? 2 : (bk.updown == 1 ? 1 : 0);
+        if ((rc = cwdm_resample_add(grd(xt), grd(o), cout, B, D >> lx, H >> lx, W >> lx, mode, take_acc(xt), dt,
+                                    stream)))
+          return rc;
+      }
+      if ((rc = dgrad(bk.c2, grd(o)))) return rc;
+      // ---- GN2 -> dh1
+      if ((rc = gn_bwd(bk.g2, h1, -1, 0))) return rc;
+      // ---- conv1: emb projection, wgrad, dgrad
+      const int k = bk.emb_k;
+      const int roff = u->emb_rows_off[k], rn = u->emb_rows_n[k];
+      if ((rc = cwdm_channel_sum(grd(h1), dt, B, Vo, cout, cout, deb + roff, u->R, nullptr, nullptr, stream)))
+        return rc;
+      if ((rc = launch_emb_bwd(deb + roff, u->R, rn, (int)B, temb, u->E, P(u->off_emb_w) + (int64_t)roff * u->E,
+                               GR(u->emb_rows_w[k]), GR(u->emb_rows_b[k]), GR(u->emb_rows_cb[k]), dsil, s)))
+        return rc;
+      if (bk.updown == 2) {
+        const auto& ps = u->pools[bk.pool];
+        if ((rc = wgrad(lout, 3, act(ps.out_h), ps.channels, nullptr, 0, 0, nullptr, grd(h1), cout, cout,
+                        GR(c1.w_p))))
+          return rc;
+      } else {
+        const int c0 = u->tensors[bk.x0].channels, cc1 = bk.x1 >= 0 ? u->tensors[bk.x1].channels : 0;
+        if ((rc = wgrad(lout, 3, act(bk.x0), c0, act(bk.x1), cc1, bk.updown == 1 ? 1 : 0, ss_of(bk.g1), grd(h1),
+                        cout, cout, GR(c1.w_p))))
+          return rc;
+      }
+      if ((rc = dgrad(bk.c1, grd(h1)))) return rc;
+      // ---- GN1 (+ resample adjoint) -> dx0 / dx1
+      if ((rc = gn_bwd(bk.g1, bk.x0, bk.x1, bk.updown == 1 ? 1 : (bk.updown == 2 ? 2 : 0)))) return rc;
+      continue;
+    }
+    // conv_in + time_embed
+    const auto& c0 = u->convs[0];
+    const int64_t V0 = D * H * W;
+    if ((rc = cwdm_channel_sum(grd(c0.out), dt, B, V0, c0.cout, c0.cout, nullptr, 0, GR(c0.b_p), nullptr, stream)))
+      return rc;
+    if ((rc = wgrad(0, 3, x, c0.cin_a, nullptr, 0, 0, nullptr, grd(c0.out), c0.cout, c0.cout, GR(c0.w_p)))) return rc;
+    if ((rc = launch_temb_bwd(t, (int)B, u->cfg.model_channels, P(u->off_te_w1), P(u->off_te_b1), P(u->off_te_w2),
+                              temb, dsil, GR(u->te_w1), GR(u->te_b1), GR(u->te_w2), GR(u->te_b2), s)))
+      return rc;
+  }
   return CWDM_OK;
 }

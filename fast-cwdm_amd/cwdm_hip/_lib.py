@@ -59,6 +59,20 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class WgradDesc(ctypes.Structure):
+    _fields_ = [
+        ("dtype", ctypes.c_int),
+        ("B", i64), ("D", i64), ("H", i64), ("W", i64),
+        ("ksize", ctypes.c_int),
+        ("u0", vp), ("u_c0", ctypes.c_int),
+        ("u1", vp), ("u_c1", ctypes.c_int),
+        ("u_mode", ctypes.c_int),
+        ("u_gn", vp),
+        ("dy", vp), ("dy_cs", ctypes.c_int), ("cout", ctypes.c_int),
+        ("dw", vp),
+    ]
+
+
 class UNetConfig(ctypes.Structure):
     _fields_ = [
         ("in_channels", ctypes.c_int), ("model_channels", ctypes.c_int),
@@ -88,6 +102,17 @@ _PROTOS = {
     "cwdm_gn_finalize": (ctypes.c_int, [vp, i64, ctypes.c_int, vp, i64, ctypes.c_int, vp, vp, ctypes.c_int, i64, i64,
                                         ctypes.c_float, vp, vp, vp]),
     "cwdm_gn_silu_pool": (ctypes.c_int, [vp, ctypes.c_int, vp, i64, i64, i64, i64, ctypes.c_int, vp, vp, vp]),
+    "cwdm_conv3d_wgrad": (ctypes.c_int, [ctypes.POINTER(WgradDesc), vp]),
+    "cwdm_gn_silu_bwd_workspace_bytes": (i64, [ctypes.c_int, i64, i64, i64, i64]),
+    "cwdm_gn_silu_bwd": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp,
+                                        ctypes.c_int, i64, i64, i64, i64, ctypes.c_int, vp, ctypes.c_int, vp,
+                                        ctypes.c_int, vp, vp, vp, i64, vp]),
+    "cwdm_resample_add": (ctypes.c_int, [vp, vp, ctypes.c_int, i64, i64, i64, i64, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, vp]),
+    "cwdm_channel_sum": (ctypes.c_int, [vp, ctypes.c_int, i64, i64, ctypes.c_int, ctypes.c_int, vp, i64, vp, vp,
+                                        vp]),
+    "cwdm_adamw": (ctypes.c_int, [vp, vp, vp, vp, i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                  ctypes.c_double, ctypes.c_double, i64, vp]),
     "cwdm_unet_create": (ctypes.c_int, [ctypes.POINTER(UNetConfig), ctypes.POINTER(vp)]),
     "cwdm_unet_destroy": (None, [vp]),
     "cwdm_unet_num_params": (ctypes.c_int, [vp]),
@@ -101,6 +126,14 @@ _PROTOS = {
     "cwdm_unet_trace_info": (ctypes.c_int, [vp, ctypes.c_int, i64, i64, i64, i64, ctypes.POINTER(i64),
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "cwdm_unet_flops": (ctypes.c_double, [vp, i64, i64, i64, i64]),
+    "cwdm_unet_packed_bwd_bytes": (i64, [vp]),
+    "cwdm_unet_pack_bwd": (ctypes.c_int, [vp, ctypes.POINTER(vp), vp, vp]),
+    "cwdm_unet_grad_workspace_bytes": (i64, [vp, i64, i64, i64, i64]),
+    "cwdm_unet_backward_segments": (ctypes.c_int, [vp]),
+    "cwdm_unet_segment_range": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
+    "cwdm_unet_backward": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, i64, vp, i64,
+                                          ctypes.c_int, ctypes.c_int, vp]),
+    "cwdm_unet_backward_flops": (ctypes.c_double, [vp, i64, i64, i64, i64]),
     "cwdm_unet_set_profiling": (ctypes.c_int, [vp, ctypes.c_int]),
     "cwdm_unet_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_int)]),

@@ -109,6 +109,61 @@ class UNetPlan:
     def flops(self, B, D, H, W):
         return float(lib().cwdm_unet_flops(self._h, B, D, H, W))
 
+    # ---- training -----------------------------------------------------------
+    @property
+    def grad_numel(self):
+        n = 0
+        for _, shape in self.param_specs:
+            k = 1
+            for s in shape:
+                k *= s
+            n += k
+        return n
+
+    def pack_bwd(self, params, packed_bwd=None):
+        """Transposed/flipped (dgrad) weight layouts; re-run after every update."""
+        _need_cuda(*params)
+        if packed_bwd is None:
+            packed_bwd = torch.empty(max(int(lib().cwdm_unet_packed_bwd_bytes(self._h)), 1), dtype=torch.uint8,
+                                     device=params[0].device)
+        arr = (ctypes.c_void_p * len(params))(*[p.data_ptr() for p in params])
+        check(lib().cwdm_unet_pack_bwd(self._h, arr, ctypes.c_void_p(packed_bwd.data_ptr()), _stream()), "pack_bwd")
+        return packed_bwd
+
+    def grad_workspace_bytes(self, B, D, H, W):
+        n = int(lib().cwdm_unet_grad_workspace_bytes(self._h, B, D, H, W))
+        if n < 0:
+            raise AssertionError("bad grid")
+        return n
+
+    @property
+    def num_segments(self):
+        return int(lib().cwdm_unet_backward_segments(self._h))
+
+    def segment_range(self, seg):
+        off, n = ctypes.c_int64(), ctypes.c_int64()
+        check(lib().cwdm_unet_segment_range(self._h, seg, ctypes.byref(off), ctypes.byref(n)))
+        return off.value, n.value
+
+    def backward(self, packed, packed_bwd, x_ndhwc, t_f32, dout_ndhwc, grads, B, D, H, W, ws, gws,
+                 seg_begin=0, seg_end=None):
+        """Gradients of all parameters (flat fp32 ``grads``) for the forward
+        that last ran on ``ws``; ``dout_ndhwc`` fp32 (B, D, H, W, out)."""
+        _need_cuda(packed, packed_bwd, x_ndhwc, t_f32, dout_ndhwc, grads, ws, gws)
+        if seg_end is None:
+            seg_end = self.num_segments
+        assert grads.dtype == torch.float32 and grads.numel() >= self.grad_numel
+        check(lib().cwdm_unet_backward(self._h, ctypes.c_void_p(packed.data_ptr()),
+                                       ctypes.c_void_p(packed_bwd.data_ptr()), ctypes.c_void_p(x_ndhwc.data_ptr()),
+                                       ctypes.c_void_p(t_f32.data_ptr()), ctypes.c_void_p(dout_ndhwc.data_ptr()),
+                                       ctypes.c_void_p(grads.data_ptr()), B, D, H, W,
+                                       ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(gws.data_ptr()),
+                                       gws.numel(), seg_begin, seg_end, _stream()), "UNetModel.backward")
+        return grads
+
+    def backward_flops(self, B, D, H, W):
+        return float(lib().cwdm_unet_backward_flops(self._h, B, D, H, W))
+
     def trace_tensors(self, ws, B, D, H, W):
         """Views of every block output left in the workspace (NDHWC)."""
         out = []

@@ -112,6 +112,50 @@ class UNetModel(nn.Module):
         self._reset_parameters()
         self._packed = None
         self._packed_key = None
+        self._packed_bwd = None
+        self._packed_bwd_key = None
+        self._grad_hook = None       # called per backward segment (DDP bucket all-reduce)
+        self._last_grad_flat = None
+        self._flatten_params()
+
+    # ---- flat parameter storage ---------------------------------------------
+    def _flatten_params(self):
+        """All parameters become views of ONE contiguous fp32 buffer (state_dict
+        order): the optimizer, gradient all-reduce and weight packing run over
+        flat ranges; the views share the buffer's version counter."""
+        params = list(self.parameters())
+        if not params:
+            return
+        dev = params[0].device
+        flat = th.empty(sum(p.numel() for p in params), dtype=th.float32, device=dev)
+        o = 0
+        with th.no_grad():
+            for p in params:
+                n = p.numel()
+                flat[o:o + n].copy_(p.data.reshape(-1))
+                p.data = flat[o:o + n].view(p.shape)
+                o += n
+        self._flat = flat
+
+    def _apply(self, fn, *args, **kwargs):
+        r = super()._apply(fn, *args, **kwargs)
+        self._flatten_params()
+        self._packed = self._packed_bwd = None
+        return r
+
+    @property
+    def flat_params(self):
+        return self._flat
+
+    def flat_grad(self):
+        """Flat fp32 gradient of the last backward (the buffer the native backward
+        wrote when the .grad tensors still alias it, else a concatenation)."""
+        params = list(self.parameters())
+        g = self._last_grad_flat
+        if g is not None and params[0].grad is not None and params[0].grad.data_ptr() == g.data_ptr() and \
+                params[-1].grad.data_ptr() == g[g.numel() - params[-1].numel():].data_ptr():
+            return g
+        return th.cat([(p.grad if p.grad is not None else th.zeros_like(p)).reshape(-1) for p in params])
 
     # ---- parameters -------------------------------------------------------
     def _reset_parameters(self):
@@ -161,6 +205,16 @@ class UNetModel(nn.Module):
             self._packed_key = key
         return self._packed
 
+    def packed_bwd_weights(self):
+        """Transposed/flipped dgrad weight layouts for the native backward."""
+        params = list(self.parameters())
+        key = (self.compute_dtype,) + tuple((p.data_ptr(), p._version) for p in params)
+        if self._packed_bwd is None or self._packed_bwd_key != key:
+            ops._need_cuda(*params)
+            self._packed_bwd = self.plan.pack_bwd([p.detach() for p in params])
+            self._packed_bwd_key = key
+        return self._packed_bwd
+
     def to(self, *args, **kwargs):
         """Reference semantics, except that a device list (the 2-GPU layer split
         of unet.py:727-752) places the whole model on the first device: on
@@ -191,16 +245,83 @@ class UNetModel(nn.Module):
             assert x.device == self.devices[0], f"{x.device=} does not match {self.devices[0]=}"
         B, C, D, H, W = x.shape
         assert C == self.in_channels
+        params = list(self.parameters())
+        if th.is_grad_enabled() and any(p.requires_grad for p in params):
+            return _UNetTrain.apply(self, x, timesteps, *params)
+        xin, t = self._prep_inputs(x, timesteps)
+        out_nd = th.empty((B, D, H, W, self.out_channels), dtype=th.float32, device=x.device)
+        self.forward_ndhwc(xin, t, out_nd)
+        return self._to_ncdhw(out_nd)
+
+    def _prep_inputs(self, x, timesteps):
+        B, C, D, H, W = x.shape
         plan = self.plan
         plan.check_grid(D, H, W)
         V = D * H * W
         xin = th.empty((B, D, H, W, C), dtype=plan.torch_dtype, device=x.device)
-        ops.copy3(x.contiguous().float() if x.dtype not in (th.float32, th.bfloat16) else x.contiguous(),
-                  (C * V, V, 1), xin, (V * C, 1, C), B, C, V)
+        ops.copy3(x.detach().contiguous().float() if x.dtype not in (th.float32, th.bfloat16) else
+                  x.detach().contiguous(), (C * V, V, 1), xin, (V * C, 1, C), B, C, V)
         t = timesteps.to(device=x.device, dtype=th.float32).contiguous()
-        out_nd = th.empty((B, D, H, W, self.out_channels), dtype=th.float32, device=x.device)
-        self.forward_ndhwc(xin, t, out_nd)
-        out = th.empty((B, self.out_channels, D, H, W), dtype=th.float32, device=x.device)
-        oc = self.out_channels
+        return xin, t
+
+    def _to_ncdhw(self, out_nd):
+        B, D, H, W, oc = out_nd.shape
+        V = D * H * W
+        out = th.empty((B, oc, D, H, W), dtype=th.float32, device=out_nd.device)
         ops.copy3(out_nd, (V * oc, 1, oc), out, (oc * V, V, 1), B, oc, V)
         return out
+
+
+class _UNetTrain(th.autograd.Function):
+    """Differentiable UNetModel.forward: the native forward keeps every
+    activation in a private workspace; backward runs the native plan backward
+    (cwdm_unet_backward) segment by segment, calling the model's grad hook
+    after each so a data-parallel reducer can all-reduce finished gradient
+    ranges while later segments compute."""
+
+    @staticmethod
+    def forward(ctx, model, x, timesteps, *params):
+        B, C, D, H, W = x.shape
+        plan = model.plan
+        xin, t = model._prep_inputs(x, timesteps)
+        ws = th.empty(plan.workspace_bytes(B, D, H, W), dtype=th.uint8, device=x.device)
+        out_nd = th.empty((B, D, H, W, model.out_channels), dtype=th.float32, device=x.device)
+        plan.forward(model.packed_weights(), xin, t, out_nd, B, D, H, W, ws=ws)
+        ctx.model = model
+        ctx.state = (xin, t, ws, (B, D, H, W))
+        return model._to_ncdhw(out_nd)
+
+    @staticmethod
+    def backward(ctx, gout):
+        model = ctx.model
+        xin, t, ws, (B, D, H, W) = ctx.state
+        ctx.state = None
+        plan = model.plan
+        oc = model.out_channels
+        V = D * H * W
+        dout = th.empty((B, D, H, W, oc), dtype=th.float32, device=xin.device)
+        ops.copy3(gout.contiguous().float(), (oc * V, V, 1), dout, (V * oc, 1, oc), B, oc, V)
+        grads = th.empty(plan.grad_numel, dtype=th.float32, device=xin.device)
+        gws = th.empty(plan.grad_workspace_bytes(B, D, H, W), dtype=th.uint8, device=xin.device)
+        packed, packed_bwd = model.packed_weights(), model.packed_bwd_weights()
+        hook = model._grad_hook
+        nseg = plan.num_segments
+        if hook is None:
+            plan.backward(packed, packed_bwd, xin, t, dout, grads, B, D, H, W, ws, gws, 0, nseg)
+        else:
+            for seg in range(nseg):
+                plan.backward(packed, packed_bwd, xin, t, dout, grads, B, D, H, W, ws, gws, seg, seg + 1)
+                off, n = plan.segment_range(seg)
+                hook(seg, grads, off, n)
+            hook(None, grads, 0, grads.numel())
+        del ws, gws
+        model._last_grad_flat = grads
+        views = []
+        o = 0
+        for _, shape in plan.param_specs:
+            n = 1
+            for s_ in shape:
+                n *= s_
+            views.append(grads[o:o + n].view(shape))
+            o += n
+        return (None, None, None, *views)

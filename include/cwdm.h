@@ -159,7 +159,8 @@ int cwdm_conv3d_pack(const float* w_oidhw, int cout, int cin, int ksize, int dty
                      void* packed, cwdm_stream_t stream);
 /* Packs the input-gradient (dgrad) conv of a (cin -> cout) conv: a (cout -> cin)
  * conv with spatially flipped, transposed weights (the backward of Conv3d's
- * input, stride 1, pad 1).  Size: cwdm_conv3d_packed_bytes(cin, cout, ksize, dtype). */
+ * input, stride 1, pad 1).  Its input channels (cout) are zero-padded up to the
+ * K chunk (16 bf16 / 8 fp32): size cwdm_conv3d_packed_bytes(cin, pad(cout), ksize, dtype). */
 int cwdm_conv3d_pack_dgrad(const float* w_oidhw, int cout, int cin, int ksize, int dtype,
                            void* packed, cwdm_stream_t stream);
 int64_t cwdm_conv3d_parts(int dtype, int64_t D, int64_t H, int64_t W, int cout);
@@ -185,6 +186,63 @@ int cwdm_gn_finalize(const float* stats0, int64_t parts0, int c0,
  * (B, d, h, w, C) in dtype; gn as for cwdm_conv3d_desc.a_gn. */
 int cwdm_gn_silu_pool(const void* x, int C, const float* gn, int64_t B, int64_t d, int64_t h, int64_t w,
                       int dtype, void* out_h, void* out_x, cwdm_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Training kernels (the backward of the forward above, as torch autograd runs
+ * it inside TrainLoop.forward_backward, guided_diffusion/train_util.py:396-462,
+ * and the AdamW step of train_util.py:111 / :383).
+ * ------------------------------------------------------------------------- */
+/* Conv3d weight gradient: dw[co][ci][tap] += sum_{b,v} dy[b,v,co] * U[b,v+tap-1,ci]
+ * with U = the conv's input recomputed from the saved sources exactly as the
+ * forward staged it (concat of u0/u1, optional GroupNorm scale/shift + SiLU,
+ * optional nearest-x2 upsample of a half-resolution source).  dw is fp32 OIDHW,
+ * accumulated with atomics (zero it first).  ksize 1: the 1x1 skip conv. */
+typedef struct {
+  int dtype;
+  int64_t B, D, H, W;       /* conv (output) grid */
+  int ksize;                /* 3 or 1 */
+  const void* u0; int u_c0;
+  const void* u1; int u_c1;
+  int u_mode;               /* 0 same grid, 1 nearest-x2 upsample (ksize 3) */
+  const float* u_gn;        /* [B][cin][2] scale/shift -> SiLU, or NULL */
+  const void* dy; int dy_cs; int cout;   /* dy [B][V][dy_cs] in dtype, first cout channels */
+  float* dw;                /* fp32 [cout][cin][ksize^3] */
+} cwdm_wgrad_desc;
+int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* desc, cwdm_stream_t stream);
+
+/* Backward of SiLU(GroupNorm(x)) (guided_diffusion/nn.py:17-19, :93-100):
+ * x = concat(x0 (c0 ch), x1 (c1 ch)) NDHWC at grid (d, h, w); du = gradient of
+ * the SiLU output in dtype with C = c0+c1 channels, at the same grid
+ * (du_mode 0), at the 2x grid of a nearest-x2 upsample that followed
+ * (du_mode 1: children summed) or at the half grid of an AvgPool2 that
+ * followed (du_mode 2: parent / 8).  scale_shift / mean_rstd are the forward's
+ * cwdm_gn_finalize outputs.  Writes dx0/dx1 (acc0/acc1: add to the existing
+ * contents) and dgamma/dbeta (fp32 [C], overwritten). */
+int64_t cwdm_gn_silu_bwd_workspace_bytes(int C, int64_t B, int64_t d, int64_t h, int64_t w);
+int cwdm_gn_silu_bwd(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode,
+                     const float* scale_shift, const float* mean_rstd, const float* gamma, int groups,
+                     int64_t B, int64_t d, int64_t h, int64_t w, int dtype,
+                     void* dx0, int acc0, void* dx1, int acc1, float* dgamma, float* dbeta,
+                     void* workspace, int64_t ws_bytes, cwdm_stream_t stream);
+
+/* Adjoint of the resampling of a residual path: dst (grid d,h,w, C channels,
+ * NDHWC, dtype) (+)= R^T src with mode 0 identity, 1 = src at the 2x grid
+ * (adjoint of nearest-x2: sum of the 8 children), 2 = src at the half grid
+ * (adjoint of AvgPool2: parent / 8). */
+int cwdm_resample_add(void* dst, const void* src, int C, int64_t B, int64_t d, int64_t h, int64_t w,
+                      int mode, int accumulate, int dtype, cwdm_stream_t stream);
+
+/* Per-channel sums of src [B][V][cs] (first C channels): out_bc[b*bc_stride+c]
+ * += sum_v, out_c[c] += sum_{b,v}, out_c2 likewise (each may be NULL; fp32
+ * atomics -- zero first).  Bias gradients and the emb-projection gradient. */
+int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V, int C, int cs,
+                     float* out_bc, int64_t bc_stride, float* out_c, float* out_c2, cwdm_stream_t stream);
+
+/* torch.optim.AdamW step (decoupled weight decay) over a flat fp32 buffer:
+ * p *= 1 - lr*wd; m = lerp(m, g, 1-beta1); v = beta2*v + (1-beta2)*g*g;
+ * p -= lr/(1-beta1^step) * m / (sqrt(v)/sqrt(1-beta2^step) + eps). */
+int cwdm_adamw(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
+               double eps, double weight_decay, int64_t step, cwdm_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * U-Net plan: the whole UNetModel.forward (guided_diffusion/unet.py:754-800)
@@ -222,6 +280,27 @@ int cwdm_unet_forward(cwdm_unet* plan, const void* packed, const void* x, const 
 int cwdm_unet_trace_count(const cwdm_unet* plan);
 int cwdm_unet_trace_info(const cwdm_unet* plan, int i, int64_t B, int64_t D, int64_t H, int64_t W,
                          int64_t* ws_offset, int* channels, int* level);
+/* Backward (training).  The forward must have run with the same workspace,
+ * which then holds every saved activation.  packed_bwd holds the
+ * transposed/flipped (dgrad) weights (cwdm_unet_pack_bwd after each update).
+ * dout: NDHWC fp32 (B, D, H, W, out_channels) gradient of the output.
+ * grads: fp32 flat buffer, parameters in state_dict order, each contiguous
+ * (offset = sum of the preceding numels).  The backward runs as segments
+ * (output head, then one per ResBlock in reverse, then conv_in + time_embed);
+ * segment s finalises the grads range cwdm_unet_segment_range(s) -- a
+ * caller can all-reduce that range while later segments run.  Segments must
+ * be issued in order, 0 first (it zeroes grads). */
+int64_t cwdm_unet_packed_bwd_bytes(const cwdm_unet* plan);
+int cwdm_unet_pack_bwd(const cwdm_unet* plan, const float* const* params, void* packed_bwd,
+                       cwdm_stream_t stream);
+int64_t cwdm_unet_grad_workspace_bytes(const cwdm_unet* plan, int64_t B, int64_t D, int64_t H, int64_t W);
+int cwdm_unet_backward_segments(const cwdm_unet* plan);
+int cwdm_unet_segment_range(const cwdm_unet* plan, int seg, int64_t* offset, int64_t* count);
+int cwdm_unet_backward(cwdm_unet* plan, const void* packed, const void* packed_bwd, const void* x,
+                       const float* t, const float* dout, float* grads, int64_t B, int64_t D, int64_t H,
+                       int64_t W, const void* workspace, int64_t ws_bytes, void* grad_ws, int64_t gws_bytes,
+                       int seg_begin, int seg_end, cwdm_stream_t stream);
+double cwdm_unet_backward_flops(const cwdm_unet* plan, int64_t B, int64_t D, int64_t H, int64_t W);
 /* Conv FLOPs (2*MAC) of one forward at this grid. */
 double cwdm_unet_flops(const cwdm_unet* plan, int64_t B, int64_t D, int64_t H, int64_t W);
 /* Optional per-conv hipEvent timing (profiling only; adds events to the stream). */

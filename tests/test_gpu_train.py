@@ -1,0 +1,424 @@
+"""Training path on the GPU: backward kernels against PyTorch-CPU fp32
+autograd of the same op, and the whole native U-Net backward against autograd
+through the oracle (fp32 within 1e-3 rel)."""
+import ctypes
+import math
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import cases, unet as ou
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _nd(x):
+    return x.permute(0, 2, 3, 4, 1).contiguous()
+
+
+def _nc(x):
+    return x.permute(0, 4, 1, 2, 3).contiguous()
+
+
+def _dt(name):
+    from cwdm_hip import _lib
+    return (_lib.CWDM_F32, torch.float32) if name == "fp32" else (_lib.CWDM_BF16, torch.bfloat16)
+
+
+# --------------------------------------------------------------------------- wgrad
+WG_CASES = [
+    # name, B, grid(conv), c0, c1, cout, umode, gn, ksize, dy_cs
+    ("gn_64_64", 1, (8, 8, 16), 64, 0, 64, 0, True, 3, 64),
+    ("concat_odd", 2, (4, 6, 20), 32, 32, 32, 0, True, 3, 32),
+    ("up", 1, (8, 8, 16), 32, 0, 64, 1, True, 3, 64),
+    ("plain_in32", 1, (8, 4, 16), 32, 0, 64, 0, False, 3, 64),
+    ("head_cout8", 1, (8, 8, 8), 64, 0, 8, 0, True, 3, 16),
+    ("skip1x1", 2, (4, 8, 16), 64, 32, 64, 0, False, 1, 64),
+    ("tiny_grid", 1, (2, 2, 2), 64, 64, 128, 0, True, 3, 128),
+]
+
+
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", WG_CASES, ids=[c[0] for c in WG_CASES])
+def test_conv3d_wgrad_vs_torch(case, dtype_name):
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import check, lib
+    name, B, grid, c0, c1, cout, umode, use_gn, k, dy_cs = case
+    dtype, tdt = _dt(dtype_name)
+    if dtype_name == "fp32" and dy_cs == 16:
+        dy_cs = 8
+    g = torch.Generator().manual_seed(3)
+    D, H, W = grid
+    sD, sH, sW = (D // 2, H // 2, W // 2) if umode == 1 else (D, H, W)
+    cin = c0 + c1
+    x = torch.randn(B, cin, sD, sH, sW, generator=g).to(tdt).float()
+    dy = torch.randn(B, cout, D, H, W, generator=g).to(tdt).float()
+    gn = None
+    h = x
+    if use_gn:
+        scale = 1 + 0.2 * torch.randn(B, cin, generator=g)
+        shift = 0.2 * torch.randn(B, cin, generator=g)
+        gn = torch.stack([scale, shift], -1).contiguous()
+        h = F.silu(x * scale[:, :, None, None, None] + shift[:, :, None, None, None])
+    if umode == 1:
+        h = F.interpolate(h, scale_factor=2, mode="nearest")
+    if dtype_name == "bf16":
+        h = h.to(tdt).float()   # staged in bf16 like the forward
+    ref = torch.nn.grad.conv3d_weight(h, (cout, cin, k, k, k), dy, padding=(k // 2))
+    xd = _nd(x).to(DEV, tdt)
+    x0 = xd[..., :c0].contiguous()
+    x1 = xd[..., c0:].contiguous() if c1 else None
+    dyd = torch.zeros(B, D, H, W, dy_cs, device=DEV, dtype=tdt)
+    dyd[..., :cout] = _nd(dy).to(DEV, tdt)
+    dw = torch.zeros(cout, cin, k, k, k, device=DEV)
+    d = _lib.WgradDesc()
+    d.dtype, d.B, d.D, d.H, d.W, d.ksize = dtype, B, D, H, W, k
+    d.u0, d.u_c0 = x0.data_ptr(), c0
+    d.u1, d.u_c1 = (x1.data_ptr(), c1) if c1 else (None, 0)
+    d.u_mode = umode
+    gnd = gn.to(DEV) if gn is not None else None
+    d.u_gn = gnd.data_ptr() if gnd is not None else None
+    d.dy, d.dy_cs, d.cout = dyd.data_ptr(), dy_cs, cout
+    d.dw = dw.data_ptr()
+    check(lib().cwdm_conv3d_wgrad(ctypes.byref(d), None))
+    tol = 1e-4 if dtype_name == "fp32" else 1e-2
+    assert rel_err(dw, ref) < tol, name
+
+
+# --------------------------------------------------------------------------- dgrad
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+@pytest.mark.parametrize("cfg", [(64, 64, (8, 8, 16)), (192, 64, (4, 8, 8)), (64, 8, (8, 8, 8)), (128, 256, (2, 2, 2))])
+def test_conv3d_dgrad_packing_vs_torch(cfg, dtype_name):
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import check, lib
+    cin, cout, grid = cfg
+    dtype, tdt = _dt(dtype_name)
+    ck = 16 if dtype_name == "bf16" else 8
+    cpad = (cout + ck - 1) // ck * ck
+    g = torch.Generator().manual_seed(4)
+    B = 1
+    w = (torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)).to(tdt).float()
+    dy = torch.randn(B, cout, *grid, generator=g).to(tdt).float()
+    ref = torch.nn.grad.conv3d_input((B, cin, *grid), w, dy, padding=1)
+    L = lib()
+    pk = torch.empty(L.cwdm_conv3d_packed_bytes(cin, cpad, 3, dtype), dtype=torch.uint8, device=DEV)
+    wd = w.to(DEV).contiguous()
+    check(L.cwdm_conv3d_pack_dgrad(ctypes.c_void_p(wd.data_ptr()), cout, cin, 3, dtype,
+                                   ctypes.c_void_p(pk.data_ptr()), None))
+    a = torch.zeros(B, *grid, cpad, device=DEV, dtype=tdt)
+    a[..., :cout] = _nd(dy).to(DEV, tdt)
+    out = torch.empty(B, *grid, cin, device=DEV, dtype=tdt)
+    d = _lib.ConvDesc()
+    d.dtype, d.B, (d.D, d.H, d.W), d.cout = dtype, B, grid, cin
+    d.a0, d.a_c0, d.a_w = a.data_ptr(), cpad, pk.data_ptr()
+    d.res_mode = -1
+    d.out, d.out_dtype = out.data_ptr(), dtype
+    nws = L.cwdm_conv3d_workspace_bytes(ctypes.byref(d))
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=DEV)
+    d.workspace, d.ws_bytes = ws.data_ptr(), nws
+    check(L.cwdm_conv3d_forward(ctypes.byref(d), None))
+    tol = 2e-5 if dtype_name == "fp32" else 2e-2
+    assert rel_err(_nc(out.float().cpu()), ref) < tol
+
+
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+def test_conv3d_b_only_dual_output_accumulate(dtype_name):
+    """1x1 skip dgrad: B-only conv writing channel slices to two buffers, accumulating."""
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import check, lib
+    dtype, tdt = _dt(dtype_name)
+    g = torch.Generator().manual_seed(8)
+    B, grid, cout, c0, c1 = 1, (4, 8, 16), 32, 40, 56
+    cin = c0 + c1
+    w = (torch.randn(cout, cin, 1, 1, 1, generator=g) / math.sqrt(cin)).to(tdt).float()
+    dy = torch.randn(B, cout, *grid, generator=g).to(tdt).float()
+    ref = torch.nn.grad.conv3d_input((B, cin, *grid), w, dy)
+    L = lib()
+    pk = torch.empty(L.cwdm_conv3d_packed_bytes(cin, cout, 1, dtype), dtype=torch.uint8, device=DEV)
+    wd = w.to(DEV).contiguous()
+    check(L.cwdm_conv3d_pack_dgrad(ctypes.c_void_p(wd.data_ptr()), cout, cin, 1, dtype,
+                                   ctypes.c_void_p(pk.data_ptr()), None))
+    base0 = torch.randn(B, *grid, c0, generator=g).to(tdt)
+    base1 = torch.randn(B, *grid, c1, generator=g).to(tdt)
+    o0, o1 = base0.to(DEV).clone(), base1.to(DEV).clone()
+    a = _nd(dy).to(DEV, tdt)
+    d = _lib.ConvDesc()
+    d.dtype, d.B, (d.D, d.H, d.W), d.cout = dtype, B, grid, cin
+    d.b0, d.b_c0, d.b_w = a.data_ptr(), cout, pk.data_ptr()
+    d.res_mode = -1
+    d.out, d.out_dtype, d.out1, d.out_c0, d.accumulate = o0.data_ptr(), dtype, o1.data_ptr(), c0, 1
+    nws = L.cwdm_conv3d_workspace_bytes(ctypes.byref(d))
+    ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=DEV)
+    d.workspace, d.ws_bytes = ws.data_ptr(), nws
+    check(L.cwdm_conv3d_forward(ctypes.byref(d), None))
+    got = torch.cat([o0.float().cpu() - base0.float(), o1.float().cpu() - base1.float()], -1)
+    tol = 2e-5 if dtype_name == "fp32" else 3e-2
+    assert rel_err(_nc(got), ref) < tol
+
+
+# --------------------------------------------------------------------------- GN/SiLU backward
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("chans", [(64, 0), (32, 32)])
+def test_gn_silu_bwd_vs_autograd(chans, mode, dtype_name):
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import check, lib
+    dtype, tdt = _dt(dtype_name)
+    c0, c1 = chans
+    C, G, B = c0 + c1, 8, 2
+    grid = (4, 8, 6)
+    g = torch.Generator().manual_seed(9)
+    x = (1.5 * torch.randn(B, C, *grid, generator=g) + 0.3).to(tdt).float()
+    gamma = 1 + 0.1 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    ugrid = {0: grid, 1: tuple(2 * s for s in grid), 2: tuple(s // 2 for s in grid)}[mode]
+    du = torch.randn(B, C, *ugrid, generator=g).to(tdt).float()
+    xr = x.clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    y = F.silu(F.group_norm(xr, G, gr, br, eps=1e-5))
+    if mode == 1:
+        y = F.interpolate(y, scale_factor=2, mode="nearest")
+    elif mode == 2:
+        y = F.avg_pool3d(y, 2)
+    (y * du).sum().backward()
+    # forward statistics as cwdm_gn_finalize produces them
+    xg = x.view(B, G, -1).double()
+    mean = xg.mean(-1)
+    rstd = 1.0 / torch.sqrt(xg.var(-1, unbiased=False) + 1e-5)
+    mr = torch.stack([mean, rstd], -1).float().contiguous()
+    cpg = C // G
+    sc = gamma[None] * rstd.float().repeat_interleave(cpg, 1)
+    sh = beta[None] - mean.float().repeat_interleave(cpg, 1) * sc
+    ss = torch.stack([sc, sh], -1).contiguous()
+    xd = _nd(x).to(DEV, tdt)
+    x0 = xd[..., :c0].contiguous()
+    x1 = xd[..., c0:].contiguous() if c1 else None
+    dud = _nd(du).to(DEV, tdt)
+    base0 = (0.01 * torch.randn(B, *grid, c0, generator=g)).to(tdt)
+    dx0 = base0.to(DEV).clone()             # acc0 = 1
+    dx1 = torch.empty(B, *grid, c1, device=DEV, dtype=tdt) if c1 else None   # acc1 = 0
+    dgam = torch.empty(C, device=DEV)
+    dbet = torch.empty(C, device=DEV)
+    L = lib()
+    nws = L.cwdm_gn_silu_bwd_workspace_bytes(C, B, *grid)
+    ws = torch.empty(nws, dtype=torch.uint8, device=DEV)
+    ssd, mrd, gd = ss.to(DEV), mr.to(DEV), gamma.to(DEV)
+    check(L.cwdm_gn_silu_bwd(x0.data_ptr(), c0, x1.data_ptr() if c1 else None, c1, dud.data_ptr(), mode,
+                             ssd.data_ptr(), mrd.data_ptr(), gd.data_ptr(), G, B, *grid, dtype,
+                             dx0.data_ptr(), 1, dx1.data_ptr() if c1 else None, 0, dgam.data_ptr(), dbet.data_ptr(),
+                             ws.data_ptr(), nws, None))
+    got = dx0.float().cpu() - base0.float()
+    if c1:
+        got = torch.cat([got, dx1.float().cpu()], -1)
+    tol = 1e-4 if dtype_name == "fp32" else 3e-2
+    assert rel_err(_nc(got), xr.grad) < tol
+    assert rel_err(dgam, gr.grad) < tol
+    assert rel_err(dbet, br.grad) < tol
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_resample_add_and_channel_sum(mode):
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import check, lib
+    L = lib()
+    g = torch.Generator().manual_seed(10)
+    B, C, grid = 2, 16, (4, 6, 8)
+    sgrid = {0: grid, 1: tuple(2 * s for s in grid), 2: tuple(s // 2 for s in grid)}[mode]
+    src = torch.randn(B, C, *sgrid, generator=g)
+    dst0 = torch.randn(B, C, *grid, generator=g)
+    xr = torch.zeros(B, C, *grid, requires_grad=True)
+    y = {0: xr, 1: F.interpolate(xr, scale_factor=2, mode="nearest") if mode == 1 else None,
+         2: F.avg_pool3d(xr, 2) if mode == 2 else None}[mode]
+    (y * src).sum().backward()
+    d = _nd(dst0).to(DEV)
+    s = _nd(src).to(DEV)
+    check(L.cwdm_resample_add(d.data_ptr(), s.data_ptr(), C, B, *grid, mode, 1, _lib.CWDM_F32, None))
+    assert rel_err(_nc(d.cpu()) - dst0, xr.grad) < 1e-6
+    out_bc = torch.zeros(B, 24, device=DEV)
+    out_c = torch.zeros(C, device=DEV)
+    check(L.cwdm_channel_sum(s.data_ptr(), _lib.CWDM_F32, B, s[0, ..., 0].numel(), 12, C, out_bc.data_ptr(), 24,
+                             out_c.data_ptr(), None, None))
+    ref_bc = src.sum(dim=(2, 3, 4))[:, :12]
+    assert rel_err(out_bc[:, :12], ref_bc) < 1e-5
+    assert rel_err(out_c[:12], ref_bc.sum(0)) < 1e-5
+
+
+def test_adamw_matches_torch():
+    from cwdm_hip._lib import check, lib
+    g = torch.Generator().manual_seed(11)
+    n = 10007
+    p0 = torch.randn(n, generator=g)
+    pr = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([pr], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, foreach=False)
+    p = p0.to(DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    for step in range(1, 4):
+        grad = torch.randn(n, generator=g)
+        pr.grad = grad.clone()
+        opt.step()
+        gd = grad.to(DEV)
+        check(lib().cwdm_adamw(p.data_ptr(), gd.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-8,
+                               0.01, step, None))
+    assert rel_err(p, pr.detach()) < 1e-6
+    st = opt.state[pr]
+    assert rel_err(m, st["exp_avg"]) < 1e-6
+    assert rel_err(v, st["exp_avg_sq"]) < 1e-6
+
+
+# --------------------------------------------------------------------------- whole U-Net backward
+def _product_model(cfg, groups, params, dtype):
+    from guided_diffusion.unet import UNetModel
+    m = UNetModel(image_size=32, in_channels=cfg["in_channels"], model_channels=cfg["model_channels"],
+                  out_channels=cfg["out_channels"], num_res_blocks=cfg["num_res_blocks"], attention_resolutions=(),
+                  channel_mult=cfg["channel_mult"], dims=3, resblock_updown=True, bottleneck_attention=False,
+                  resample_2d=False, num_groups=groups, compute_dtype=dtype)
+    m.load_state_dict(params)
+    return m.to(DEV)
+
+
+def _unet_grads(cfg, G, P, x, t, R, dtype):
+    model = _product_model(cfg, G, P, dtype)
+    out = model(x.to(DEV), t.to(DEV))
+    (out * R.to(DEV)).sum().backward()
+    return out.detach().cpu(), {n: p.grad.detach().cpu() for n, p in model.named_parameters()}, model
+
+
+def _oracle_grads(cfg, G, P, x, t, R):
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    out = ou.unet_forward(Pr, x, t, num_groups=G, **cfg)
+    (out * R).sum().backward()
+    return out.detach(), {k: v.grad for k, v in Pr.items()}
+
+
+@pytest.mark.parametrize("dtype,tol", [("fp32", 1e-3), ("bf16", 8e-2)])
+def test_unet_backward_vs_oracle_autograd(dtype, tol):
+    cfg, G = cases.C1_CFG, cases.C1_GROUPS
+    P = ou.random_params(seed=21, **cfg)
+    g = torch.Generator().manual_seed(22)
+    x = torch.randn(2, 32, 16, 16, 16, generator=g)
+    t = torch.tensor([5, 700])
+    R = torch.randn(2, 8, 16, 16, 16, generator=g)
+    out, grads, model = _unet_grads(cfg, G, P, x, t, R, dtype)
+    ref_out, ref = _oracle_grads(cfg, G, P, x, t, R)
+    assert rel_err(out, ref_out) < tol
+    assert set(grads) == set(ref)
+    worst = {}
+    for k in ref:
+        a, b = grads[k].double(), ref[k].double()
+        worst[k] = float((a - b).norm() / b.norm().clamp_min(1e-30))
+    bad = {k: v for k, v in worst.items() if v > tol}
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:8]
+    # the flat gradient the native backward wrote is what the optimizer sees
+    flat = model.flat_grad()
+    assert flat.numel() == sum(p.numel() for p in model.parameters())
+
+
+def test_unet_backward_segments_and_hook():
+    """Segment-wise backward with a per-segment hook (DDP bucket seam) gives the
+    same gradients and covers the flat buffer exactly once."""
+    cfg, G = cases.C1_CFG, cases.C1_GROUPS
+    P = ou.random_params(seed=23, **cfg)
+    g = torch.Generator().manual_seed(24)
+    x = torch.randn(1, 32, 16, 16, 16, generator=g)
+    t = torch.tensor([42])
+    R = torch.randn(1, 8, 16, 16, 16, generator=g)
+    _, g_all, _ = _unet_grads(cfg, G, P, x, t, R, "fp32")
+    model = _product_model(cfg, G, P, "fp32")
+    seen = []
+
+    def hook(seg, flat, off, n):
+        if seg is not None:
+            seen.append((seg, off, n))
+    model._grad_hook = hook
+    out = model(x.to(DEV), t.to(DEV))
+    (out * R.to(DEV)).sum().backward()
+    n = sum(p.numel() for p in model.parameters())
+    assert sum(s[2] for s in seen) == n
+    assert [s[0] for s in seen] == list(range(model.plan.num_segments))
+    for name, p in model.named_parameters():
+        assert rel_err(p.grad, g_all[name]) < 1e-5, name
+
+
+def _c1_model_and_diffusion(P, dtype="fp32"):
+    from guided_diffusion import script_util
+    args = script_util.run_sh_model_args(num_channels=32, channel_mult="1,2", num_res_blocks=1, num_groups=8)
+    keys = script_util.model_and_diffusion_defaults().keys()
+    model, diffusion = script_util.create_model_and_diffusion(**{k: args[k] for k in keys})
+    model.set_compute_dtype(dtype)
+    model.load_state_dict(P)
+    return model.to(DEV), diffusion
+
+
+def test_training_step_vs_oracle():
+    """training_losses -> loss.backward() -> FlatAdamW.step() (TrainLoop.forward_backward
+    + run_step) against the oracle's loss/autograd and torch.optim.AdamW."""
+    from cwdm_hip.optim import FlatAdamW
+    from oracle import diffusion as od
+    vols = {k: v.to(DEV) for k, v in cases.data.brats_batch(32, seed=4, batch=2).items()}
+    P = ou.random_params(seed=31, **cases.C1_CFG)
+    model, diffusion = _c1_model_and_diffusion(P)
+    t = torch.tensor([5, 700], device=DEV)
+    noise = torch.randn(2, 1, 32, 32, 32, device=DEV)
+    terms, out, _ = diffusion.training_losses(model, vols, t, mode="i2i", contr="t2w", noise=noise)
+    loss = terms["mse_wav"].mean()
+    loss.backward()
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"))
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+
+    def om(x, tt, **kw):
+        return ou.unet_forward(Pr, x, tt, num_groups=8, **cases.C1_CFG)
+    rterms, rout, _ = od.training_losses(tab, om, {k: v.cpu() for k, v in vols.items()}, t.cpu(), noise.cpu(),
+                                         contr="t2w")
+    rloss = rterms["mse_wav"].mean()
+    rloss.backward()
+    assert abs(float(loss) - float(rloss)) / float(rloss) < 1e-4
+    for n, p in model.named_parameters():
+        err = float((p.grad.double().cpu() - Pr[n].grad.double()).norm() / Pr[n].grad.double().norm().clamp_min(1e-30))
+        assert err < 1e-3, (n, err)
+    # optimizer: one fused launch == torch.optim.AdamW on the same gradients
+    p0 = model.flat_params.detach().clone()
+    g = model.flat_grad().detach().clone()
+    opt = FlatAdamW(model, lr=1e-3, weight_decay=0.01)
+    opt.step()
+    ref = p0.cpu().clone().requires_grad_(True)
+    topt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=0.01, foreach=False)
+    ref.grad = g.cpu()
+    topt.step()
+    assert rel_err(model.flat_params, ref.detach()) < 1e-6
+    # the packed kernel weights follow the update
+    with torch.no_grad():
+        o2 = model(torch.randn(1, 32, 16, 16, 16, device=DEV), torch.tensor([3], device=DEV))
+    assert torch.isfinite(o2).all()
+
+
+def test_trainloop_runs_and_learns(tmp_path, monkeypatch):
+    from guided_diffusion import dist_util, train_util
+    monkeypatch.setenv("CWDM_LOGDIR", str(tmp_path))
+    dist_util.setup_dist()
+    P = ou.random_params(seed=41, **cases.C1_CFG)
+    model, diffusion = _c1_model_and_diffusion(P)
+    batch = cases.data.brats_batch(32, seed=5, batch=1)
+    data = [batch] * 2
+    loop = train_util.TrainLoop(model=model, diffusion=diffusion, data=data, batch_size=1, in_channels=32,
+                                image_size=64, microbatch=-1, lr=1e-4, ema_rate="0.9999", log_interval=1,
+                                contr="t1n", save_interval=100, resume_checkpoint="", resume_step=0,
+                                lr_anneal_steps=4, mode="i2i", diffusion_steps=1000)
+    p0 = model.flat_params.detach().clone()
+    loop.run_loop()
+    assert loop.step == 4
+    assert not torch.equal(p0, model.flat_params)
+    assert torch.isfinite(model.flat_params).all()
+    assert float(loop.last_info["norm/grad_max"]) > 0
+    assert os.path.exists(os.path.join(tmp_path, "checkpoints", "brats_t1n_BEST_direct_1000.pt"))
+    sd = torch.load(os.path.join(tmp_path, "checkpoints", "brats_t1n_BEST_direct_1000.pt"), weights_only=True)
+    assert set(sd) == set(P)
