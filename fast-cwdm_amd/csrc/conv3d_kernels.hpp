@@ -138,6 +138,20 @@ struct Stager {
     *hv = (*hz * HY + *hy) * HX + *hx;
   }
 
+  // GroupNorm scale/shift of this thread's quad (fetch() does it unless told
+  // to defer it, so the 2*EPQ registers are not live while the loads fly)
+  __device__ __forceinline__ void load_gn(const ConvParams& p, int chunk, int b, int tid) {
+    const int q = tid & 1;
+    const int cb = chunk * CK + q * EPQ;
+    const int ctot = p.ac0 + p.ac1;
+#pragma unroll
+    for (int e = 0; e < EPQ; ++e) {
+      sc[e] = p.agn[((long long)b * ctot + cb + e) * 2 + 0];
+      sh[e] = p.agn[((long long)b * ctot + cb + e) * 2 + 1];
+    }
+  }
+
+  template <bool LOAD_GN = true>
   __device__ __forceinline__ void fetch(const ConvParams& p, bool segA, int chunk, int b, int x0, int y0, int z0,
                                         int tid) {
     seg_a = segA;
@@ -149,7 +163,7 @@ struct Stager {
     if (cb < c0) { src = segA ? p.a0 : p.b0; ch = cb; csrc = c0; }
     else { src = segA ? p.a1 : p.b1; ch = cb - c0; csrc = c1; }
     base = reinterpret_cast<const T*>(src) + ch;
-    if (GN && segA) {
+    if (GN && segA && LOAD_GN) {
       const int ctot = c0 + c1;
 #pragma unroll
       for (int e = 0; e < EPQ; ++e) {

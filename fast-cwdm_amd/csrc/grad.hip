@@ -50,27 +50,30 @@ template <> __device__ __forceinline__ void store8<bf16_t>(bf16_t* p, const floa
 // path of resample_add (an undefined register in the address -> aperture
 // violation), so every caller is instantiated per mode.
 template <typename T, int MODE>
-__device__ __forceinline__ void load_du(const T* du, int C, int c, int b, int z, int y, int x, int d, int h, int w,
-                                        float* f) {
-  constexpr int mode = MODE;
-  if constexpr (mode == 0) {
-    load8<T>(du + ((((long long)b * d + z) * h + y) * w + x) * C + c, f);
-  } else if constexpr (mode == 1) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = 0.f;
-    const int D2 = 2 * d, H2 = 2 * h, W2 = 2 * w;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float g[8];
-      load8<T>(du + ((((long long)b * D2 + 2 * z + (k >> 2)) * H2 + 2 * y + ((k >> 1) & 1)) * W2 + 2 * x + (k & 1)) * C + c,
-               g);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] += g[e];
-    }
+__device__ __forceinline__ void load_du(const T* du, int C, int c, int b, unsigned v, int d, int h, int w, float* f) {
+  if constexpr (MODE == 0) {
+    load8<T>(du + ((long long)b * ((long long)d * h * w) + v) * C + c, f);
   } else {
-    load8<T>(du + ((((long long)b * (d >> 1) + (z >> 1)) * (h >> 1) + (y >> 1)) * (w >> 1) + (x >> 1)) * C + c, f);
+    const unsigned x = v % (unsigned)w, yz = v / (unsigned)w;
+    const unsigned y = yz % (unsigned)h, z = yz / (unsigned)h;
+    if constexpr (MODE == 1) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] *= 0.125f;
+      for (int e = 0; e < 8; ++e) f[e] = 0.f;
+      const int D2 = 2 * d, H2 = 2 * h, W2 = 2 * w;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float g[8];
+        load8<T>(du + ((((long long)b * D2 + 2 * z + (k >> 2)) * H2 + 2 * y + ((k >> 1) & 1)) * W2 + 2 * x + (k & 1)) * C +
+                     c,
+                 g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += g[e];
+      }
+    } else {
+      load8<T>(du + ((((long long)b * (d >> 1) + (z >> 1)) * (h >> 1) + (y >> 1)) * (w >> 1) + (x >> 1)) * C + c, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] *= 0.125f;
+    }
   }
 }
 
@@ -107,10 +110,9 @@ __global__ void __launch_bounds__(256) gn_bwd_reduce_kernel(const T* __restrict_
   if (slot < nslots) {
     const long long v0 = blk * vpb, v1 = v0 + vpb < V ? v0 + vpb : V;
     for (long long v = v0 + slot; v < v1; v += nslots) {
-      const int x = (int)(v % w), y = (int)((v / w) % h), z = (int)(v / ((long long)w * h));
       float xv[8], g[8];
       load8<T>(xs + ((long long)b * V + v) * xc + xo, xv);
-      load_du<T, MODE>(du, C, c, b, z, y, x, d, h, w, g);
+      load_du<T, MODE>(du, C, c, b, (unsigned)v, d, h, w, g);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float dz = dsilu(xv[e] * sc[e] + sh[e], g[e]);
@@ -142,23 +144,44 @@ __global__ void __launch_bounds__(512) gn_bwd_finalize_kernel(const float* __res
                                                              const float* __restrict__ mr, int groups,
                                                              long long V, float* __restrict__ coef,
                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  __shared__ double sA[1024], sB[1024], s1[256], s2[256];
+  __shared__ double sA[1024], sB[1024], s1[256], s2[256], rA[512], rB[512];
   const int cpg = C / groups;
+  // C <= 512: `sub` threads per channel split the partial blocks; C > 512: 2 channels per thread
+  const int sub = C <= 512 ? 512 / C : 1;
+  const int cpt = C <= 512 ? 1 : 2;
   double dg[2] = {0.0, 0.0}, db[2] = {0.0, 0.0};
   for (int b = 0; b < B; ++b) {
-    for (int k = 0; k < 2; ++k) {
-      const int c = threadIdx.x + 512 * k;
-      if (c < C) {
-        double a = 0.0, bb = 0.0;
-        for (int i = 0; i < nblk; ++i) {
-          a += (double)part[(((long long)b * nblk + i) * C + c) * 2];
-          bb += (double)part[(((long long)b * nblk + i) * C + c) * 2 + 1];
+    for (int k = 0; k < cpt; ++k) {
+      const int c = cpt == 1 ? threadIdx.x % C : threadIdx.x + 512 * k;
+      const int j = cpt == 1 ? threadIdx.x / C : 0;
+      double a = 0.0, bb = 0.0;
+      if (c < C && j < sub) {
+        for (int i = j; i < nblk; i += sub) {
+          const float2 v = *reinterpret_cast<const float2*>(part + (((long long)b * nblk + i) * C + c) * 2);
+          a += (double)v.x;
+          bb += (double)v.y;
         }
+      }
+      if (cpt == 1) {
+        rA[threadIdx.x] = a; rB[threadIdx.x] = bb;
+      } else if (c < C) {
         sA[c] = a; sB[c] = bb;
-        dg[k] += bb; db[k] += a;
       }
     }
     __syncthreads();
+    if (cpt == 1 && threadIdx.x < C) {
+      double a = 0.0, bb = 0.0;
+      for (int j = 0; j < sub; ++j) {
+        a += rA[j * C + threadIdx.x];
+        bb += rB[j * C + threadIdx.x];
+      }
+      sA[threadIdx.x] = a; sB[threadIdx.x] = bb;
+    }
+    __syncthreads();
+    for (int k = 0; k < 2; ++k) {
+      const int c = threadIdx.x + 512 * k;
+      if (c < C) { dg[k] += sB[c]; db[k] += sA[c]; }
+    }
     if (threadIdx.x < groups) {
       const int g = threadIdx.x;
       double a = 0.0, bb = 0.0;
@@ -206,7 +229,6 @@ __global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__
   const int cg = (int)(i % ncg);
   const long long v = i / ncg;
   const int c = cg * 8;
-  const int x = (int)(v % w), y = (int)((v / w) % h), z = (int)(v / ((long long)w * h));
   const bool first = c < c0;
   const T* xs = first ? x0 : x1;
   T* dx = first ? dx0 : dx1;
@@ -214,7 +236,7 @@ __global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__
   const int acc = first ? acc0 : acc1;
   float xv[8], g[8], o[8];
   load8<T>(xs + ((long long)b * V + v) * xc + xo, xv);
-  load_du<T, MODE>(du, C, c, b, z, y, x, d, h, w, g);
+  load_du<T, MODE>(du, C, c, b, (unsigned)v, d, h, w, g);
   if (acc) load8<T>(dx + ((long long)b * V + v) * xc + xo, o);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -236,9 +258,8 @@ __global__ void __launch_bounds__(256) resample_add_kernel(T* __restrict__ dst, 
   if (i >= V * ncg) return;
   const int c = (int)(i % ncg) * 8;
   const long long v = i / ncg;
-  const int x = (int)(v % w), y = (int)((v / w) % h), z = (int)(v / ((long long)w * h));
   float g[8], o[8];
-  load_du<T, MODE>(src, C, c, b, z, y, x, d, h, w, g);
+  load_du<T, MODE>(src, C, c, b, (unsigned)v, d, h, w, g);
   T* p = dst + ((long long)b * V + v) * C + c;
   if (acc) {
     load8<T>(p, o);
@@ -327,15 +348,23 @@ __global__ void __launch_bounds__(256) emb_bwd_w_kernel(const float* __restrict_
   }
 }
 
+// dsil[b][e] += sum_r W[r][e] * dEb[b][r]: 64 e x 4 row groups per block,
+// row chunks of 32 over grid.z, fp32 atomics
 __global__ void __launch_bounds__(256) emb_bwd_x_kernel(const float* __restrict__ dEb, int R, int n,
                                                        const float* __restrict__ W, int E,
                                                        float* __restrict__ dsil) {
+  __shared__ float red[256];
   const int b = blockIdx.y;
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= E) return;
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  const int r0 = blockIdx.z * 32;
   float s = 0.f;
-  for (int r = 0; r < n; ++r) s += W[(long long)r * E + e] * dEb[(long long)b * R + r];
-  dsil[(long long)b * E + e] += s;
+  if (e < E)
+    for (int r = r0 + rg; r < r0 + 32 && r < n; r += 4) s += W[(long long)r * E + e] * dEb[(long long)b * R + r];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (rg == 0 && e < E)
+    atomicAdd(dsil + (long long)b * E + e, red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] +
+                                              red[threadIdx.x + 192]);
 }
 
 // time_embed MLP backward (unet.py:534-539): one workgroup, batch looped.
@@ -408,7 +437,7 @@ int dispatch_mode(int mode, F&& f) {
 long long gn_bwd_blocks(int C, long long V) {
   (void)C;
   long long nb = ceil_div(V, 512);
-  if (nb > 1024) nb = 1024;
+  if (nb > 512) nb = 512;
   if (nb < 1) nb = 1;
   return nb;
 }
@@ -420,7 +449,8 @@ int launch_emb_bwd(const float* dEb, int R, int n, int B, const float* temb, int
   hipLaunchKernelGGL(emb_bwd_w_kernel, dim3((unsigned)ceil_div((long long)n * E, 256)), dim3(256), 0, s, dEb, R, n,
                      B, temb, E, dw, db, dcb);
   CWDM_LAUNCHED();
-  hipLaunchKernelGGL(emb_bwd_x_kernel, dim3((unsigned)ceil_div(E, 256), B), dim3(256), 0, s, dEb, R, n, W, E, dsil);
+  hipLaunchKernelGGL(emb_bwd_x_kernel, dim3((unsigned)ceil_div(E, 64), B, (unsigned)ceil_div(n, 32)), dim3(256), 0, s,
+                     dEb, R, n, W, E, dsil);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }

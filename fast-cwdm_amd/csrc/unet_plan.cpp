@@ -653,7 +653,7 @@ namespace {
 
 struct GLayout {
   std::vector<int64_t> g_off;
-  int64_t tmp, dout, deb, dsil, gnws, gnws_bytes, split, split_bytes, total;
+  int64_t tmp, dout, deb, dsil, gnws, gnws_bytes, split, split_bytes, wgws, total;
 };
 
 int ckpad(const cwdm_unet* u, int c) {
@@ -686,7 +686,11 @@ GLayout glayout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) 
     if ((int)i == u->input_tensor) { G.g_off.push_back(-1); continue; }
     G.g_off.push_back(take(B * (D >> t.level) * (H >> t.level) * (W >> t.level) * t.channels * es));
   }
-  int64_t tmp = 0, split = 0, gnws = 0;
+  int64_t tmp = 0, split = 0, gnws = 0, wgws = 0;
+  for (const auto& cs : u->convs) {
+    wgws = std::max(wgws, cwdm_conv3d_wgrad_workspace_bytes(cs.cout, cs.cin_a, 3));
+    if (cs.ws_p >= 0) wgws = std::max(wgws, cwdm_conv3d_wgrad_workspace_bytes(cs.cout, cs.cin_b, 1));
+  }
   for (size_t i = 1; i < u->convs.size(); ++i) {
     const auto& cs = u->convs[i];
     const int64_t v = B * (D >> cs.level) * (H >> cs.level) * (W >> cs.level);
@@ -706,6 +710,7 @@ GLayout glayout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) 
   G.gnws = take(gnws);
   G.split_bytes = split;
   G.split = take(split);
+  G.wgws = take(wgws);
   G.total = off;
   return G;
 }
@@ -821,6 +826,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
     d.dtype = dt; d.B = B; d.D = D >> level; d.H = H >> level; d.W = W >> level; d.ksize = ksize;
     d.u0 = u0; d.u_c0 = uc0; d.u1 = u1; d.u_c1 = uc1; d.u_mode = umode; d.u_gn = ugn;
     d.dy = dy; d.dy_cs = dy_cs; d.cout = cout; d.dw = dw;
+    d.workspace = gb + G.wgws;
     return cwdm_conv3d_wgrad(&d, stream);
   };
   auto dgrad = [&](int ci, const void* dy) -> int {

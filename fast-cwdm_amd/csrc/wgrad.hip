@@ -10,19 +10,20 @@
 // nearest-x2 upsample, two-source concat, zero padding), so nothing but the
 // raw activations is kept for the backward.
 //
-// Work decomposition (one 512-thread workgroup = 8 waves, 1 per CU):
+// Work decomposition (one 256-thread workgroup = 4 waves, one wave per SIMD
+// so each wave holds its 7 taps x 64 x 32 fp32 accumulators in AGPRs):
 //   * tile = 32*MC output channels x 32 input channels x all taps; K is walked
 //     in bricks of 16x4x4 voxels (a range of bricks per workgroup, split over
 //     the grid; partial tiles are combined with fp32 atomics).
-//   * per brick: waves 0-3 / 4-7 stage the halo of input-channel chunks into
-//     LDS (one image per 16-channel chunk, 32-B rows), all threads stage the
-//     brick's dY rows [voxel][co].
+//   * per brick: the halo of the two 16-channel input chunks (one LDS image
+//     each, 32-B rows) and the brick's dY rows [voxel][co] are committed from
+//     registers that were loaded while the previous brick's MFMAs ran.
 //   * both MFMA operands need K (voxels) along the lane's 8 elements while
 //     LDS rows hold channels: bf16 reads them with the gfx950 transposed LDS
 //     read ds_read_b64_tr_b16 (4 voxel rows x 16 channels per 16-lane group),
 //     so no transposed copy is ever written.
-//   * 3x3x3: wave w owns taps {w, w+8, w+16, w+24}; the dY fragments of a
-//     K-step are read once and reused for all its taps.  1x1: the 8 waves split
+//   * 3x3x3: wave w owns taps {w, w+4, ..., <27}; the dY fragments of a
+//     K-step are read once and reused for all its taps.  1x1: the 4 waves split
 //     the K-steps instead.
 // fp32 (parity mode) runs the same structure on exact-fp32 v_mfma_f32_32x32x2_f32.
 #include "conv3d_kernels.hpp"
@@ -75,28 +76,6 @@ __device__ __forceinline__ int dy_quad(int qd, int v) {
   else return qd;
 }
 
-template <typename T, int MC>
-__device__ __forceinline__ void stage_dy(const WgradParams& p, unsigned char* dyl, int b, int x0, int y0, int z0,
-                                         int co0, int tid) {
-  using C = WgCfg<T, MC>;
-  constexpr int QPV = C::DYP / 16;  // quads per voxel row
-  constexpr int EPQ = 16 / (int)sizeof(T);
-  constexpr int NQ = 256 * QPV;
-#pragma unroll
-  for (int j = 0; j < NQ / 512; ++j) {
-    const int q = tid + 512 * j;
-    const int v = q / QPV, qd = q % QPV;
-    const int x = x0 + (v & 15), y = y0 + ((v >> 4) & 3), z = z0 + (v >> 6);
-    const int c = co0 + qd * EPQ;
-    u32x4 val = u32x4{0u, 0u, 0u, 0u};
-    if (x < p.cp.W && y < p.cp.H && z < p.cp.D && c < p.dy_cs) {
-      const long long vox = (((long long)b * p.cp.D + z) * p.cp.H + y) * p.cp.W + x;
-      val = ldg16(reinterpret_cast<const T*>(p.dy) + vox * p.dy_cs + c);
-    }
-    *reinterpret_cast<u32x4*>(dyl + v * C::DYP + dy_quad<T, MC>(qd, v) * 16) = val;
-  }
-}
-
 // halo offset (in rows) of tap t = (kz, ky, kx)
 __device__ __forceinline__ int tap_rows(int t) {
   const int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;
@@ -104,69 +83,101 @@ __device__ __forceinline__ int tap_rows(int t) {
 }
 
 template <typename T, int MC, int MODE, bool GN, int TAPS>
-__global__ void __launch_bounds__(512) wgrad_kernel(WgradParams p) {
+__global__ void __launch_bounds__(256) wgrad_kernel(WgradParams p) {
   using C = WgCfg<T, MC>;
   constexpr int CK = C::CK, NCH = C::NCH;
+  constexpr int QPV = C::DYP / 16;          // dY quads per voxel row
+  constexpr int EPQ = 16 / (int)sizeof(T);
+  constexpr bool PF = sizeof(T) == 2;       // register prefetch of the next brick (bf16)
+  constexpr int NT = TAPS == 27 ? 7 : 1;    // taps per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* halo = smem;
   unsigned char* dyl = smem + C::DY_OFF;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const int half = tid >> 8, htid = tid & 255;
   const int ct = blockIdx.y % p.nco, it = blockIdx.y / p.nco;
   const int co0 = ct * C::CO, ci0 = it * 32;
   const long long bb = (long long)blockIdx.x * p.per;
   const long long be = bb + p.per < p.nbricks ? bb + p.per : p.nbricks;
   constexpr bool SEGA = TAPS == 27;
 
-  // this wave's taps (3x3x3) or K-steps (1x1)
-  int ntap, toff[4];
-  if constexpr (TAPS == 27) {
-    ntap = wv < 3 ? 4 : 3;
+  // taps of this wave: w, w+4, w+8, ... (7/7/7/6); 1x1: the waves split the K-steps
+  const int ntap = TAPS == 27 ? (wv < 3 ? 7 : 6) : 1;
+  int toff[NT];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) toff[k] = tap_rows(wv + 8 * k < 27 ? wv + 8 * k : 0);
-  } else {
-    ntap = 1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) toff[k] = tap_rows(13);
-  }
+  for (int k = 0; k < NT; ++k) toff[k] = TAPS == 27 ? tap_rows(wv + 4 * k < 27 ? wv + 4 * k : 0) : tap_rows(13);
 
-  f32x16 acc[4][MC];
+  f32x16 acc[NT][MC];
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < NT; ++k)
 #pragma unroll
     for (int m = 0; m < MC; ++m)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[k][m][i] = 0.f;
 
-  Stager<T, WBX, WBY, WBZ, MODE, GN> sg;
+  Stager<T, WBX, WBY, WBZ, MODE, GN> sg[NCH];
+  u32x4 dyr[QPV];
   const int nb_vol = p.tx * p.ty * p.tz;
-  for (long long bi = bb; bi < be; ++bi) {
+  int fb = 0;  // batch index of the fetched brick
+
+  // global -> registers for brick bi (nothing waits here)
+  auto fetch = [&](long long bi) {
     const int b = (int)(bi / nb_vol);
+    fb = b;
     int r = (int)(bi % nb_vol);
     const int x0 = (r % p.tx) * WBX;
     r /= p.tx;
     const int y0 = (r % p.ty) * WBY;
     const int z0 = (r / p.ty) * WBZ;
-    __syncthreads();  // previous brick's reads are done
-    sg.cached = false;
 #pragma unroll
-    for (int c = half; c < NCH; c += 2) {
-      sg.fetch(p.cp, SEGA, ci0 / CK + c, b, x0, y0, z0, htid);
-      sg.template store<false>(halo + c * WIMG, p.cp, b, x0, y0, z0, htid);
+    for (int c = 0; c < NCH; ++c) {
+      sg[c].cached = false;
+      sg[c].template fetch<false>(p.cp, SEGA, ci0 / CK + c, b, x0, y0, z0, tid);
     }
-    stage_dy<T, MC>(p, dyl, b, x0, y0, z0, co0, tid);
+#pragma unroll
+    for (int j = 0; j < QPV; ++j) {
+      const int q = tid + 256 * j;
+      const int v = q / QPV, qd = q % QPV;
+      const int x = x0 + (v & 15), y = y0 + ((v >> 4) & 3), z = z0 + (v >> 6);
+      const int cc = co0 + qd * EPQ;
+      const bool in = x < p.cp.W && y < p.cp.H && z < p.cp.D && cc < p.dy_cs;
+      const long long vox = in ? (((long long)b * p.cp.D + z) * p.cp.H + y) * p.cp.W + x : 0;
+      const u32x4 val = ldg16(reinterpret_cast<const T*>(p.dy) + vox * p.dy_cs + (in ? cc : 0));
+      const unsigned keep = in ? ~0u : 0u;
+      dyr[j] = u32x4{val[0] & keep, val[1] & keep, val[2] & keep, val[3] & keep};
+    }
+  };
+  // registers -> LDS (GroupNorm + SiLU / zero padding applied here)
+  auto commit = [&]() {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (GN && SEGA) sg[c].load_gn(p.cp, ci0 / CK + c, fb, tid);
+      sg[c].transform();
+      sg[c].template write<false>(halo + c * WIMG, tid);
+    }
+#pragma unroll
+    for (int j = 0; j < QPV; ++j) {
+      const int q = tid + 256 * j;
+      const int v = q / QPV, qd = q % QPV;
+      *reinterpret_cast<u32x4*>(dyl + v * C::DYP + dy_quad<T, MC>(qd, v) * 16) = dyr[j];
+    }
+  };
+
+  if (PF && bb < be) fetch(bb);
+  for (long long bi = bb; bi < be; ++bi) {
+    __syncthreads();  // previous brick's LDS reads are done
+    if (!PF) fetch(bi);
+    commit();
     __syncthreads();
+    if (PF && bi + 1 < be) fetch(bi + 1);  // next brick's loads fly during the MFMAs
 
     if constexpr (sizeof(T) == 2) {
-      // lane roles in the transposed reads
       const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, h = g >> 1;
       const unsigned char* bimg = halo + (g & 1) * WIMG + 8 * pp;
-      constexpr int S0 = TAPS == 27 ? 0 : 0;
-      const int s_begin = TAPS == 27 ? 0 : 2 * wv, s_end = TAPS == 27 ? 16 : 2 * wv + 2;
-      (void)S0;
-      for (int s = s_begin; s < s_end; ++s) {
+      constexpr int NS = TAPS == 27 ? 16 : 4;   // K-steps of this wave
+      const int s0 = TAPS == 27 ? 0 : 4 * wv;
+      // fragments of K-step s: dY (A) for every co sub-tile, U (B) for every tap
+      auto load_frags = [&](int s, bf16x8* a, bf16x8* bfr) {
         const int y = s & 3, z = s >> 2;
-        bf16x8 a[MC];
 #pragma unroll
         for (int m = 0; m < MC; ++m) {
           const int v0 = 16 * s + 8 * h + q, v1 = v0 + 4;
@@ -175,22 +186,38 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradParams p) {
           const v4s hi = tr_read(dyl + v1 * C::DYP + dy_quad<T, MC>(qd, v1) * 16 + 8 * (pp & 1));
           a[m] = join(lo, hi);
         }
-        const int hrow = (z * WHY + y) * WHX + 8 * h + q;  // halo row of voxel (x=8h+q, y, z) at tap (0,0,0)
+        const int hrow = (z * WHY + y) * WHX + 8 * h + q;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < NT; ++k) {
           if (k < ntap) {
             const unsigned char* bp = bimg + (hrow + toff[k]) * 32;
-            const bf16x8 bf = join(tr_read(bp), tr_read(bp + 4 * 32));
-#pragma unroll
-            for (int m = 0; m < MC; ++m)
-              acc[k][m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m], bf, acc[k][m], 0, 0, 0);
+            bfr[k] = join(tr_read(bp), tr_read(bp + 4 * 32));
           }
         }
+      };
+      // software pipeline: K-step s+1's LDS reads are in flight during K-step s's MFMAs
+      bf16x8 fa0[MC], fb0[NT], fa1[MC], fb1[NT];
+      auto mfmas = [&](const bf16x8* a, const bf16x8* bfr) {
+#pragma unroll
+        for (int k = 0; k < NT; ++k) {
+          if (k < ntap) {
+#pragma unroll
+            for (int m = 0; m < MC; ++m)
+              acc[k][m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m], bfr[k], acc[k][m], 0, 0, 0);
+          }
+        }
+      };
+      load_frags(s0, fa0, fb0);
+#pragma unroll 1
+      for (int i = 0; i < NS; i += 2) {
+        load_frags(s0 + i + 1, fa1, fb1);
+        mfmas(fa0, fb0);
+        if (i + 2 < NS) load_frags(s0 + i + 2, fa0, fb0);
+        mfmas(fa1, fb1);
       }
     } else {
-      // fp32: lane holds one K element (voxel 2s + (lane >> 5)) of one row/column
       const int col = lane & 31, hh = lane >> 5;
-      const int s_begin = TAPS == 27 ? 0 : 16 * wv, s_end = TAPS == 27 ? 128 : 16 * wv + 16;
+      const int s_begin = TAPS == 27 ? 0 : 32 * wv, s_end = TAPS == 27 ? 128 : 32 * wv + 32;
       const unsigned char* bimg = halo + (col >> 3) * WIMG + (col & 7) * 4;
       for (int s = s_begin; s < s_end; ++s) {
         const int v = 2 * s + hh;
@@ -200,7 +227,7 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradParams p) {
         for (int m = 0; m < MC; ++m) a[m] = *reinterpret_cast<const float*>(dyl + v * C::DYP + (32 * m + col) * 4);
         const int hrow = (z * WHY + y) * WHX + x;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < NT; ++k) {
           if (k < ntap) {
             const float bv = *reinterpret_cast<const float*>(bimg + (hrow + toff[k]) * 32);
 #pragma unroll
@@ -212,22 +239,35 @@ __global__ void __launch_bounds__(512) wgrad_kernel(WgradParams p) {
     }
   }
 
-  // combine: fp32 atomics into dW[co][ci][tap]
+  // combine: fp32 atomics into the [tap][co][ci] scratch -- one accumulator
+  // register is two 128-B row segments (ci contiguous), the full-rate atomic
+  // shape; OIDHW order would scatter the 64 lanes over 64 rows (~17x slower)
   const int ci = ci0 + (lane & 31);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < NT; ++k) {
     if (k < ntap) {
-      const int tap = TAPS == 27 ? wv + 8 * k : 0;
+      const int tap = TAPS == 27 ? wv + 4 * k : 0;
 #pragma unroll
       for (int m = 0; m < MC; ++m)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int co = co0 + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
           if (co < p.cout && ci < p.cin)
-            atomicAdd(p.dw + ((long long)co * p.cin + ci) * TAPS + tap, acc[k][m][i]);
+            atomicAdd(p.dw + ((long long)tap * p.cout + co) * p.cin + ci, acc[k][m][i]);
         }
     }
   }
+}
+
+// dW[co][ci][tap] += scratch[tap][co][ci]
+__global__ void __launch_bounds__(256) wgrad_finish_kernel(const float* __restrict__ scr, float* __restrict__ dw,
+                                                          int cout, int cin, int taps) {
+  const long long n = (long long)cout * cin * taps;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int tap = (int)(i % taps);
+  const long long oc = i / taps;  // co * cin + ci
+  dw[i] += scr[(long long)tap * cout * cin + oc];
 }
 
 template <typename T, int MC, int MODE, bool GN, int TAPS>
@@ -236,7 +276,7 @@ int launch_wg(const WgradParams& p, dim3 grid, hipStream_t s) {
   static_assert(smem <= 160 * 1024, "wgrad LDS");
   auto k = wgrad_kernel<T, MC, MODE, GN, TAPS>;
   CWDM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, smem));
-  hipLaunchKernelGGL(k, grid, dim3(512), smem, s, p);
+  hipLaunchKernelGGL(k, grid, dim3(256), smem, s, p);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }
@@ -272,6 +312,7 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
   if (d->u_mode == 1)
     CWDM_REQUIRE(d->D % 2 == 0 && d->H % 2 == 0 && d->W % 2 == 0, CWDM_E_SHAPE,
                  "cwdm_conv3d_wgrad: upsampled grid must be even");
+  CWDM_REQUIRE(d->workspace, CWDM_E_WORKSPACE, "cwdm_conv3d_wgrad: workspace (cwdm_conv3d_wgrad_workspace_bytes) missing");
   WgradParams p{};
   ConvParams& c = p.cp;
   c.B = (int)d->B; c.D = (int)d->D; c.H = (int)d->H; c.W = (int)d->W;
@@ -280,15 +321,14 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
   } else {
     c.b0 = d->u0; c.bc0 = d->u_c0; c.b1 = d->u1; c.bc1 = d->u_c1;
   }
-  p.dy = d->dy; p.dy_cs = d->dy_cs; p.cout = d->cout; p.cin = cin; p.taps = d->ksize == 3 ? 27 : 1; p.dw = d->dw;
+  p.dy = d->dy; p.dy_cs = d->dy_cs; p.cout = d->cout; p.cin = cin; p.taps = d->ksize == 3 ? 27 : 1;
+  p.dw = reinterpret_cast<float*>(d->workspace);
   p.tx = (int)ceil_div(d->W, WBX); p.ty = (int)ceil_div(d->H, WBY); p.tz = (int)ceil_div(d->D, WBZ);
   p.nbricks = d->B * (long long)p.tx * p.ty * p.tz;
-  // MC = 2 (64-channel tiles) spills at 2 waves/SIMD with the staging state
-  // live; 32-channel tiles for now
-  const int mc = 1;
+  const int mc = d->cout > 32 ? 2 : 1;
   p.nco = (int)ceil_div(d->cout, 32 * mc);
   const long long tiles = (long long)p.nco * (cin / 32);
-  long long S = ceil_div(512, tiles);
+  long long S = ceil_div(256, tiles);
   if (S > p.nbricks) S = p.nbricks;
   if (S < 1) S = 1;
   p.per = ceil_div(p.nbricks, S);
@@ -297,6 +337,21 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
   dim3 grid((unsigned)S, (unsigned)tiles);
   hipStream_t s = (hipStream_t)stream;
   const bool gn = d->u_gn != nullptr;
-  if (d->dtype == CWDM_BF16) return dispatch_wg<bf16_t, 1>(p, d->u_mode, gn, grid, s);
-  return dispatch_wg<float, 1>(p, d->u_mode, gn, grid, s);
+  const long long nw = (long long)d->cout * cin * p.taps;
+  CWDM_HIP(hipMemsetAsync(d->workspace, 0, nw * 4, s));
+  int rc;
+  if (d->dtype == CWDM_BF16)
+    rc = mc == 2 ? dispatch_wg<bf16_t, 2>(p, d->u_mode, gn, grid, s) : dispatch_wg<bf16_t, 1>(p, d->u_mode, gn, grid, s);
+  else
+    rc = mc == 2 ? dispatch_wg<float, 2>(p, d->u_mode, gn, grid, s) : dispatch_wg<float, 1>(p, d->u_mode, gn, grid, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)ceil_div(nw, 256)), dim3(256), 0, s,
+                     reinterpret_cast<const float*>(d->workspace), d->dw, d->cout, cin, p.taps);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+extern "C" int64_t cwdm_conv3d_wgrad_workspace_bytes(int cout, int cin, int ksize) {
+  if (cout <= 0 || cin <= 0 || (ksize != 1 && ksize != 3)) return -1;
+  return (int64_t)cout * cin * ksize * ksize * ksize * 4;
 }

@@ -70,6 +70,7 @@ class WgradDesc(ctypes.Structure):
         ("u_gn", vp),
         ("dy", vp), ("dy_cs", ctypes.c_int), ("cout", ctypes.c_int),
         ("dw", vp),
+        ("workspace", vp),
     ]
 
 
@@ -103,6 +104,7 @@ _PROTOS = {
                                         ctypes.c_float, vp, vp, vp]),
     "cwdm_gn_silu_pool": (ctypes.c_int, [vp, ctypes.c_int, vp, i64, i64, i64, i64, ctypes.c_int, vp, vp, vp]),
     "cwdm_conv3d_wgrad": (ctypes.c_int, [ctypes.POINTER(WgradDesc), vp]),
+    "cwdm_conv3d_wgrad_workspace_bytes": (i64, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "cwdm_gn_silu_bwd_workspace_bytes": (i64, [ctypes.c_int, i64, i64, i64, i64]),
     "cwdm_gn_silu_bwd": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp,
                                         ctypes.c_int, i64, i64, i64, i64, ctypes.c_int, vp, ctypes.c_int, vp,

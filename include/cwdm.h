@@ -195,8 +195,11 @@ int cwdm_gn_silu_pool(const void* x, int C, const float* gn, int64_t B, int64_t 
 /* Conv3d weight gradient: dw[co][ci][tap] += sum_{b,v} dy[b,v,co] * U[b,v+tap-1,ci]
  * with U = the conv's input recomputed from the saved sources exactly as the
  * forward staged it (concat of u0/u1, optional GroupNorm scale/shift + SiLU,
- * optional nearest-x2 upsample of a half-resolution source).  dw is fp32 OIDHW,
- * accumulated with atomics (zero it first).  ksize 1: the 1x1 skip conv. */
+ * optional nearest-x2 upsample of a half-resolution source).  dw is fp32 OIDHW
+ * and is accumulated into (dw += dW).  workspace: fp32 scratch of
+ * cwdm_conv3d_wgrad_workspace_bytes (zeroed by the call; partial tiles meet
+ * there with full-rate atomics before one transposing pass into dw).
+ * ksize 1: the 1x1 skip conv. */
 typedef struct {
   int dtype;
   int64_t B, D, H, W;       /* conv (output) grid */
@@ -207,7 +210,9 @@ typedef struct {
   const float* u_gn;        /* [B][cin][2] scale/shift -> SiLU, or NULL */
   const void* dy; int dy_cs; int cout;   /* dy [B][V][dy_cs] in dtype, first cout channels */
   float* dw;                /* fp32 [cout][cin][ksize^3] */
+  void* workspace;
 } cwdm_wgrad_desc;
+int64_t cwdm_conv3d_wgrad_workspace_bytes(int cout, int cin, int ksize);
 int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* desc, cwdm_stream_t stream);
 
 /* Backward of SiLU(GroupNorm(x)) (guided_diffusion/nn.py:17-19, :93-100):

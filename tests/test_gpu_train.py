@@ -88,6 +88,8 @@ def test_conv3d_wgrad_vs_torch(case, dtype_name):
     d.u_gn = gnd.data_ptr() if gnd is not None else None
     d.dy, d.dy_cs, d.cout = dyd.data_ptr(), dy_cs, cout
     d.dw = dw.data_ptr()
+    wsw = torch.empty(lib().cwdm_conv3d_wgrad_workspace_bytes(cout, cin, k), dtype=torch.uint8, device=DEV)
+    d.workspace = wsw.data_ptr()
     check(lib().cwdm_conv3d_wgrad(ctypes.byref(d), None))
     tol = 1e-4 if dtype_name == "fp32" else 1e-2
     assert rel_err(dw, ref) < tol, name
