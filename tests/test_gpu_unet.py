@@ -38,7 +38,8 @@ def test_tiny_unet_forward_and_trace(dtype, tol):
     t = torch.tensor([3, 917])
     trace = []
     ref = ou.unet_forward(P, x, t, num_groups=G, trace=trace, **cfg)
-    out = model(x.to(DEV), t.to(DEV))
+    with torch.no_grad():  # inference path: activations land in the plan's own workspace
+        out = model(x.to(DEV), t.to(DEV))
     assert out.shape == ref.shape
     assert rel_err(out, ref) < tol
     # block-by-block (NDHWC workspace views)
