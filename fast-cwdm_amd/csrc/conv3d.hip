@@ -1,5 +1,7 @@
 // Conv3d host side: weight packing, launch planning (brick, split-K) and the C ABI.
 // Kernels: conv3d_kernels.hpp, instantiated in conv3d_inst_*.hip.
+#include <algorithm>
+
 #include "conv3d_kernels.hpp"
 
 namespace cwdm {
@@ -142,9 +144,17 @@ Plan1 plan_conv(const cwdm_conv3d_desc* d) {
 }
 }  // namespace
 
+namespace cwdm {
+bool v4_eligible(const cwdm_conv3d_desc* d);
+int64_t v4_workspace_bytes(const cwdm_conv3d_desc* d);
+int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s);
+int legacy_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream);
+}  // namespace cwdm
+
 extern "C" int64_t cwdm_conv3d_workspace_bytes(const cwdm_conv3d_desc* d) {
   if (!d || d->B <= 0 || d->D <= 0 || d->H <= 0 || d->W <= 0 || d->cout <= 0) return -1;
-  return plan_conv(d).ws;
+  const int64_t legacy = plan_conv(d).ws;
+  return v4_eligible(d) ? std::max(legacy, v4_workspace_bytes(d)) : legacy;
 }
 
 extern "C" int64_t cwdm_conv3d_parts(int dtype, int64_t D, int64_t H, int64_t W, int cout) {
@@ -173,6 +183,15 @@ extern "C" int cwdm_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stre
   CWDM_REQUIRE(d->res_mode < 0 || d->res, CWDM_E_INVALID, "cwdm_conv3d_forward: residual pointer missing");
   CWDM_REQUIRE(d->out_dtype == CWDM_F32 || d->out_dtype == d->dtype, CWDM_E_INVALID,
                "cwdm_conv3d_forward: output dtype must be fp32 or the compute dtype");
+  if (v4_eligible(d)) {
+    const int64_t need = v4_workspace_bytes(d);
+    if (need == 0 || (d->workspace && d->ws_bytes >= need)) return conv3d_v4_forward(d, (hipStream_t)stream);
+  }
+  return legacy_conv3d_forward(d, stream);
+}
+
+// the brick / split-K kernels of conv3d_kernels.hpp (every shape and mode)
+int cwdm::legacy_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream) {
   const Plan1 pl = plan_conv(d);
   const int nf = pl.nf;
   CWDM_REQUIRE(nf == 2 || d->cout % 32 == 0 || d->cout < 32, CWDM_E_UNSUPPORTED,

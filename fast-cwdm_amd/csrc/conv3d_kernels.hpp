@@ -737,8 +737,11 @@ __device__ __forceinline__ void mfma_acc(f32x16& acc, const u32x4& a, const u32x
 
 template <int G, int NI, typename SG>
 __device__ __forceinline__ void transform_group(SG* sg) {
-  // items of the next chunk assigned to (dz, dx) group G of 9, spread evenly
-  constexpr int j0 = (G * NI) / 9, j1 = ((G + 1) * NI) / 9;
+  // items of the next chunk assigned to (dz, dx) groups 3..8 (the dz = 0, +1
+  // slabs), spread evenly: the loads issued at the top of the chunk get the
+  // whole first slab (~2300 MFMA cycles) to land before the first transform
+  constexpr int GG = G < 3 ? -1 : G - 3;
+  constexpr int j0 = GG < 0 ? 0 : (GG * NI) / 6, j1 = GG < 0 ? 0 : ((GG + 1) * NI) / 6;
   if constexpr (j0 < j1) sg->template transform_item<j0>();
   if constexpr (j0 + 1 < j1) sg->template transform_item<j0 + 1>();
   if constexpr (j0 + 2 < j1) sg->template transform_item<j0 + 2>();

@@ -347,6 +347,10 @@ cwdm_conv3d_desc conv_shape(const cwdm_unet* u, const ConvStep& cs, int64_t B, i
   d.a_c0 = u->tensors[cs.a0].channels;
   d.a_c1 = cs.a1 >= 0 ? u->tensors[cs.a1].channels : 0;
   d.a_mode = cs.amode;
+  // presence flags only: they select the kernel path and size its workspace
+  // (the DMA-staged kernel needs room for the GroupNorm+SiLU'd input and the skip)
+  d.a_w = reinterpret_cast<const void*>(1);
+  if (cs.gn >= 0) d.a_gn = reinterpret_cast<const float*>(1);
   if (cs.ws_p >= 0) {
     d.b_c0 = u->tensors[cs.sb0].channels;
     d.b_c1 = cs.sb1 >= 0 ? u->tensors[cs.sb1].channels : 0;

@@ -187,6 +187,19 @@ int cwdm_gn_finalize(const float* stats0, int64_t parts0, int c0,
 int cwdm_gn_silu_pool(const void* x, int C, const float* gn, int64_t B, int64_t d, int64_t h, int64_t w,
                       int dtype, void* out_h, void* out_x, cwdm_stream_t stream);
 
+/* Conv kernel-path policy for cwdm_conv3d_forward (process-wide): 0 = auto
+ * (DMA-staged kernel on wide grids with >= 512 tiles, brick/split-K kernels
+ * elsewhere), 1 = brick kernels only, 2 = DMA-staged kernel wherever the shape
+ * allows.  Returns the previous policy.  Initial value: env CWDM_CONV_PATH. */
+int cwdm_conv3d_set_path(int path);
+
+/* GroupNorm+SiLU applied once: out[b,v,:] = SiLU(concat(x0, x1)[b,v,:] * scale + shift)
+ * (GroupNorm32 + SiLU of ResBlock.in_layers / out_layers, guided_diffusion/nn.py:17-19,
+ * unet.py:226-262), NDHWC, channels c0 + c1 (multiples of 8).  cwdm_conv3d_forward
+ * runs it internally (into its workspace) before the DMA-staged conv kernel. */
+int cwdm_gn_apply(const void* x0, int c0, const void* x1, int c1, const float* scale_shift, int64_t B,
+                  int64_t voxels, int dtype, void* out, cwdm_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Training kernels (the backward of the forward above, as torch autograd runs
  * it inside TrainLoop.forward_backward, guided_diffusion/train_util.py:396-462,
