@@ -3,6 +3,7 @@
 //     written once into a workspace tensor (the conv then stages raw copies),
 //   * the 1x1 skip segment (ResBlock skip_connection) runs first as a B-only
 //     conv into a workspace tensor that the 3x3x3 conv adds as its residual.
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 
@@ -10,18 +11,22 @@
 
 namespace cwdm {
 
-template __global__ void conv3d_v4_kernel<bf16_t, 0>(V4Params);
-template __global__ void conv3d_v4_kernel<bf16_t, 1>(V4Params);
-template __global__ void conv3d_v4_kernel<float, 0>(V4Params);
-template __global__ void conv3d_v4_kernel<float, 1>(V4Params);
+template __global__ void conv3d_v4_kernel<bf16_t, 0, true>(V4Params);
+template __global__ void conv3d_v4_kernel<bf16_t, 1, true>(V4Params);
+template __global__ void conv3d_v4_kernel<bf16_t, 0, false>(V4Params);
+template __global__ void conv3d_v4_kernel<bf16_t, 1, false>(V4Params);
+template __global__ void conv3d_v4_kernel<float, 0, false>(V4Params);
+template __global__ void conv3d_v4_kernel<float, 1, false>(V4Params);
 
 namespace {
 
 // one thread per (voxel, 8-channel group): out[v][c] = SiLU(x[v][c] * sc[b][c] + sh[b][c])
+// cm: write the chunk-major layout [B][C / CK][V][CK] the DMA-staged conv reads
+// as contiguous halo rows (CK = 16 bf16 / 8 fp32 channels = 32 bytes per voxel)
 template <typename T>
 __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x0, int c0, const T* __restrict__ x1,
                                                       int c1, const float* __restrict__ gn, long long vpb,
-                                                      long long n8, T* __restrict__ out) {
+                                                      long long n8, T* __restrict__ out, int cm) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n8) return;
   const int C = c0 + c1, G8 = C >> 3;
@@ -45,7 +50,8 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x0,
     y[2 * e] = silu(xv[2 * e] * s.x + s.y);
     y[2 * e + 1] = silu(xv[2 * e + 1] * s.z + s.w);
   }
-  T* dst = out + v * C + c;
+  constexpr int CK = 32 / sizeof(T);
+  T* dst = cm ? out + ((b * (C / CK) + c / CK) * vpb + (v - b * vpb)) * CK + (c % CK) : out + v * C + c;
   if constexpr (sizeof(T) == 2) {
     *reinterpret_cast<u32x4*>(dst) = pack<bf16_t>(y);
   } else {
@@ -68,6 +74,8 @@ std::atomic<int> g_conv_path{[] {
   const char* e = std::getenv("CWDM_CONV_PATH");
   return e ? std::atoi(e) : 0;
 }()};
+
+std::atomic<unsigned long long*> g_stamps{nullptr};
 
 bool v4_eligible(const cwdm_conv3d_desc* d) {
   const int path = g_conv_path.load(std::memory_order_relaxed);
@@ -98,17 +106,17 @@ int64_t v4_workspace_bytes(const cwdm_conv3d_desc* d) {
 int legacy_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream);
 
 int gn_apply(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
-             void* out, hipStream_t s) {
+             void* out, hipStream_t s, int cm = 0) {
   const int64_t n8 = B * vpb * ((c0 + c1) / 8);
   const dim3 grid((unsigned)ceil_div(n8, 256));
   if (dtype == CWDM_BF16)
     hipLaunchKernelGGL(gn_apply_kernel<bf16_t>, grid, dim3(256), 0, s, reinterpret_cast<const bf16_t*>(x0), c0,
                        reinterpret_cast<const bf16_t*>(x1), c1, gn, (long long)vpb, (long long)n8,
-                       reinterpret_cast<bf16_t*>(out));
+                       reinterpret_cast<bf16_t*>(out), cm);
   else
     hipLaunchKernelGGL(gn_apply_kernel<float>, grid, dim3(256), 0, s, reinterpret_cast<const float*>(x0), c0,
                        reinterpret_cast<const float*>(x1), c1, gn, (long long)vpb, (long long)n8,
-                       reinterpret_cast<float*>(out));
+                       reinterpret_cast<float*>(out), cm);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }
@@ -121,12 +129,14 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   const void* a0 = d->a0;
   const void* a1 = d->a1;
   int c0 = d->a_c0, c1 = d->a_c1;
+  int a0_cm = 0;
   int rc;
   if (d->a_gn) {
     void* act = ws;
     ws += align256(d->B * SV * (c0 + c1) * esz);
-    if ((rc = gn_apply(a0, c0, a1, c1, d->a_gn, d->B, SV, d->dtype, act, s))) return rc;
+    if ((rc = gn_apply(a0, c0, a1, c1, d->a_gn, d->B, SV, d->dtype, act, s, 1))) return rc;
     a0 = act; c0 = c0 + c1; a1 = nullptr; c1 = 0;
+    a0_cm = 1;
   }
   const void* res = d->res;
   int rmode = d->res_mode;
@@ -149,6 +159,8 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   p.a0_bstride = SV * c0 * esz; p.a1_bstride = SV * c1 * esz;
   p.a0_bytes = (unsigned)(SV * c0 * esz); p.a1_bytes = (unsigned)(SV * c1 * esz);
   p.amode = d->a_mode;
+  p.a0_cm = a0_cm;
+  p.a0_cvox = (int)SV;
   p.aw = reinterpret_cast<const unsigned char*>(d->a_w);
   p.bias = d->bias; p.bias_bs = d->bias_bstride;
   p.res = res; p.rmode = rmode;
@@ -157,14 +169,29 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   p.stats = d->stats;
   p.out1 = d->out1; p.out_c0 = d->out_c0;
   p.accumulate = d->accumulate;
+  p.stamps = g_stamps.load(std::memory_order_relaxed);
   const long long nblk = (long long)p.B * p.tx * p.ty * p.tz * p.nct;
-  const dim3 grid((unsigned)nblk);
+  p.nblk = (int)nblk;
+  // persistent: two workgroups per CU (80 KB LDS, <= 256 registers per lane each)
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  const dim3 grid((unsigned)std::min<long long>(nblk, 2LL * ncu));
+  const bool fast = !p.out_f32 && !p.accumulate && !p.out1;
   if (d->dtype == CWDM_BF16) {
-    if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 1>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 0>), grid, dim3(256), 0, s, p);
+    if (fast) {
+      if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 1, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 0, true>), grid, dim3(256), 0, s, p);
+    } else {
+      if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 1, false>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 0, false>), grid, dim3(256), 0, s, p);
+    }
   } else {
-    if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<float, 1>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((conv3d_v4_kernel<float, 0>), grid, dim3(256), 0, s, p);
+    if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<float, 1, false>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv3d_v4_kernel<float, 0, false>), grid, dim3(256), 0, s, p);
   }
   CWDM_LAUNCHED();
   return CWDM_OK;
@@ -186,4 +213,12 @@ extern "C" int cwdm_gn_apply(const void* x0, int c0, const void* x1, int c1, con
 extern "C" int cwdm_conv3d_set_path(int path) {
   CWDM_REQUIRE(path >= 0 && path <= 2, CWDM_E_INVALID, "cwdm_conv3d_set_path: path must be 0, 1 or 2");
   return g_conv_path.exchange(path);
+}
+
+// diagnostics: the DMA-staged conv kernel writes 24 u64 per workgroup (s_memtime
+// at start / after the prologue / after each of the first 16 chunks / at the end,
+// and HW_ID, XCC_ID) into buf (device memory, >= 24 * workgroups); null disables
+extern "C" int cwdm_debug_conv_stamps(void* buf) {
+  g_stamps.store(reinterpret_cast<unsigned long long*>(buf));
+  return CWDM_OK;
 }

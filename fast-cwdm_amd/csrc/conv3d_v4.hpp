@@ -31,6 +31,8 @@
 //     store (or accumulate), per-channel (sum, sum^2) partials for the next
 //     GroupNorm, reduced across lanes with DPP and across waves in LDS.
 #pragma once
+#include <type_traits>
+
 #include "conv3d_kernels.hpp"
 
 namespace cwdm {
@@ -44,6 +46,8 @@ struct V4Params {
   unsigned a0_bytes, a1_bytes;        // per-batch bytes of each source (DMA range check)
   long long a0_bstride, a1_bstride;   // per-batch bytes of each source (batch offset)
   int amode;                          // 0 same grid, 1 nearest x2 upsample (source at half resolution)
+  int a0_cm;                          // source 0 is chunk-major [B][C / CK][V][CK] (cwdm_gn_apply output)
+  int a0_cvox;                        // voxels per batch of source 0 (chunk stride of the chunk-major layout)
   const unsigned char* aw;            // packed weights, NT = 64
   const float* bias; long long bias_bs;
   const void* res; int rmode;         // -1 none, 0 same grid, 1 upsampled
@@ -51,6 +55,8 @@ struct V4Params {
   float* stats;
   void* out1; int out_c0;
   int accumulate;
+  int nblk;  // tiles in total (B * tx * ty * tz * nct); gridDim.x <= nblk
+  unsigned long long* stamps;  // diagnostics: per-workgroup s_memtime stamps (cwdm_debug_conv_stamps), else null
 };
 
 struct V4Cfg {
@@ -59,6 +65,10 @@ struct V4Cfg {
   static constexpr int PIECES = 2 * HVP / 64;                        // 40 DMA pieces per chunk
   static constexpr int HALO_B = 2 * HVP * 16;                        // 40960 per buffer
   static constexpr int SMEM = 2 * HALO_B;                            // double-buffered halo: 80 KB
+  // unused padding slots 1224..1279 of quad plane k & 1 of halo buffer k >> 1
+  // (896 B each; the halo DMA never writes them): statistics scratch of wave k
+  // and, in region 0 at +256, the bias of the next tile
+  static constexpr int pad(int k) { return (k >> 1) * HALO_B + (k & 1) * HVP * 16 + HV * 16; }
 };
 
 template <typename T>
@@ -74,17 +84,30 @@ __device__ __forceinline__ void v4_mfma(f32x16& acc, const u32x4& a, const u32x4
 __device__ __forceinline__ void v4_gload(u32x4& dst, const unsigned char* src) {
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(src) : "memory");
 }
+#ifdef CWDM_CONV_STAMPS  // diagnostics build (tools/conv_stamps.py): per-workgroup s_memtime stamps
+#define V4_STAMP(k)                                                                                   \
+  do {                                                                                                \
+    if (p.stamps && tid == 0) p.stamps[(long long)blockIdx.x * 24 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define V4_STAMP(k) do { } while (0)
+#endif
 #define V4_WAIT_W(n, w) \
   asm volatile("s_waitcnt vmcnt(" #n ")" : "+v"((w)[0]), "+v"((w)[1]), "+v"((w)[2]) :: "memory")
 
-// sum of v over the 32 lanes of each half-wave (lanes 0-31 / 32-63), result in
-// every lane of the half
-__device__ __forceinline__ float halfwave_sum(float v) {
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_t));
+}
+
+// sum of v over the 16 lanes of each DPP row, result in every lane of the row
+__device__ __forceinline__ float row16_sum(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));  // quad_perm 1,0,3,2
   v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));  // quad_perm 2,3,0,1
   v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true)); // row_half_mirror
   v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, true)); // row_mirror
-  v += __shfl_xor(v, 16, 64);
   return v;
 }
 
@@ -97,8 +120,187 @@ __device__ __forceinline__ void v4_read_step(u32x4 (&av)[6], const unsigned char
     av[L] = *reinterpret_cast<const u32x4*>(hb + (((PL + 1 + DZ) * V4Cfg::HY + L) * V4Cfg::HX + (DX + 1)) * 16);
 }
 
-template <typename T, int MODE>
+// Epilogue of one output tile from the accumulator registers: + residual,
+// store (or accumulate), per-channel (sum, sum^2) partials for the next
+// GroupNorm.  R: 4 x 256 B of LDS (one slice per wave) for the cross-wave
+// statistics; every wave of the workgroup calls this.
+template <typename T, bool FAST>
+__device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][4], int b, int sl, int ct, int x0,
+                                            int y0, int z0, int tid, int wv, unsigned char* smem) {
+  const int lane = tid & 63, lr = lane & 31, hh = lane >> 5, f = wv & 1, vg = wv >> 1;
+  const int cbase = ct * 64 + f * 32 + 4 * hh;
+  float ssum[16], ssq[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { ssum[i] = 0.f; ssq[i] = 0.f; }
+  const int ox = x0 + lr;
+  const long long HW = (long long)p.H * p.W;
+  // voxel of (plane pl, line m) = vox0 + pl * HW + m * W
+  const long long vox0 = (((long long)b * p.D + z0 + 2 * vg) * p.H + y0) * p.W + ox;
+  if constexpr (FAST) {
+    // bf16 fast path: 16-byte residual loads and stores.  A lane pair (l, l+32)
+    // holds channels 8j..8j+7 of one voxel split 4 / 4; v_permlane32_swap turns
+    // two such groups (j, j+1) into 8 consecutive channels per lane.
+    const bf16_t* res0 = nullptr;
+    long long rHW = 0, rW = 0;
+    if (p.rmode == 0) {
+      res0 = reinterpret_cast<const bf16_t*>(p.res) + vox0 * p.cout + ct * 64 + f * 32 + 8 * hh;
+      rHW = HW * p.cout; rW = (long long)p.W * p.cout;
+    }
+    bf16_t* out0 = reinterpret_cast<bf16_t*>(p.out) + vox0 * p.cout + ct * 64 + f * 32 + 8 * hh;
+    const long long oHW = HW * p.cout, oW = (long long)p.W * p.cout;
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) {
+      u32x4 rq[4][2];  // this plane's residual rows, all loads in flight at once
+      if (p.rmode >= 0) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const bf16_t* r;
+          if (p.rmode == 0) {
+            r = res0 + pl * rHW + m * rW;
+          } else {
+            const int oy = y0 + m, oz = z0 + 2 * vg + pl;
+            const long long rvox =
+                (((long long)b * (p.D >> 1) + (oz >> 1)) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1);
+            r = reinterpret_cast<const bf16_t*>(p.res) + rvox * p.cout + ct * 64 + f * 32 + 8 * hh;
+          }
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) rq[m][jj] = *reinterpret_cast<const u32x4*>(r + 16 * jj);
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        bf16_t* o = out0 + pl * oHW + m * oW;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          float v[8];  // groups j = 2 jj (v[0..3]) and 2 jj + 1 (v[4..7]) in accumulator layout
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = acc[pl][m][8 * jj + k];
+          if (p.rmode >= 0) {
+            const u32x4 q = rq[m][jj];
+            const auto s0 = __builtin_amdgcn_permlane32_swap(q[0], q[2], false, false);
+            const auto s1 = __builtin_amdgcn_permlane32_swap(q[1], q[3], false, false);
+            const unsigned g0 = s0[0], g1 = s1[0], h0 = s0[1], h1 = s1[1];
+            v[0] += __uint_as_float(g0 << 16); v[1] += __uint_as_float(g0 & 0xffff0000u);
+            v[2] += __uint_as_float(g1 << 16); v[3] += __uint_as_float(g1 & 0xffff0000u);
+            v[4] += __uint_as_float(h0 << 16); v[5] += __uint_as_float(h0 & 0xffff0000u);
+            v[6] += __uint_as_float(h1 << 16); v[7] += __uint_as_float(h1 & 0xffff0000u);
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            ssum[8 * jj + k] += v[k];
+            ssq[8 * jj + k] += v[k] * v[k];
+          }
+          const unsigned p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
+          const unsigned p2 = pack_bf16x2(v[4], v[5]), p3 = pack_bf16x2(v[6], v[7]);
+          const auto t0 = __builtin_amdgcn_permlane32_swap(p0, p2, false, false);
+          const auto t1 = __builtin_amdgcn_permlane32_swap(p1, p3, false, false);
+          u32x4 w;
+          w[0] = t0[0]; w[1] = t1[0]; w[2] = t0[1]; w[3] = t1[1];
+          *reinterpret_cast<u32x4*>(o + 16 * jj) = w;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int oy = y0 + m, oz = z0 + 2 * vg + pl;
+        const long long vox = vox0 + pl * HW + (long long)m * p.W;
+        long long rvox = vox;
+        if (p.rmode == 1)
+          rvox = (((long long)b * (p.D >> 1) + (oz >> 1)) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int co = cbase + 8 * j;
+          float v[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = acc[pl][m][4 * j + k];
+          if (p.rmode >= 0) {
+            const T* r = reinterpret_cast<const T*>(p.res) + rvox * p.cout + co;
+            if constexpr (sizeof(T) == 2) {
+              const uint2 rq = *reinterpret_cast<const uint2*>(r);
+              v[0] += __uint_as_float(rq.x << 16); v[1] += __uint_as_float(rq.x & 0xffff0000u);
+              v[2] += __uint_as_float(rq.y << 16); v[3] += __uint_as_float(rq.y & 0xffff0000u);
+            } else {
+              const float4 rq = *reinterpret_cast<const float4*>(r);
+              v[0] += rq.x; v[1] += rq.y; v[2] += rq.z; v[3] += rq.w;
+            }
+          }
+          void* obase = p.out;
+          int ostride = p.cout, oc = co;
+          if (p.out1) {
+            if (co >= p.out_c0) { obase = p.out1; ostride = p.cout - p.out_c0; oc = co - p.out_c0; }
+            else ostride = p.out_c0;
+          }
+          if (p.out_f32 || sizeof(T) == 4) {
+            float* o = reinterpret_cast<float*>(obase) + vox * ostride + oc;
+            if (p.accumulate) {
+              const float4 oq = *reinterpret_cast<const float4*>(o);
+              v[0] += oq.x; v[1] += oq.y; v[2] += oq.z; v[3] += oq.w;
+            }
+            *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+            bf16_t* o = reinterpret_cast<bf16_t*>(obase) + vox * ostride + oc;
+            if (p.accumulate) {
+              const uint2 oq = *reinterpret_cast<const uint2*>(o);
+              v[0] += __uint_as_float(oq.x << 16); v[1] += __uint_as_float(oq.x & 0xffff0000u);
+              v[2] += __uint_as_float(oq.y << 16); v[3] += __uint_as_float(oq.y & 0xffff0000u);
+            }
+            uint2 sq;
+            sq.x = pack_bf16x2(v[0], v[1]);
+            sq.y = pack_bf16x2(v[2], v[3]);
+            *reinterpret_cast<uint2*>(o) = sq;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            ssum[4 * j + k] += v[k];
+            ssq[4 * j + k] += v[k] * v[k];
+          }
+        }
+      }
+    }
+  }
+  if (p.stats) {
+    // the 16 lanes of a row hold the same 16 channels for 16 voxels: reduce
+    // within rows by DPP, the two rows of a half-wave by a swap, then across
+    // the two voxel-group waves in LDS
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      ssum[i] = row16_sum(ssum[i]);
+      ssq[i] = row16_sum(ssq[i]);
+      ssum[i] += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, ssum[i]), 0x401F));
+      ssq[i] += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, ssq[i]), 0x401F));
+    }
+    float* R = reinterpret_cast<float*>(smem + V4Cfg::pad(wv));  // this wave's [hh][16 sums | 16 squares]
+    if (lr == 0) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        R[hh * 32 + i] = ssum[i];
+        R[hh * 32 + 16 + i] = ssq[i];
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const int ff = tid >> 5, c32 = tid & 31, j = c32 >> 3, h2 = (c32 >> 2) & 1, k = c32 & 3;
+      const int i = 4 * j + k;
+      const float* R0 = reinterpret_cast<const float*>(smem + V4Cfg::pad(ff)) + h2 * 32;       // vg 0
+      const float* R1 = reinterpret_cast<const float*>(smem + V4Cfg::pad(ff + 2)) + h2 * 32;   // vg 1
+      const int tiles = p.tx * p.ty * p.tz;
+      const int c = ct * 64 + tid;
+      const long long pidx = ((long long)b * tiles + sl) * p.cout + c;
+      p.stats[pidx * 2 + 0] = R0[i] + R1[i];
+      p.stats[pidx * 2 + 1] = R0[16 + i] + R1[16 + i];
+    }
+  }
+}
+
+// Persistent: gridDim.x <= the number of tiles; workgroup k runs tiles
+// k, k + gridDim.x, ... as one continuous chunk stream, so the next tile's halo,
+// weights and bias are prefetched under the current tile's last chunk.
+template <typename T, int MODE, bool FAST>
 __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
+  static_assert(!FAST || sizeof(T) == 2, "the fast epilogue is bf16 only");
   using C = V4Cfg;
   constexpr int CK = ConvTr<T>::CK;
   constexpr int ESZ = sizeof(T);
@@ -107,230 +309,198 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, hh = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int f = wv & 1, vg = wv >> 1;
-
-  // XCD-aware, bijective block -> (spatial tile, channel tile) map: each XCD
-  // gets a contiguous run of tiles (x fastest), so halo neighbours share its L2
-  const int nblk = gridDim.x;
-  const int bid = blockIdx.x, xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int ct = wg % p.nct;
-  const int st = wg / p.nct;
-  const int tiles = p.tx * p.ty * p.tz;
-  const int b = st / tiles;
-  const int sl = st - b * tiles;
-  const int x0 = (sl % p.tx) * 32, y0 = ((sl / p.tx) % p.ty) * 4, z0 = (sl / (p.tx * p.ty)) * 4;
-
-  // ---- per-lane source voxel of this wave's 10 halo pieces (chunk-invariant)
-  const int SH = MODE == 1 ? p.H >> 1 : p.H, SW = MODE == 1 ? p.W >> 1 : p.W;
-  int svox[10];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) {
-    const int pc = wv + 4 * j;                 // piece id (wave-uniform)
-    const int hv = (pc % 20) * 64 + lane;      // slot in the quad plane
-    int sv = -1;
-    if (hv < C::HV) {
-      const int hx = hv % C::HX, hy = (hv / C::HX) % C::HY, hz = hv / (C::HX * C::HY);
-      int ox = x0 + hx - 1, oy = y0 + hy - 1, oz = z0 + hz - 1;
-      if (ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) {
-        if (MODE == 1) { ox >>= 1; oy >>= 1; oz >>= 1; }
-        sv = (oz * SH + oy) * SW + ox;
-      }
-    }
-    svox[j] = sv;
+  V4_STAMP(0);
+#ifdef CWDM_CONV_STAMPS
+  if (p.stamps && tid == 0) {
+    p.stamps[(long long)blockIdx.x * 24 + 22] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+    p.stamps[(long long)blockIdx.x * 24 + 23] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // XCC_ID
   }
-  const unsigned char* a0b = reinterpret_cast<const unsigned char*>(p.a0) + (long long)b * p.a0_bstride;
-  const unsigned char* a1b = p.a1 ? reinterpret_cast<const unsigned char*>(p.a1) + (long long)b * p.a1_bstride : a0b;
-  const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void*)a0b, (short)0, (int)p.a0_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a1b, (short)0, (int)p.a1_bytes, 0x00020000);
+#endif
 
-  // issue the 10 halo pieces of chunk c into halo buffer c & 1
-  auto issue_halo = [&](int c) {
+  const int nblk = p.nblk;
+  const int tiles = p.tx * p.ty * p.tz;
+  const int SH = MODE == 1 ? p.H >> 1 : p.H, SW = MODE == 1 ? p.W >> 1 : p.W;
+  // tile it of this workgroup -> (b, spatial tile sl, channel tile ct, origin) through the
+  // XCD-aware bijective map: the tiles an XCD runs are one contiguous run (x fastest)
+  struct Tile { int b, sl, ct, x0, y0, z0; };
+  auto tile_of = [&](int it) {
+    const int t = blockIdx.x + it * gridDim.x;
+    const int xcd = t & 7, q8 = nblk >> 3, r8 = nblk & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (t >> 3);
+    Tile r;
+    r.ct = wg % p.nct;
+    const int st = wg / p.nct;
+    r.b = st / tiles;
+    r.sl = st - r.b * tiles;
+    r.x0 = (r.sl % p.tx) * 32; r.y0 = ((r.sl / p.tx) % p.ty) * 4; r.z0 = (r.sl / (p.tx * p.ty)) * 4;
+    // wave-uniform by construction; say so, or every buffer op gets a waterfall loop
+    r.ct = __builtin_amdgcn_readfirstlane(r.ct); r.b = __builtin_amdgcn_readfirstlane(r.b);
+    r.sl = __builtin_amdgcn_readfirstlane(r.sl); r.x0 = __builtin_amdgcn_readfirstlane(r.x0);
+    r.y0 = __builtin_amdgcn_readfirstlane(r.y0); r.z0 = __builtin_amdgcn_readfirstlane(r.z0);
+    return r;
+  };
+  const int ntile = (nblk - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+
+  // per-lane source voxel of this wave's halo pieces for one tile.  Pieces
+  // wv + 4 j and wv + 4 (j + 5) cover the same voxel slots of the two quad
+  // planes, so 5 voxel indices serve all 10 pieces; -2 marks the padding slots
+  // (never written: they hold the bias / statistics scratch)
+  int svox[5];
+  auto compute_svox = [&](const Tile& tt) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int hv = (wv + 4 * j) * 64 + lane;
+      int sv = -2;
+      if (hv < C::HV) {
+        sv = -1;
+        const int hx = hv % C::HX, hy = (hv / C::HX) % C::HY, hz = hv / (C::HX * C::HY);
+        int ox = tt.x0 + hx - 1, oy = tt.y0 + hy - 1, oz = tt.z0 + hz - 1;
+        if (ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) {
+          if (MODE == 1) { ox >>= 1; oy >>= 1; oz >>= 1; }
+          sv = (oz * SH + oy) * SW + ox;
+        }
+      }
+      svox[j] = sv;
+    }
+  };
+  // halo pieces of chunk c of tile tt into halo buffer hbuf
+  auto issue_halo = [&](const Tile& tt, int c, int hbuf) {
     const bool s0 = c < p.nch0;
+    const unsigned char* base = s0 ? reinterpret_cast<const unsigned char*>(p.a0) + (long long)tt.b * p.a0_bstride
+                                   : reinterpret_cast<const unsigned char*>(p.a1) + (long long)tt.b * p.a1_bstride;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(s0 ? p.a0_bytes : p.a1_bytes), 0x00020000);
     const int cs = s0 ? p.ac0 : p.ac1;
     const int cb = (s0 ? c : c - p.nch0) * CK;
-    const unsigned rowb = (unsigned)cs * ESZ;
-    unsigned char* hb = smem + (c & 1) * C::HALO_B;
+    // byte offset of (voxel sv, quad qd) = sv * rowb + cofs + 16 qd
+    const bool cm = s0 && p.a0_cm;
+    const unsigned rowb = cm ? 32u : (unsigned)cs * ESZ;
+    const unsigned cofs = cm ? (unsigned)c * (unsigned)p.a0_cvox * 32u : (unsigned)(cb * ESZ);
+    unsigned char* hb = smem + hbuf * C::HALO_B;
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
       const int pc = wv + 4 * j;
-      const int qd = pc / 20;
-      const unsigned voff = svox[j] >= 0 ? (unsigned)svox[j] * rowb + (unsigned)(cb * ESZ + qd * 16) : 0xFFFFFFF0u;
-      unsigned char* dst = hb + pc * 1024;
-      if (s0)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs0, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
+      const int sv = svox[j % 5];
+      const unsigned voff = sv >= 0 ? (unsigned)sv * rowb + cofs + (unsigned)((j / 5) * 16) : 0xFFFFFFF0u;
+      if (sv != -2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(hb + pc * 1024), 16,
+                                                 voff, 0, 0, 0);
     }
   };
-  // weight fragments of group G (chunk G / 9, (dz, dx) = G % 9): the 3 dy taps,
-  // this lane's row (output channel) lr of the wave's 32-channel slice, quad hh
-  const int total = 9 * p.nch;
-  const unsigned char* wlane =
-      p.aw + (long long)ct * p.nch * 27 * 2048 + f * 1024 + lr * 32 + ((hh ^ ((lr >> 3) & 1)) << 4);
-  auto load_w = [&](u32x4 (&w)[3], int G) {
-    G = G < total ? G : total - 1;  // past the end: harmless reload keeps the wait counts uniform
-    const int c = G / 9, g = G - 9 * c;
-    const unsigned char* src = wlane + ((long long)c * 27 + (g / 3) * 9 + (g % 3)) * 2048;
+  // weight fragments of group g of chunk c, channel tile ct: the 3 dy taps, this
+  // lane's row (output channel) lr of the wave's 32-channel slice, quad hh
+  const unsigned char* wlane = p.aw + f * 1024 + lr * 32 + ((hh ^ ((lr >> 3) & 1)) << 4);
+  auto load_w = [&](u32x4 (&w)[3], int ct, int c, int g) {
+    const unsigned char* src = wlane + (((long long)ct * p.nch + c) * 27 + (g / 3) * 9 + (g % 3)) * 2048;
     v4_gload(w[0], src);
     v4_gload(w[1], src + 3 * 2048);
     v4_gload(w[2], src + 6 * 2048);
   };
-
+  // the 64 bias values of a tile into this wave's LDS padding slice (one 4-byte DMA per lane)
+  auto issue_bias = [&](const Tile& tt) {
+    if (p.bias && wv == 0)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(
+                                           p.bias + (long long)tt.b * p.bias_bs + tt.ct * 64 + lane),
+                                       (__attribute__((address_space(3))) void*)(smem + C::pad(0) + 256), 4, 0, 0);
+  };
+  // accumulators start at the bias of their output channel (i = 4 j + k -> channel 8 j + 4 hh + k)
   f32x16 acc[2][4];
+  auto init_acc = [&]() {
+    float bia[16];
+    const float* bl = reinterpret_cast<const float*>(smem + C::pad(0) + 256) + f * 32 + 4 * hh;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int i = 0; i < 16; ++i) bia[i] = p.bias ? bl[8 * (i >> 2) + (i & 3)] : 0.f;
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[a][m][i] = 0.f;
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[a][m][i] = bia[i];
+  };
 
   // lane read base: halo voxel (z = 2 vg, line 0, x = lr) of quad plane hh
   const int hlane = hh * (C::HVP * 16) + ((2 * vg) * (C::HX * C::HY) + lr) * 16;
 
+  Tile cur = tile_of(0);
   u32x4 wr[3][3];
-  load_w(wr[0], 0);
-  load_w(wr[1], 1);
-  issue_halo(0);
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2]), "+v"(wr[1][0]),
-               "+v"(wr[1][1]), "+v"(wr[1][2])::"memory");
-  __builtin_amdgcn_s_barrier();
-  for (int c = 0; c < p.nch; ++c) {
-    const unsigned char* hb = smem + (c & 1) * C::HALO_B + hlane;
-    // 18 steps per chunk: step K = (group K / 2, plane K % 2).  The 6 halo
-    // lines of step K + 1 are read before the 12 MFMAs of step K (software
-    // pipeline, pinned by sched_barrier), so every MFMA block finds its
-    // operands already in registers.
-    u32x4 av[2][6];
-    v4_read_step<0>(av[0], hb);
-#define V4_STEP(K)                                                                                            \
-    {                                                                                                         \
-      constexpr int GI = (K) / 2, PL = (K) % 2;                                                               \
-      if (PL == 0) {                                                                                          \
-        if (GI == 0 && c + 1 < p.nch) issue_halo(c + 1);                                                      \
-        load_w(wr[(GI + 2) % 3], 9 * c + GI + 2);                                                             \
-      }                                                                                                       \
-      if ((K) < 17) v4_read_step<((K) + 1) % 18>(av[((K) + 1) & 1], hb);                                      \
-      if (PL == 0 && GI >= 2) V4_WAIT_W(6, wr[GI % 3]);                                                       \
-      __builtin_amdgcn_sched_barrier(0);                                                                      \
-      _Pragma("unroll") for (int dy = 0; dy < 3; ++dy)                                                        \
-      _Pragma("unroll") for (int m = 0; m < 4; ++m)                                                           \
-        v4_mfma<T>(acc[PL][m], wr[GI % 3][dy], av[(K) & 1][m + dy]);                                          \
-      __builtin_amdgcn_sched_barrier(0);                                                                      \
-    }
-    V4_STEP(0) V4_STEP(1) V4_STEP(2) V4_STEP(3) V4_STEP(4) V4_STEP(5)
-    V4_STEP(6) V4_STEP(7) V4_STEP(8) V4_STEP(9) V4_STEP(10) V4_STEP(11)
-    V4_STEP(12) V4_STEP(13) V4_STEP(14) V4_STEP(15) V4_STEP(16) V4_STEP(17)
-#undef V4_STEP
-    // next chunk: its halo (issued at group 0) and its first two weight groups
-    // (issued at groups 7, 8) must have landed; then every wave is past this
-    // chunk's reads of the buffer the following chunk's halo will overwrite
+  compute_svox(cur);
+  issue_bias(cur);
+  issue_halo(cur, 0, 0);
+  int gch = 0;  // chunk counter of the stream (selects the halo buffer)
+  for (int it = 0; it < ntile; ++it) {
+    const bool more = it + 1 < ntile;
+    // the tile's halo and bias were issued under the previous tile (or above)
+    load_w(wr[0], cur.ct, 0, 0);
+    load_w(wr[1], cur.ct, 0, 1);
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2]), "+v"(wr[1][0]),
                  "+v"(wr[1][1]), "+v"(wr[1][2])::"memory");
     __builtin_amdgcn_s_barrier();
-  }
-
-  // ---------------- epilogue (from registers) ----------------
-  const int cbase = ct * 64 + f * 32 + 4 * hh;   // + 8 j + k
-  float bia[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int co = cbase + 8 * (i >> 2) + (i & 3);
-    bia[i] = p.bias ? p.bias[(long long)b * p.bias_bs + co] : 0.f;
-  }
-  float ssum[16], ssq[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { ssum[i] = 0.f; ssq[i] = 0.f; }
-  const int ox = x0 + lr;
-#pragma unroll
-  for (int pl = 0; pl < 2; ++pl) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int oy = y0 + m, oz = z0 + 2 * vg + pl;
-      const long long vox = (((long long)b * p.D + oz) * p.H + oy) * p.W + ox;
-      long long rvox = vox;
-      if (p.rmode == 1)
-        rvox = (((long long)b * (p.D >> 1) + (oz >> 1)) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int co = cbase + 8 * j;
-        float v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = acc[pl][m][4 * j + k] + bia[4 * j + k];
-        if (p.rmode >= 0) {
-          const T* r = reinterpret_cast<const T*>(p.res) + rvox * p.cout + co;
-          if constexpr (sizeof(T) == 2) {
-            const uint2 rq = *reinterpret_cast<const uint2*>(r);
-            v[0] += __uint_as_float(rq.x << 16); v[1] += __uint_as_float(rq.x & 0xffff0000u);
-            v[2] += __uint_as_float(rq.y << 16); v[3] += __uint_as_float(rq.y & 0xffff0000u);
-          } else {
-            const float4 rq = *reinterpret_cast<const float4*>(r);
-            v[0] += rq.x; v[1] += rq.y; v[2] += rq.z; v[3] += rq.w;
-          }
-        }
-        void* obase = p.out;
-        int ostride = p.cout, oc = co;
-        if (p.out1) {
-          if (co >= p.out_c0) { obase = p.out1; ostride = p.cout - p.out_c0; oc = co - p.out_c0; }
-          else ostride = p.out_c0;
-        }
-        if (p.out_f32) {
-          float* o = reinterpret_cast<float*>(obase) + vox * ostride + oc;
-          if (p.accumulate) {
-            const float4 oq = *reinterpret_cast<const float4*>(o);
-            v[0] += oq.x; v[1] += oq.y; v[2] += oq.z; v[3] += oq.w;
-          }
-          *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-        } else if constexpr (sizeof(T) == 2) {
-          bf16_t* o = reinterpret_cast<bf16_t*>(obase) + vox * ostride + oc;
-          if (p.accumulate) {
-            const uint2 oq = *reinterpret_cast<const uint2*>(o);
-            v[0] += __uint_as_float(oq.x << 16); v[1] += __uint_as_float(oq.x & 0xffff0000u);
-            v[2] += __uint_as_float(oq.y << 16); v[3] += __uint_as_float(oq.y & 0xffff0000u);
-          }
-          uint2 sq;
-          sq.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-          sq.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-          *reinterpret_cast<uint2*>(o) = sq;
-        } else {
-          float* o = reinterpret_cast<float*>(obase) + vox * ostride + oc;
-          if (p.accumulate) {
-            const float4 oq = *reinterpret_cast<const float4*>(o);
-            v[0] += oq.x; v[1] += oq.y; v[2] += oq.z; v[3] += oq.w;
-          }
-          *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          ssum[4 * j + k] += v[k];
-          ssq[4 * j + k] += v[k] * v[k];
-        }
+    if (it == 0) V4_STAMP(1);
+    init_acc();
+    // one chunk: 18 steps, step K = (group K / 2, plane K % 2).  The 6 halo
+    // lines of step K + 1 are read before the 12 MFMAs of step K (software
+    // pipeline, pinned by sched_barrier), so every MFMA block finds its
+    // operands already in registers.  LAST: the tile's last chunk, which
+    // prefetches the next tile's chunk 0 (halo, bias) instead of chunk c + 1.
+    auto chunk = [&](auto lastc, int c) {
+      constexpr bool LAST = decltype(lastc)::value;
+      const unsigned char* hb = smem + (gch & 1) * C::HALO_B + hlane;
+      const bool has_next = !LAST || more;
+      u32x4 av[2][6];
+      v4_read_step<0>(av[0], hb);
+#define V4_STEP(K)                                                                                            \
+      {                                                                                                       \
+        constexpr int GI = (K) / 2, PL = (K) % 2;                                                             \
+        if (PL == 0) {                                                                                        \
+          /* weights of group GI + 2: this chunk or the next; past the tile's last group a */                 \
+          /* harmless reload keeps the wait counts uniform */                                                 \
+          if (GI + 2 < 9) load_w(wr[(GI + 2) % 3], cur.ct, c, GI + 2);                                        \
+          else if (!LAST) load_w(wr[(GI + 2) % 3], cur.ct, c + 1, GI + 2 - 9);                                \
+          else load_w(wr[(GI + 2) % 3], cur.ct, c, 8);                                                        \
+          if (GI == 0 && has_next) {                                                                          \
+            if (LAST) {                                                                                       \
+              const Tile nxt = tile_of(it + 1);                                                               \
+              compute_svox(nxt);                                                                              \
+              issue_bias(nxt);                                                                                \
+              issue_halo(nxt, 0, (gch + 1) & 1);                                                              \
+            } else {                                                                                          \
+              issue_halo(cur, c + 1, (gch + 1) & 1);                                                          \
+            }                                                                                                 \
+          }                                                                                                   \
+        }                                                                                                     \
+        if ((K) < 17) v4_read_step<((K) + 1) % 18>(av[((K) + 1) & 1], hb);                                    \
+        /* W(G) is retired with the 2 younger weight groups (and at group 2 the */                            \
+        /* next chunk's halo pieces) still in flight */                                                       \
+        if (PL == 0 && GI == 2) { if (has_next) V4_WAIT_W(16, wr[2]); else V4_WAIT_W(6, wr[2]); }             \
+        if (PL == 0 && GI >= 3) V4_WAIT_W(6, wr[GI % 3]);                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                                    \
+        _Pragma("unroll") for (int dy = 0; dy < 3; ++dy)                                                      \
+        _Pragma("unroll") for (int m = 0; m < 4; ++m)                                                         \
+          v4_mfma<T>(acc[PL][m], wr[GI % 3][dy], av[(K) & 1][m + dy]);                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                                    \
       }
-    }
+      V4_STEP(0) V4_STEP(1) V4_STEP(2) V4_STEP(3) V4_STEP(4) V4_STEP(5)
+      V4_STEP(6) V4_STEP(7) V4_STEP(8) V4_STEP(9) V4_STEP(10) V4_STEP(11)
+      V4_STEP(12) V4_STEP(13) V4_STEP(14) V4_STEP(15) V4_STEP(16) V4_STEP(17)
+#undef V4_STEP
+      // the next chunk's halo (and, at a tile end, the next tile's bias) and its
+      // first two weight groups (issued at groups 7, 8) must have landed; then
+      // every wave is past this chunk's reads of the buffer the following
+      // chunk's halo will overwrite
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2]), "+v"(wr[1][0]),
+                   "+v"(wr[1][1]), "+v"(wr[1][2])::"memory");
+      __builtin_amdgcn_s_barrier();
+      if (it == 0 && c < 8) V4_STAMP(4 + c);
+      ++gch;
+    };
+    for (int c = 0; c + 1 < p.nch; ++c) chunk(std::false_type{}, c);
+    chunk(std::true_type{}, p.nch - 1);
+    if (it == 0) V4_STAMP(12);
+    v4_epilogue<T, FAST>(p, acc, cur.b, cur.sl, cur.ct, cur.x0, cur.y0, cur.z0, tid, wv, smem);
+    if (it == 0) V4_STAMP(13);
+    if (more) cur = tile_of(it + 1);
   }
-  if (p.stats) {
-    // lanes of a half-wave hold the same 16 channels for 32 different voxels
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      ssum[i] = halfwave_sum(ssum[i]);
-      ssq[i] = halfwave_sum(ssq[i]);
-    }
-    float* R = reinterpret_cast<float*>(smem);  // [vg][64 ch][2]
-    if (lr == 0) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int cl = f * 32 + 4 * hh + 8 * (i >> 2) + (i & 3);
-        R[(vg * 64 + cl) * 2 + 0] = ssum[i];
-        R[(vg * 64 + cl) * 2 + 1] = ssq[i];
-      }
-    }
-    __syncthreads();
-    if (tid < 64) {
-      const int c = ct * 64 + tid;
-      const long long pidx = ((long long)b * tiles + sl) * p.cout + c;
-      p.stats[pidx * 2 + 0] = R[tid * 2 + 0] + R[(64 + tid) * 2 + 0];
-      p.stats[pidx * 2 + 1] = R[tid * 2 + 1] + R[(64 + tid) * 2 + 1];
-    }
-  }
+  V4_STAMP(15);
 }
 
 }  // namespace cwdm

@@ -193,6 +193,12 @@ int cwdm_gn_silu_pool(const void* x, int C, const float* gn, int64_t B, int64_t 
  * allows.  Returns the previous policy.  Initial value: env CWDM_CONV_PATH. */
 int cwdm_conv3d_set_path(int path);
 
+/* Diagnostics only: per-workgroup timestamps of the DMA-staged conv kernel
+ * (24 x u64 per workgroup: s_memtime at start, after the prologue, after each of
+ * the first 16 chunks, at the end; [22] HW_ID, [23] XCC_ID) into the device
+ * buffer buf; NULL turns it off. */
+int cwdm_debug_conv_stamps(void* buf);
+
 /* GroupNorm+SiLU applied once: out[b,v,:] = SiLU(concat(x0, x1)[b,v,:] * scale + shift)
  * (GroupNorm32 + SiLU of ResBlock.in_layers / out_layers, guided_diffusion/nn.py:17-19,
  * unet.py:226-262), NDHWC, channels c0 + c1 (multiples of 8).  cwdm_conv3d_forward
