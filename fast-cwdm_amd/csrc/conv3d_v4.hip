@@ -180,6 +180,9 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     return n > 0 ? n : 256;
   }();
   const dim3 grid((unsigned)std::min<long long>(nblk, 2LL * ncu));
+  // half a tile: ~17k cycles per chunk and ~12k for the epilogue when shared (tools/conv_stamps.py)
+  static const int stagger_env = [] { const char* e = std::getenv("CWDM_CONV_STAGGER"); return e ? std::atoi(e) : -1; }();
+  p.stagger_cycles = nblk > 2LL * ncu ? (stagger_env >= 0 ? stagger_env : (p.nch * 17000 + 12000) / 2) : 0;
   const bool fast = !p.out_f32 && !p.accumulate && !p.out1;
   if (d->dtype == CWDM_BF16) {
     if (fast) {

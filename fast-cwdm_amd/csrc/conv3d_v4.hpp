@@ -20,8 +20,8 @@
 //   * K loop: chunks of 16 (bf16) / 8 (fp32) input channels; per chunk 9
 //     groups (dz, dx), each = 3 dy taps x 2 planes x 4 lines = 24 MFMAs that
 //     reuse 6 input lines per plane.  Weights: every lane loads its own A
-//     fragments (16 B of one output channel) straight into VGPRs, two groups
-//     ahead, through a 3-deep register ring with counted vmcnt waits.
+//     fragments (16 B of one output channel) straight into VGPRs, one group
+//     ahead, through a 3-slot register ring with counted vmcnt waits.
 //   * The halo is double-buffered (the next chunk's DMA is issued at the top
 //     of the current chunk): one raw s_barrier per chunk, no exposed DMA
 //     latency.  Two workgroups share a CU (80 KB LDS each, <= 256 registers
@@ -55,9 +55,12 @@ struct V4Params {
   float* stats;
   void* out1; int out_c0;
   int accumulate;
+  int stagger_cycles;  // delay of the second workgroup on each CU (0: off)
   int nblk;  // tiles in total (B * tx * ty * tz * nct); gridDim.x <= nblk
   unsigned long long* stamps;  // diagnostics: per-workgroup s_memtime stamps (cwdm_debug_conv_stamps), else null
 };
+
+__device__ unsigned g_v4_cu_arrivals[8 * 256];
 
 struct V4Cfg {
   static constexpr int HX = 34, HY = 6, HZ = 6, HV = HX * HY * HZ;  // 1224 halo voxels
@@ -311,12 +314,32 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   const int f = wv & 1, vg = wv >> 1;
   V4_STAMP(0);
 #ifdef CWDM_CONV_STAMPS
+  if (p.stamps && tid == 0) p.stamps[(long long)blockIdx.x * 24 + 20] = __builtin_amdgcn_s_memrealtime();
   if (p.stamps && tid == 0) {
     p.stamps[(long long)blockIdx.x * 24 + 22] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
     p.stamps[(long long)blockIdx.x * 24 + 23] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // XCC_ID
   }
 #endif
 
+  // The two workgroups that share a CU would run in lockstep and hit their
+  // epilogues (VALU + stores, no MFMA) together.  The second one to arrive on
+  // a CU starts half a tile late, so each epilogue runs beside the partner's
+  // MFMAs.  (Arrival order per CU from a monotonic counter: every launch adds
+  // two arrivals per CU, so the parity needs no reset.)
+  if (p.stagger_cycles > 0) {
+    unsigned* slot = reinterpret_cast<unsigned*>(smem + V4Cfg::pad(0) + 512);
+    if (tid == 0) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // XCC_ID
+      *slot = atomicAdd(&g_v4_cu_arrivals[((xcc & 7) << 8) | ((hw >> 8) & 0xFF)], 1u) & 1u;
+    }
+    __syncthreads();
+    if (*slot) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+      while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)p.stagger_cycles) __builtin_amdgcn_s_sleep(32);
+    }
+    __syncthreads();
+  }
   const int nblk = p.nblk;
   const int tiles = p.tx * p.ty * p.tz;
   const int SH = MODE == 1 ? p.H >> 1 : p.H, SW = MODE == 1 ? p.W >> 1 : p.W;
@@ -341,12 +364,13 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   };
   const int ntile = (nblk - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
 
-  // per-lane source voxel of this wave's halo pieces for one tile.  Pieces
-  // wv + 4 j and wv + 4 (j + 5) cover the same voxel slots of the two quad
-  // planes, so 5 voxel indices serve all 10 pieces; -2 marks the padding slots
-  // (never written: they hold the bias / statistics scratch)
-  int svox[5];
-  auto compute_svox = [&](const Tile& tt) {
+  // halo pieces of chunk c of tile tt into halo buffer hbuf
+  // Per-lane source voxel of this wave's pieces: pieces wv + 4 j and wv + 4 (j + 5)
+  // cover the same voxel slots of the two quad planes, so 5 voxel indices serve
+  // all 10; -2 marks the padding slots (never written: bias / statistics scratch).
+  // Recomputed per chunk (a few VALU per piece) rather than held in registers.
+  auto issue_halo = [&](const Tile& tt, int c, int hbuf) {
+    int svox[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       const int hv = (wv + 4 * j) * 64 + lane;
@@ -362,9 +386,6 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
       }
       svox[j] = sv;
     }
-  };
-  // halo pieces of chunk c of tile tt into halo buffer hbuf
-  auto issue_halo = [&](const Tile& tt, int c, int hbuf) {
     const bool s0 = c < p.nch0;
     const unsigned char* base = s0 ? reinterpret_cast<const unsigned char*>(p.a0) + (long long)tt.b * p.a0_bstride
                                    : reinterpret_cast<const unsigned char*>(p.a1) + (long long)tt.b * p.a1_bstride;
@@ -423,7 +444,6 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
 
   Tile cur = tile_of(0);
   u32x4 wr[3][3];
-  compute_svox(cur);
   issue_bias(cur);
   issue_halo(cur, 0, 0);
   int gch = 0;  // chunk counter of the stream (selects the halo buffer)
@@ -431,48 +451,39 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
     const bool more = it + 1 < ntile;
     // the tile's halo and bias were issued under the previous tile (or above)
     load_w(wr[0], cur.ct, 0, 0);
-    load_w(wr[1], cur.ct, 0, 1);
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2]), "+v"(wr[1][0]),
-                 "+v"(wr[1][1]), "+v"(wr[1][2])::"memory");
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2])::"memory");
     __builtin_amdgcn_s_barrier();
     if (it == 0) V4_STAMP(1);
     init_acc();
     // one chunk: 18 steps, step K = (group K / 2, plane K % 2).  The 6 halo
     // lines of step K + 1 are read before the 12 MFMAs of step K (software
     // pipeline, pinned by sched_barrier), so every MFMA block finds its
-    // operands already in registers.  LAST: the tile's last chunk, which
-    // prefetches the next tile's chunk 0 (halo, bias) instead of chunk c + 1.
+    // operands already in registers.  LAST: the tile's last chunk; the next
+    // tile's chunk 0 (halo, bias) is issued after its MFMAs and lands under the
+    // epilogue.
     auto chunk = [&](auto lastc, int c) {
       constexpr bool LAST = decltype(lastc)::value;
       const unsigned char* hb = smem + (gch & 1) * C::HALO_B + hlane;
-      const bool has_next = !LAST || more;
+      constexpr bool has_next = !LAST;
       u32x4 av[2][6];
       v4_read_step<0>(av[0], hb);
 #define V4_STEP(K)                                                                                            \
       {                                                                                                       \
         constexpr int GI = (K) / 2, PL = (K) % 2;                                                             \
         if (PL == 0) {                                                                                        \
-          /* weights of group GI + 2: this chunk or the next; past the tile's last group a */                 \
-          /* harmless reload keeps the wait counts uniform */                                                 \
-          if (GI + 2 < 9) load_w(wr[(GI + 2) % 3], cur.ct, c, GI + 2);                                        \
-          else if (!LAST) load_w(wr[(GI + 2) % 3], cur.ct, c + 1, GI + 2 - 9);                                \
-          else load_w(wr[(GI + 2) % 3], cur.ct, c, 8);                                                        \
-          if (GI == 0 && has_next) {                                                                          \
-            if (LAST) {                                                                                       \
-              const Tile nxt = tile_of(it + 1);                                                               \
-              compute_svox(nxt);                                                                              \
-              issue_bias(nxt);                                                                                \
-              issue_halo(nxt, 0, (gch + 1) & 1);                                                              \
-            } else {                                                                                          \
-              issue_halo(cur, c + 1, (gch + 1) & 1);                                                          \
-            }                                                                                                 \
-          }                                                                                                   \
+          /* weights of group GI + 1: this chunk or the next.  Nothing past the tile's last */                \
+          /* group: a load nobody waits for would land in registers the epilogue reuses */                    \
+          if (GI + 1 < 9) load_w(wr[(GI + 1) % 3], cur.ct, c, GI + 1);                                        \
+          else if (!LAST) load_w(wr[(GI + 1) % 3], cur.ct, c + 1, 0);                                         \
+          if (GI == 1 && has_next) issue_halo(cur, c + 1, (gch + 1) & 1);                                     \
         }                                                                                                     \
         if ((K) < 17) v4_read_step<((K) + 1) % 18>(av[((K) + 1) & 1], hb);                                    \
-        /* W(G) is retired with the 2 younger weight groups (and at group 2 the */                            \
-        /* next chunk's halo pieces) still in flight */                                                       \
-        if (PL == 0 && GI == 2) { if (has_next) V4_WAIT_W(16, wr[2]); else V4_WAIT_W(6, wr[2]); }             \
-        if (PL == 0 && GI >= 3) V4_WAIT_W(6, wr[GI % 3]);                                                     \
+        /* W(G) is retired with the younger weight group (and at group 2 the next */                          \
+        /* chunk's halo pieces) still in flight; W(0) landed before the chunk */                              \
+        if (PL == 0 && GI == 1) { if (has_next) V4_WAIT_W(13, wr[1]); else V4_WAIT_W(3, wr[1]); }             \
+        if (PL == 0 && GI == 2) { if (has_next) V4_WAIT_W(13, wr[2]); else V4_WAIT_W(3, wr[2]); }             \
+        if (PL == 0 && GI >= 3 && (GI < 8 || !LAST)) V4_WAIT_W(3, wr[GI % 3]);                                \
+        if (PL == 0 && GI == 8 && LAST) V4_WAIT_W(0, wr[2]);  /* nothing younger in flight */                 \
         __builtin_amdgcn_sched_barrier(0);                                                                    \
         _Pragma("unroll") for (int dy = 0; dy < 3; ++dy)                                                      \
         _Pragma("unroll") for (int m = 0; m < 4; ++m)                                                         \
@@ -483,13 +494,19 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
       V4_STEP(6) V4_STEP(7) V4_STEP(8) V4_STEP(9) V4_STEP(10) V4_STEP(11)
       V4_STEP(12) V4_STEP(13) V4_STEP(14) V4_STEP(15) V4_STEP(16) V4_STEP(17)
 #undef V4_STEP
-      // the next chunk's halo (and, at a tile end, the next tile's bias) and its
-      // first two weight groups (issued at groups 7, 8) must have landed; then
-      // every wave is past this chunk's reads of the buffer the following
-      // chunk's halo will overwrite
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2]), "+v"(wr[1][0]),
-                   "+v"(wr[1][1]), "+v"(wr[1][2])::"memory");
-      __builtin_amdgcn_s_barrier();
+      if constexpr (!LAST) {
+        // the next chunk's halo and its first weight group (issued at group 8)
+        // must have landed; then every wave is past this chunk's reads of the
+        // buffer the following chunk's halo will overwrite
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2])::"memory");
+        __builtin_amdgcn_s_barrier();
+      } else if (more) {
+        // next tile's chunk 0 into the other buffer (last read by chunk gch - 1,
+        // which every wave finished before the previous barrier)
+        const Tile nxt = tile_of(it + 1);
+        issue_bias(nxt);
+        issue_halo(nxt, 0, (gch + 1) & 1);
+      }
       if (it == 0 && c < 8) V4_STAMP(4 + c);
       ++gch;
     };
@@ -501,6 +518,9 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
     if (more) cur = tile_of(it + 1);
   }
   V4_STAMP(15);
+#ifdef CWDM_CONV_STAMPS
+  if (p.stamps && tid == 0) p.stamps[(long long)blockIdx.x * 24 + 21] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 }  // namespace cwdm

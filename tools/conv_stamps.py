@@ -43,6 +43,8 @@ def main():
     for nm, (a, b) in zip(names, idx):
         v = [r[b] - r[a] for r in st]
         print(f"  {nm:20s} {mean(v):9.0f} {min(v):9d} {max(v):9d}")
+    clk = [(r[15] - r[0]) / max(r[21] - r[20], 1) * 0.1 for r in st]
+    print(f"  shader clock (s_memtime / s_memrealtime): mean {mean(clk):.2f} GHz, min {min(clk):.2f}, max {max(clk):.2f}")
     # co-residency: workgroups on the same (xcc, se/sh/cu)
     cu = collections.defaultdict(list)
     for i, r in enumerate(st):
