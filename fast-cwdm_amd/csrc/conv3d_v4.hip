@@ -121,35 +121,13 @@ int gn_apply(const void* x0, int c0, const void* x1, int c1, const float* gn, in
   return CWDM_OK;
 }
 
-int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
+// launch of the DMA-staged kernel on prepared sources: a0 (c0 channels,
+// chunk-major if a0_cm) and a1 (c1 channels, channels-last), residual res/rmode
+int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
+              const void* res, int rmode, hipStream_t s) {
   const int esz = d->dtype == CWDM_BF16 ? 2 : 4;
   const int ck = d->dtype == CWDM_BF16 ? 16 : 8;
-  unsigned char* ws = reinterpret_cast<unsigned char*>(d->workspace);
   const int64_t SV = src_voxels(d);
-  const void* a0 = d->a0;
-  const void* a1 = d->a1;
-  int c0 = d->a_c0, c1 = d->a_c1;
-  int a0_cm = 0;
-  int rc;
-  if (d->a_gn) {
-    void* act = ws;
-    ws += align256(d->B * SV * (c0 + c1) * esz);
-    if ((rc = gn_apply(a0, c0, a1, c1, d->a_gn, d->B, SV, d->dtype, act, s, 1))) return rc;
-    a0 = act; c0 = c0 + c1; a1 = nullptr; c1 = 0;
-    a0_cm = 1;
-  }
-  const void* res = d->res;
-  int rmode = d->res_mode;
-  if (d->b_w) {
-    void* skip = ws;
-    cwdm_conv3d_desc e = *d;
-    e.a0 = nullptr; e.a1 = nullptr; e.a_c0 = 0; e.a_c1 = 0; e.a_gn = nullptr; e.a_w = nullptr; e.a_mode = 0;
-    e.bias = nullptr; e.bias_bstride = 0; e.stats = nullptr;
-    e.out = skip; e.out_dtype = d->dtype; e.out1 = nullptr; e.out_c0 = 0; e.accumulate = 0;
-    e.workspace = nullptr; e.ws_bytes = 0;
-    if ((rc = legacy_conv3d_forward(&e, (cwdm_stream_t)s))) return rc;
-    res = skip; rmode = 0;
-  }
   V4Params p{};
   p.B = (int)d->B; p.D = (int)d->D; p.H = (int)d->H; p.W = (int)d->W;
   p.tx = p.W / 32; p.ty = p.H / 4; p.tz = p.D / 4;
@@ -196,6 +174,169 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<float, 1, false>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((conv3d_v4_kernel<float, 0, false>), grid, dim3(256), 0, s, p);
   }
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
+  const int esz = d->dtype == CWDM_BF16 ? 2 : 4;
+  unsigned char* ws = reinterpret_cast<unsigned char*>(d->workspace);
+  const int64_t SV = src_voxels(d);
+  const void* a0 = d->a0;
+  const void* a1 = d->a1;
+  int c0 = d->a_c0, c1 = d->a_c1;
+  int a0_cm = 0;
+  int rc;
+  if (d->a_gn) {
+    void* act = ws;
+    ws += align256(d->B * SV * (c0 + c1) * esz);
+    if ((rc = gn_apply(a0, c0, a1, c1, d->a_gn, d->B, SV, d->dtype, act, s, 1))) return rc;
+    a0 = act; c0 = c0 + c1; a1 = nullptr; c1 = 0;
+    a0_cm = 1;
+  }
+  const void* res = d->res;
+  int rmode = d->res_mode;
+  if (d->b_w) {
+    void* skip = ws;
+    cwdm_conv3d_desc e = *d;
+    e.a0 = nullptr; e.a1 = nullptr; e.a_c0 = 0; e.a_c1 = 0; e.a_gn = nullptr; e.a_w = nullptr; e.a_mode = 0;
+    e.bias = nullptr; e.bias_bstride = 0; e.stats = nullptr;
+    e.out = skip; e.out_dtype = d->dtype; e.out1 = nullptr; e.out_c0 = 0; e.accumulate = 0;
+    e.workspace = nullptr; e.ws_bytes = 0;
+    if ((rc = legacy_conv3d_forward(&e, (cwdm_stream_t)s))) return rc;
+    res = skip; rmode = 0;
+  }
+  return v4_launch(d, a0, c0, a1, c1, a0_cm, res, rmode, s);
+}
+
+// ---------------------------------------------------------------------------
+// ResBlock with a 1x1 skip_connection (unet.py:264-271): x is read once for
+// both users.  One pass writes act = SiLU(GN1(x)) (chunk-major, conv1's input)
+// and skip = W_skip . x (channels-last, conv2's residual; its bias is folded
+// into conv2's).  Per block of 128 voxels the workgroup copies the x rows into
+// LDS with coalesced 16-byte loads (rows padded by 16 B: conflict-free column
+// reads); then each wave takes 32 voxels: lane (v, hh) reads quad hh of every
+// 16-channel chunk of voxel v, transforms it for act (stored 1 KB-contiguous per
+// wave instruction) and feeds it raw as the MFMA B operand against W_skip (A
+// operand, the conv packing of a 1x1 kernel, staged once per workgroup) -- the
+// conv kernel's accumulator layout.
+// ---------------------------------------------------------------------------
+struct ApplySkipParams {
+  const void* x0; int c0; const void* x1; int c1;
+  const float* gn;     // [B][C][2] scale / shift
+  long long vpb;       // voxels per batch (% 128 == 0)
+  long long nvox;      // B * vpb
+  int B;
+  void* act;           // chunk-major [B][C / CK][vpb][CK]
+  const unsigned char* ws;  // packed 1x1 weights, NT = 64 rows per channel tile
+  int cout;            // 32 NF
+  void* skip;          // [B][vpb][cout]
+};
+
+template <typename T, int NF>
+__global__ void __launch_bounds__(256) gn_apply_skip_kernel(ApplySkipParams p) {
+  constexpr int CK = ConvTr<T>::CK, EPQ = ConvTr<T>::EPQ, ES = sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int C = p.c0 + p.c1, nk = C / CK;
+  const int wbytes = NF * 32 * C * ES;
+  const int RS = C * ES + 16;                      // padded LDS row of one voxel
+  for (int i = threadIdx.x * 16; i < wbytes; i += 256 * 16)
+    *reinterpret_cast<u32x4*>(lds + i) = *reinterpret_cast<const u32x4*>(p.ws + i);
+  float* gl = reinterpret_cast<float*>(lds + wbytes);
+  for (int i = threadIdx.x; i < p.B * C * 2; i += 256) gl[i] = p.gn[i];
+  unsigned char* xt = lds + wbytes + ((p.B * C * 8 + 15) & ~15);
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, hh = lane >> 5, wv = tid >> 6;
+  const int q0 = p.c0 * ES / 16, q1 = p.c1 * ES / 16;   // 16-byte quads per row of each source
+  const long long nblocks = p.nvox / 128;
+  for (long long blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    const long long v0 = blk * 128;
+    __syncthreads();  // previous block's column reads are done (and W / gn staged, first time)
+    // stage the 128 x rows: consecutive lanes read consecutive 16-byte quads
+    for (int i = tid; i < 128 * q0; i += 256) {
+      const int vl = i / q0, qq = i - vl * q0;
+      *reinterpret_cast<u32x4*>(xt + vl * RS + qq * 16) =
+          *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(p.x0) + ((v0 + vl) * q0 + qq) * 16);
+    }
+    for (int i = tid; i < 128 * q1; i += 256) {
+      const int vl = i / q1, qq = i - vl * q1;
+      *reinterpret_cast<u32x4*>(xt + vl * RS + (q0 + qq) * 16) =
+          *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(p.x1) + ((v0 + vl) * q1 + qq) * 16);
+    }
+    __syncthreads();
+    const int vl = wv * 32 + lr;
+    const long long v = v0 + vl;
+    const int b = (int)(v0 / p.vpb);
+    const long long vb = v - (long long)b * p.vpb;
+    f32x16 acc[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[f][i] = 0.f;
+    for (int k = 0; k < nk; ++k) {
+      const u32x4 q = *reinterpret_cast<const u32x4*>(xt + vl * RS + k * 32 + hh * 16);
+      float xv[EPQ], y[EPQ];
+      unpack<T>(q, xv);
+      const float* gs = gl + ((long long)b * C + k * CK + hh * EPQ) * 2;
+#pragma unroll
+      for (int e = 0; e < EPQ; ++e) y[e] = silu(xv[e] * gs[2 * e] + gs[2 * e + 1]);
+      T* dst = reinterpret_cast<T*>(p.act) + (((long long)b * nk + k) * p.vpb + vb) * CK + hh * EPQ;
+      *reinterpret_cast<u32x4*>(dst) = pack<T>(y);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int n = (f & 1) * 32 + lr;
+        const u32x4 a = *reinterpret_cast<const u32x4*>(
+            lds + (((f >> 1) * nk + k) * 64 + n) * 32 + ((hh ^ ((n >> 3) & 1)) << 4));
+        mfma_acc(acc[f], a, q, (T*)nullptr);
+      }
+    }
+    // skip store: lane (v, hh) holds channels 32 f + 8 j + 4 hh + 0..3 of voxel v
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        T* o = reinterpret_cast<T*>(p.skip) + v * p.cout + f * 32 + 8 * j + 4 * hh;
+        if constexpr (sizeof(T) == 2) {
+          uint2 w;
+          w.x = pack_bf16x2(acc[f][4 * j], acc[f][4 * j + 1]);
+          w.y = pack_bf16x2(acc[f][4 * j + 2], acc[f][4 * j + 3]);
+          *reinterpret_cast<uint2*>(o) = w;
+        } else {
+          *reinterpret_cast<float4*>(o) = make_float4(acc[f][4 * j], acc[f][4 * j + 1], acc[f][4 * j + 2], acc[f][4 * j + 3]);
+        }
+      }
+    }
+  }
+}
+
+int64_t apply_skip_lds_bytes(int dtype, int C, int cout, int64_t B) {
+  const int es = dtype == CWDM_BF16 ? 2 : 4;
+  return (int64_t)cout * C * es + ((B * C * 8 + 15) & ~15) + 128LL * (C * es + 16);
+}
+
+bool apply_skip_ok(int dtype, int C, int cout, int64_t B, int64_t vpb) {
+  const int ck = dtype == CWDM_BF16 ? 16 : 8;
+  return (dtype == CWDM_BF16 || dtype == CWDM_F32) && (cout == 64 || cout == 128) && vpb % 128 == 0 &&
+         C % ck == 0 && apply_skip_lds_bytes(dtype, C, cout, B) <= 160 * 1024;
+}
+
+int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
+                  const void* wskip, int cout, void* act, void* skip, hipStream_t s) {
+  CWDM_REQUIRE(apply_skip_ok(dtype, c0 + c1, cout, B, vpb), CWDM_E_UNSUPPORTED, "gn_apply_skip: unsupported shape");
+  ApplySkipParams p{};
+  p.x0 = x0; p.c0 = c0; p.x1 = x1; p.c1 = c1; p.gn = gn; p.vpb = vpb; p.nvox = B * vpb; p.B = (int)B;
+  p.act = act; p.ws = reinterpret_cast<const unsigned char*>(wskip); p.cout = cout; p.skip = skip;
+  const int64_t lds = apply_skip_lds_bytes(dtype, c0 + c1, cout, B);
+  const int64_t nblocks = p.nvox / 128;
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(nblocks, 1024)));
+  auto go = [&](auto kern) -> int {
+    CWDM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kern, grid, dim3(256), (unsigned)lds, s, p);
+    return CWDM_OK;
+  };
+  int rc;
+  if (dtype == CWDM_BF16) rc = cout == 64 ? go(gn_apply_skip_kernel<bf16_t, 2>) : go(gn_apply_skip_kernel<bf16_t, 4>);
+  else rc = cout == 64 ? go(gn_apply_skip_kernel<float, 2>) : go(gn_apply_skip_kernel<float, 4>);
+  if (rc) return rc;
   CWDM_LAUNCHED();
   return CWDM_OK;
 }

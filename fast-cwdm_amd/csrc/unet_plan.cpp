@@ -9,6 +9,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
@@ -63,6 +64,7 @@ struct ConvStep {
   int cout;
   int level;                    // output level
   bool stats;
+  int skip_conv = -1;           // conv1 of a block with a 1x1 skip: index of the block's conv2
 };
 
 struct PoolStep {  // down-ResBlock pre-pass (cwdm_gn_silu_pool)
@@ -225,6 +227,7 @@ void build(cwdm_unet* u) {
     if (cin != cout) {
       conv_params(p + ".skip_connection", cout, cin, 1, &c2.ws_p, &c2.wsb_p);
       c2.sb0 = x0; c2.sb1 = x1; c2.cin_b = cin;
+      u->convs[blk.c1].skip_conv = (int)u->convs.size();  // c2's index once pushed below
     } else {
       c2.res = xres;
       c2.rmode = xrmode;
@@ -331,8 +334,21 @@ void build(cwdm_unet* u) {
   u->packed_bwd_bytes = bo;
 }
 
+}  // namespace
+namespace cwdm {
+bool v4_eligible(const cwdm_conv3d_desc* d);
+bool apply_skip_ok(int dtype, int C, int cout, int64_t B, int64_t vpb);
+int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
+                  const void* wskip, int cout, void* act, void* skip, hipStream_t s);
+int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
+              const void* res, int rmode, hipStream_t s);
+}  // namespace cwdm
+namespace {
+
 struct Layout {
   int64_t temb, ebias, split, split_bytes;
+  int64_t skipbuf = 0;          // conv2 residual written by the fused GroupNorm + 1x1-skip pass
+  std::vector<char> skip_fused; // per conv1 with a skip: that pass is used
   std::vector<int64_t> t_off, s_off, s_parts;
   std::vector<int64_t> ss_off, mr_off;
   int64_t total;
@@ -390,6 +406,25 @@ Layout layout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
   }
   L.split_bytes = split;
   L.split = take(split);
+  // ResBlocks with a 1x1 skip whose convs run on the DMA kernel: GN1 and the
+  // skip read x in one pass (cwdm::gn_apply_skip)
+  L.skip_fused.assign(u->convs.size(), 0);
+  int64_t skipb = 0;
+  const char* fe = std::getenv("CWDM_SKIP_FUSE");  // "0": A/B switch for the fused pass
+  const bool fuse = !(fe && fe[0] == '0');
+  for (size_t i = 0; fuse && i < u->convs.size(); ++i) {
+    const auto& c1 = u->convs[i];
+    if (c1.skip_conv < 0 || c1.gn < 0 || c1.amode != 0) continue;
+    const auto& c2 = u->convs[c1.skip_conv];
+    cwdm_conv3d_desc d1 = conv_shape(u, c1, B, D, H, W), d2 = conv_shape(u, c2, B, D, H, W);
+    const int64_t vpb = d1.D * d1.H * d1.W;
+    if (!cwdm::v4_eligible(&d1) || !cwdm::v4_eligible(&d2) ||
+        !cwdm::apply_skip_ok(u->cfg.dtype, c1.cin_a, c2.cout, B, vpb))
+      continue;
+    L.skip_fused[i] = 1;
+    skipb = std::max(skipb, B * vpb * c2.cout * es);
+  }
+  L.skipbuf = take(skipb);
   L.total = off;
   return L;
 }
@@ -595,7 +630,23 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
     else { d.out = wb + L.t_off[cs.out]; d.out_dtype = u->cfg.dtype; }
     d.stats = (cs.stats && cs.out >= 0) ? reinterpret_cast<float*>(wb + L.s_off[cs.out]) : nullptr;
     if (u->profiling) CWDM_HIP(hipEventRecord(u->ev[2 * conv_i], s));
-    if ((rc = cwdm_conv3d_forward(&d, stream))) return rc;
+    if (L.skip_fused[st.idx]) {
+      // conv1 of a skip block: SiLU(GN1(x)) for this conv and W_skip . x for conv2 in one pass
+      const auto& c2 = u->convs[cs.skip_conv];
+      const int64_t vpb = d.D * d.H * d.W;
+      void* act = wb + L.split;
+      if ((rc = cwdm::gn_apply_skip(d.a0, d.a_c0, d.a1, d.a_c1, d.a_gn, B, vpb, u->cfg.dtype, pk + c2.wsk_off,
+                                    c2.cout, act, wb + L.skipbuf, s)))
+        return rc;
+      if ((rc = cwdm::v4_launch(&d, act, d.a_c0 + d.a_c1, nullptr, 0, 1, d.res, d.res_mode, s))) return rc;
+    } else {
+      if (cs.ws_p >= 0 && st.idx > 0 && L.skip_fused[st.idx - 1] && u->convs[st.idx - 1].skip_conv == st.idx) {
+        // the skip was computed in conv1's GroupNorm pass: a plain residual here
+        d.b0 = d.b1 = nullptr; d.b_c0 = d.b_c1 = 0; d.b_w = nullptr;
+        d.res = wb + L.skipbuf; d.res_mode = 0;
+      }
+      if ((rc = cwdm_conv3d_forward(&d, stream))) return rc;
+    }
     if (u->profiling) {
       CWDM_HIP(hipEventRecord(u->ev[2 * conv_i + 1], s));
       u->ev_flops[conv_i] = 2.0 * B * d.D * d.H * d.W * cs.cout * (27.0 * cs.cin_a + cs.cin_b);

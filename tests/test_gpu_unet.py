@@ -65,6 +65,30 @@ def test_production_unet_forward_fp32(grid):
     assert rel_err(out, ref) < 1e-3
 
 
+@pytest.mark.parametrize("grid", [(16, 16, 32), (32, 32, 64)])
+def test_production_unet_forward_dma_kernel(grid):
+    """Every conv the shape allows on the DMA-staged kernel (path 2), including
+    the fused GroupNorm + 1x1-skip pass of the skip ResBlocks, vs the oracle
+    (fp32, 1e-3); then the bf16 model on the same path within 6e-2 of it."""
+    from cwdm_hip._lib import lib
+    P = ou.random_params(seed=13)
+    cfg = dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4))
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(1, 32, *grid, generator=g)
+    t = torch.tensor([700])
+    prev = lib().cwdm_conv3d_set_path(2)
+    try:
+        m32 = _product_model(cfg, 32, P, "fp32")
+        with torch.no_grad():
+            out = m32(x.to(DEV), t.to(DEV))
+            if grid[0] <= 16:
+                assert rel_err(out, ou.unet_forward(P, x, t)) < 1e-3
+            m16 = _product_model(cfg, 32, P, "bf16")
+            assert rel_err(m16(x.to(DEV), t.to(DEV)), out) < 6e-2
+    finally:
+        lib().cwdm_conv3d_set_path(prev)
+
+
 def test_production_unet_bf16_close_to_fp32():
     P = ou.random_params(seed=12)
     cfg = dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4))
