@@ -648,7 +648,8 @@ __global__ void __launch_bounds__(256) conv3d_kernel(ConvParams p) {
 }
 
 // split-K, stage 1: partial[0] += partial[1..S-1], elementwise over the whole
-// output (bandwidth-bound, every CU busy) ...
+// output (bandwidth-bound, every CU busy; the per-tile finish below has only
+// one workgroup per tile) ...
 template <int Dummy = 0>
 __global__ void __launch_bounds__(256) splitk_sum_kernel(float* __restrict__ part, int S, long long n4) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -662,9 +663,10 @@ __global__ void __launch_bounds__(256) splitk_sum_kernel(float* __restrict__ par
   p4[i] = a;
 }
 
-// ... stage 2: epilogue on the summed tile, one workgroup per (spatial tile, channel tile)
+// ... stage 2 (S = 1), or the whole finish for small S: sum the S partial slices of a tile and run the epilogue on it,
+// one workgroup per (spatial tile, channel tile)
 template <typename T, int BX, int BY, int BZ, int NF>
-__global__ void __launch_bounds__(256) conv3d_reduce_kernel(ConvParams p) {
+__global__ void __launch_bounds__(256) conv3d_reduce_kernel(ConvParams p, int S) {
   constexpr int ROWS = BX * BY * BZ, NT = 32 * NF, LD = NT + 4, CG = NT / 8;
   __shared__ __attribute__((aligned(16))) float E[ROWS * LD > 256 * 16 ? ROWS * LD : 256 * 16];
   const int tid = threadIdx.x;
@@ -684,13 +686,16 @@ __global__ void __launch_bounds__(256) conv3d_reduce_kernel(ConvParams p) {
     for (int e = 0; e < 8; ++e) v[e] = 0.f;
     if (!(ox >= p.W || oy >= p.H || oz >= p.D || nvalid <= 0)) {
       const long long vox = (((long long)b * p.D + oz) * p.H + oy) * p.W + ox;
-      const float* src = p.partial + vox * p.cout + cbase;
-      if (nvalid == 8) {
-        float4 a = *reinterpret_cast<const float4*>(src), c = *reinterpret_cast<const float4*>(src + 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-        v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
-      } else {
-        for (int e = 0; e < nvalid; ++e) v[e] = src[e];
+      const long long slice = (long long)p.B * p.D * p.H * p.W * p.cout;
+      for (int k = 0; k < S; ++k) {
+        const float* src = p.partial + k * slice + vox * p.cout + cbase;
+        if (nvalid == 8) {
+          const float4 a = *reinterpret_cast<const float4*>(src), c = *reinterpret_cast<const float4*>(src + 4);
+          v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+          v[4] += c.x; v[5] += c.y; v[6] += c.z; v[7] += c.w;
+        } else {
+          for (int e = 0; e < nvalid; ++e) v[e] += src[e];
+        }
       }
     }
 #pragma unroll
@@ -964,7 +969,7 @@ int launch_conv(const ConvParams& p, hipStream_t s) {
     CWDM_LAUNCHED();
     ConvParams q = p;
     q.ksplit = 1;
-    hipLaunchKernelGGL((conv3d_reduce_kernel<T, BX, BY, BZ, NF>), dim3((unsigned)nblk), dim3(256), 0, s, q);
+    hipLaunchKernelGGL((conv3d_reduce_kernel<T, BX, BY, BZ, NF>), dim3((unsigned)nblk), dim3(256), 0, s, q, 1);
     CWDM_LAUNCHED();
   }
   return CWDM_OK;
@@ -993,7 +998,7 @@ int launch_wide(const ConvParams& p, hipStream_t s) {
     CWDM_LAUNCHED();
     ConvParams q = p;
     q.ksplit = 1;
-    hipLaunchKernelGGL((conv3d_reduce_kernel<T, 32, 4, 4, NF>), dim3((unsigned)nblk), dim3(256), 0, s, q);
+    hipLaunchKernelGGL((conv3d_reduce_kernel<T, 32, 4, 4, NF>), dim3((unsigned)nblk), dim3(256), 0, s, q, 1);
     CWDM_LAUNCHED();
   }
   return CWDM_OK;

@@ -77,6 +77,23 @@ std::atomic<int> g_conv_path{[] {
 
 std::atomic<unsigned long long*> g_stamps{nullptr};
 
+int64_t v4_items(const cwdm_conv3d_desc* d) {
+  return d->B * (d->W / 32) * (d->H / 4) * (d->D / 4) * (d->cout / 64);
+}
+
+// K split of a grid with fewer tiles than two workgroups per CU (the 32^3
+// level): enough K slices for ~512 work items, at least two chunks per slice
+int v4_ksplit(const cwdm_conv3d_desc* d) {
+  const int ck = d->dtype == CWDM_BF16 ? 16 : 8;
+  const int nch = (d->a_c0 + d->a_c1) / ck;
+  const int64_t nblk = v4_items(d);
+  if (nblk >= 512 || nch < 2) return 1;
+  int S = (int)std::min<int64_t>((512 + nblk - 1) / nblk, nch / 2);
+  if (S < 1) S = 1;
+  const int per = (nch + S - 1) / S;
+  return (nch + per - 1) / per;
+}
+
 bool v4_eligible(const cwdm_conv3d_desc* d) {
   const int path = g_conv_path.load(std::memory_order_relaxed);
   if (path == 1) return false;
@@ -85,8 +102,8 @@ bool v4_eligible(const cwdm_conv3d_desc* d) {
   if (d->a_mode != 0 && d->a_mode != 1) return false;
   if (d->res_mode < -1 || d->res_mode > 1) return false;
   if (d->out1 && d->out_c0 % 8) return false;
-  const int64_t nblk = d->B * (d->W / 32) * (d->H / 4) * (d->D / 4) * (d->cout / 64);
-  if (nblk < 512 && path != 2) return false;  // small grids: the split-K brick kernels fill the chip better
+  const int64_t nblk = v4_items(d);
+  if (nblk * v4_ksplit(d) < 384 && path != 2) return false;  // too few work items even K-split: the brick kernels
   const int esz = d->dtype == CWDM_BF16 ? 2 : 4;
   const int64_t sv = src_voxels(d);
   // the DMA range check works on 32-bit byte offsets per batch
@@ -100,6 +117,8 @@ int64_t v4_workspace_bytes(const cwdm_conv3d_desc* d) {
   int64_t ws = 0;
   if (d->a_gn) ws += align256(d->B * src_voxels(d) * (d->a_c0 + d->a_c1) * esz);
   if (d->b_w) ws += align256(d->B * d->D * d->H * d->W * d->cout * esz);
+  const int S = v4_ksplit(d);
+  if (S > 1) ws += align256(S * d->B * d->D * d->H * d->W * d->cout * 4);
   return ws;
 }
 
@@ -122,9 +141,10 @@ int gn_apply(const void* x0, int c0, const void* x1, int c1, const float* gn, in
 }
 
 // launch of the DMA-staged kernel on prepared sources: a0 (c0 channels,
-// chunk-major if a0_cm) and a1 (c1 channels, channels-last), residual res/rmode
+// chunk-major if a0_cm) and a1 (c1 channels, channels-last), residual res/rmode;
+// partial: fp32 scratch of v4_ksplit(d) output slices (unused without a K split)
 int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
-              const void* res, int rmode, hipStream_t s) {
+              const void* res, int rmode, void* partial, hipStream_t s) {
   const int esz = d->dtype == CWDM_BF16 ? 2 : 4;
   const int ck = d->dtype == CWDM_BF16 ? 16 : 8;
   const int64_t SV = src_voxels(d);
@@ -148,7 +168,16 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   p.out1 = d->out1; p.out_c0 = d->out_c0;
   p.accumulate = d->accumulate;
   p.stamps = g_stamps.load(std::memory_order_relaxed);
-  const long long nblk = (long long)p.B * p.tx * p.ty * p.tz * p.nct;
+  const int S = v4_ksplit(d);
+  p.ksplit = S;
+  p.kper = (p.nch + S - 1) / S;
+  if (S > 1) {
+    CWDM_REQUIRE(partial, CWDM_E_INVALID, "conv3d: K-split scratch missing");
+    p.ks_stride = (long long)p.B * p.D * p.H * p.W * p.cout;
+    p.bias = nullptr; p.res = nullptr; p.rmode = -1; p.stats = nullptr;
+    p.out = partial; p.out_f32 = 1; p.out1 = nullptr; p.out_c0 = 0; p.accumulate = 0;
+  }
+  const long long nblk = (long long)p.B * p.tx * p.ty * p.tz * p.nct * S;
   p.nblk = (int)nblk;
   // persistent: two workgroups per CU (80 KB LDS, <= 256 registers per lane each)
   static const int ncu = [] {
@@ -175,6 +204,29 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
     else hipLaunchKernelGGL((conv3d_v4_kernel<float, 0, false>), grid, dim3(256), 0, s, p);
   }
   CWDM_LAUNCHED();
+  if (S > 1) {
+    // finish: slice sum over the whole chip, then the per-tile epilogue
+    const long long n4 = p.ks_stride / 4;
+    float* part = reinterpret_cast<float*>(partial);
+    hipLaunchKernelGGL(splitk_sum_kernel<0>, dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, s, part, S, n4);
+    CWDM_LAUNCHED();
+    ConvParams q{};
+    q.B = p.B; q.D = p.D; q.H = p.H; q.W = p.W;
+    q.tx = p.tx; q.ty = p.ty; q.tz = p.tz;
+    q.cout = p.cout; q.nct = p.nct;
+    q.bias = d->bias; q.bias_bs = d->bias_bstride;
+    q.res = res; q.rmode = rmode;
+    q.out = d->out; q.out_f32 = (d->out_dtype == CWDM_F32 && d->dtype != CWDM_F32) ? 1 : (d->dtype == CWDM_F32);
+    q.stats = d->stats;
+    q.out1 = d->out1; q.out_c0 = d->out_c0;
+    q.accumulate = d->accumulate;
+    q.ksplit = 1;
+    q.partial = part;
+    const dim3 rg((unsigned)v4_items(d));
+    if (d->dtype == CWDM_BF16) hipLaunchKernelGGL((conv3d_reduce_kernel<bf16_t, 32, 4, 4, 2>), rg, dim3(256), 0, s, q, 1);
+    else hipLaunchKernelGGL((conv3d_reduce_kernel<float, 32, 4, 4, 2>), rg, dim3(256), 0, s, q, 1);
+    CWDM_LAUNCHED();
+  }
   return CWDM_OK;
 }
 
@@ -198,6 +250,7 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   int rmode = d->res_mode;
   if (d->b_w) {
     void* skip = ws;
+    ws += align256(d->B * d->D * d->H * d->W * d->cout * esz);
     cwdm_conv3d_desc e = *d;
     e.a0 = nullptr; e.a1 = nullptr; e.a_c0 = 0; e.a_c1 = 0; e.a_gn = nullptr; e.a_w = nullptr; e.a_mode = 0;
     e.bias = nullptr; e.bias_bstride = 0; e.stats = nullptr;
@@ -206,7 +259,7 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     if ((rc = legacy_conv3d_forward(&e, (cwdm_stream_t)s))) return rc;
     res = skip; rmode = 0;
   }
-  return v4_launch(d, a0, c0, a1, c1, a0_cm, res, rmode, s);
+  return v4_launch(d, a0, c0, a1, c1, a0_cm, res, rmode, v4_ksplit(d) > 1 ? ws : nullptr, s);
 }
 
 // ---------------------------------------------------------------------------

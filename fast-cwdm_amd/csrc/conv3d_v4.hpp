@@ -56,12 +56,18 @@ struct V4Params {
   void* out1; int out_c0;
   int accumulate;
   int stagger_cycles;  // delay of the second workgroup on each CU (0: off)
-  int nblk;  // tiles in total (B * tx * ty * tz * nct); gridDim.x <= nblk
+  int nblk;  // work items in total (B * tx * ty * tz * nct * ksplit); gridDim.x <= nblk
+  // split-K (small grids): work item = (tile, K slice ks); slice ks runs chunks
+  // [ks kper, min(nch, (ks + 1) kper)) and stores its fp32 partial tile at
+  // out + ks * ks_stride (the launcher points out at the fp32 slices, [V][cout]
+  // each, with no bias / residual / statistics); splitk_sum_kernel +
+  // conv3d_reduce_kernel finish the output.
+  int ksplit, kper;
+  long long ks_stride;
   unsigned long long* stamps;  // diagnostics: per-workgroup s_memtime stamps (cwdm_debug_conv_stamps), else null
 };
 
 __device__ unsigned g_v4_cu_arrivals[8 * 256];
-
 struct V4Cfg {
   static constexpr int HX = 34, HY = 6, HZ = 6, HV = HX * HY * HZ;  // 1224 halo voxels
   static constexpr int HVP = 1280;                                   // slots per quad plane (20 pieces)
@@ -129,7 +135,7 @@ __device__ __forceinline__ void v4_read_step(u32x4 (&av)[6], const unsigned char
 // statistics; every wave of the workgroup calls this.
 template <typename T, bool FAST>
 __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][4], int b, int sl, int ct, int x0,
-                                            int y0, int z0, int tid, int wv, unsigned char* smem) {
+                                            int y0, int z0, int ks, int tid, int wv, unsigned char* smem) {
   const int lane = tid & 63, lr = lane & 31, hh = lane >> 5, f = wv & 1, vg = wv >> 1;
   const int cbase = ct * 64 + f * 32 + 4 * hh;
   float ssum[16], ssq[16];
@@ -237,7 +243,7 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
             else ostride = p.out_c0;
           }
           if (p.out_f32 || sizeof(T) == 4) {
-            float* o = reinterpret_cast<float*>(obase) + vox * ostride + oc;
+            float* o = reinterpret_cast<float*>(obase) + ks * p.ks_stride + vox * ostride + oc;
             if (p.accumulate) {
               const float4 oq = *reinterpret_cast<const float4*>(o);
               v[0] += oq.x; v[1] += oq.y; v[2] += oq.z; v[3] += oq.w;
@@ -345,12 +351,18 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   const int SH = MODE == 1 ? p.H >> 1 : p.H, SW = MODE == 1 ? p.W >> 1 : p.W;
   // tile it of this workgroup -> (b, spatial tile sl, channel tile ct, origin) through the
   // XCD-aware bijective map: the tiles an XCD runs are one contiguous run (x fastest)
-  struct Tile { int b, sl, ct, x0, y0, z0; };
+  // (K slice slowest: the tiles an XCD runs share their weight chunks)
+  struct Tile { int b, sl, ct, x0, y0, z0, ks, c0, c1; };
+  const int nbase = nblk / p.ksplit;
   auto tile_of = [&](int it) {
     const int t = blockIdx.x + it * gridDim.x;
     const int xcd = t & 7, q8 = nblk >> 3, r8 = nblk & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (t >> 3);
+    int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (t >> 3);
     Tile r;
+    r.ks = wg / nbase;
+    wg -= r.ks * nbase;
+    r.c0 = r.ks * p.kper;
+    r.c1 = min(p.nch, r.c0 + p.kper);
     r.ct = wg % p.nct;
     const int st = wg / p.nct;
     r.b = st / tiles;
@@ -360,6 +372,8 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
     r.ct = __builtin_amdgcn_readfirstlane(r.ct); r.b = __builtin_amdgcn_readfirstlane(r.b);
     r.sl = __builtin_amdgcn_readfirstlane(r.sl); r.x0 = __builtin_amdgcn_readfirstlane(r.x0);
     r.y0 = __builtin_amdgcn_readfirstlane(r.y0); r.z0 = __builtin_amdgcn_readfirstlane(r.z0);
+    r.ks = __builtin_amdgcn_readfirstlane(r.ks); r.c0 = __builtin_amdgcn_readfirstlane(r.c0);
+    r.c1 = __builtin_amdgcn_readfirstlane(r.c1);
     return r;
   };
   const int ntile = (nblk - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
@@ -426,11 +440,11 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   };
   // accumulators start at the bias of their output channel (i = 4 j + k -> channel 8 j + 4 hh + k)
   f32x16 acc[2][4];
-  auto init_acc = [&]() {
+  auto init_acc = [&](int ks) {
     float bia[16];
     const float* bl = reinterpret_cast<const float*>(smem + C::pad(0) + 256) + f * 32 + 4 * hh;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) bia[i] = p.bias ? bl[8 * (i >> 2) + (i & 3)] : 0.f;
+    for (int i = 0; i < 16; ++i) bia[i] = (p.bias && ks == 0) ? bl[8 * (i >> 2) + (i & 3)] : 0.f;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -445,16 +459,16 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   Tile cur = tile_of(0);
   u32x4 wr[3][3];
   issue_bias(cur);
-  issue_halo(cur, 0, 0);
+  issue_halo(cur, cur.c0, 0);
   int gch = 0;  // chunk counter of the stream (selects the halo buffer)
   for (int it = 0; it < ntile; ++it) {
     const bool more = it + 1 < ntile;
     // the tile's halo and bias were issued under the previous tile (or above)
-    load_w(wr[0], cur.ct, 0, 0);
+    load_w(wr[0], cur.ct, cur.c0, 0);
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2])::"memory");
     __builtin_amdgcn_s_barrier();
     if (it == 0) V4_STAMP(1);
-    init_acc();
+    init_acc(cur.ks);
     // one chunk: 18 steps, step K = (group K / 2, plane K % 2).  The 6 halo
     // lines of step K + 1 are read before the 12 MFMAs of step K (software
     // pipeline, pinned by sched_barrier), so every MFMA block finds its
@@ -505,15 +519,16 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
         // which every wave finished before the previous barrier)
         const Tile nxt = tile_of(it + 1);
         issue_bias(nxt);
-        issue_halo(nxt, 0, (gch + 1) & 1);
+        issue_halo(nxt, nxt.c0, (gch + 1) & 1);
       }
-      if (it == 0 && c < 8) V4_STAMP(4 + c);
+      if (it == 0 && c - cur.c0 < 8) V4_STAMP(4 + c - cur.c0);
       ++gch;
     };
-    for (int c = 0; c + 1 < p.nch; ++c) chunk(std::false_type{}, c);
-    chunk(std::true_type{}, p.nch - 1);
+    for (int c = cur.c0; c + 1 < cur.c1; ++c) chunk(std::false_type{}, c);
+    chunk(std::true_type{}, cur.c1 - 1);
     if (it == 0) V4_STAMP(12);
-    v4_epilogue<T, FAST>(p, acc, cur.b, cur.sl, cur.ct, cur.x0, cur.y0, cur.z0, tid, wv, smem);
+    // (K split: out is this slice's fp32 partial, see V4Params)
+    v4_epilogue<T, FAST>(p, acc, cur.b, cur.sl, cur.ct, cur.x0, cur.y0, cur.z0, cur.ks, tid, wv, smem);
     if (it == 0) V4_STAMP(13);
     if (more) cur = tile_of(it + 1);
   }

@@ -341,7 +341,7 @@ bool apply_skip_ok(int dtype, int C, int cout, int64_t B, int64_t vpb);
 int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
                   const void* wskip, int cout, void* act, void* skip, hipStream_t s);
 int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
-              const void* res, int rmode, hipStream_t s);
+              const void* res, int rmode, void* partial, hipStream_t s);
 }  // namespace cwdm
 namespace {
 
@@ -638,7 +638,8 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
       if ((rc = cwdm::gn_apply_skip(d.a0, d.a_c0, d.a1, d.a_c1, d.a_gn, B, vpb, u->cfg.dtype, pk + c2.wsk_off,
                                     c2.cout, act, wb + L.skipbuf, s)))
         return rc;
-      if ((rc = cwdm::v4_launch(&d, act, d.a_c0 + d.a_c1, nullptr, 0, 1, d.res, d.res_mode, s))) return rc;
+      void* part = wb + L.split + ((B * vpb * (d.a_c0 + d.a_c1) * es + 255) & ~(int64_t)255);
+      if ((rc = cwdm::v4_launch(&d, act, d.a_c0 + d.a_c1, nullptr, 0, 1, d.res, d.res_mode, part, s))) return rc;
     } else {
       if (cs.ws_p >= 0 && st.idx > 0 && L.skip_fused[st.idx - 1] && u->convs[st.idx - 1].skip_conv == st.idx) {
         // the skip was computed in conv1's GroupNorm pass: a plain residual here

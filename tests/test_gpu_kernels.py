@@ -231,6 +231,9 @@ V4_CASES = [
     ("v4_gn_concat_skip_res", 2, (4, 8, 32), 32, 16, 64, 0, True, True, 0),
     ("v4_up_res", 1, (8, 4, 64), 32, 0, 128, 1, True, False, 1),
     ("v4_concat_nogn", 1, (4, 12, 32), 16, 32, 128, 0, False, False, 0),
+    # K-split work items (fewer tiles than CU slots): partial slices + finish pass
+    ("v4_ksplit_gn_skip", 1, (8, 4, 32), 96, 32, 128, 0, True, True, 0),
+    ("v4_ksplit_up", 2, (8, 8, 32), 64, 0, 64, 1, True, False, 1),
 ]
 
 
@@ -242,8 +245,8 @@ def test_conv3d_dma_kernel_vs_torch(case, dtype_name):
     from cwdm_hip._lib import lib
     L = lib()
     prev = L.cwdm_conv3d_set_path(2)
-    try:
-        test_conv3d_fused_vs_torch(case, dtype_name, False)
+    try:  # with a workspace: the GroupNorm pre-pass, the 1x1 skip and the K-split partials live there
+        test_conv3d_fused_vs_torch(case, dtype_name, True)
     finally:
         L.cwdm_conv3d_set_path(prev)
 
