@@ -251,6 +251,27 @@ def test_conv3d_dma_kernel_vs_torch(case, dtype_name):
         L.cwdm_conv3d_set_path(prev)
 
 
+@pytest.mark.parametrize("grid,B,cin", [((4, 4, 32), 1, 64), ((8, 8, 64), 2, 64), ((4, 8, 32), 1, 32)])
+def test_output_head_kernel_vs_torch(grid, B, cin):
+    """The narrow-output head kernel (conv3d_head.hip: GN+SiLU fused, 16x16x32
+    MFMA, 8 of 16 output lanes real): bf16 operands, fp32 output, vs F.conv3d."""
+    from cwdm_hip import _lib
+    g = torch.Generator().manual_seed(11)
+    D, H, W = grid
+    cout = 8
+    x = torch.randn(B, cin, D, H, W, generator=g).to(torch.bfloat16).float()
+    w = (torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)).to(torch.bfloat16).float()
+    bias = torch.randn(cout, generator=g) * 0.1
+    scale = 1 + 0.2 * torch.randn(B, cin, generator=g)
+    shift = 0.2 * torch.randn(B, cin, generator=g)
+    gn = torch.stack([scale, shift], -1).contiguous()
+    h = F.silu(x * scale[:, :, None, None, None] + shift[:, :, None, None, None]).to(torch.bfloat16).float()
+    ref = F.conv3d(h, w, bias, padding=1)
+    out, _ = _conv_call(_lib.CWDM_BF16, (B, D, H, W), _nd(x).to(DEV, torch.bfloat16), None, 0, gn.to(DEV),
+                        w.to(DEV), bias.to(DEV), out_f32=True, stats=False)
+    assert rel_err(_nc(out.float().cpu()), ref) < 1e-2
+
+
 def test_gn_apply_matches_torch():
     from cwdm_hip import _lib
     from cwdm_hip._lib import check, lib
