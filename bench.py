@@ -32,6 +32,7 @@ for _p in (os.path.join(ROOT, "fast-cwdm_amd"), ROOT):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3
 
@@ -157,6 +158,13 @@ def main():
     plan.set_profiling(False)
     step_flops = plan.flops(1, n, n, n)
 
+    # HBM bytes of the same conv family per step, from the committed rocprofv3
+    # PMC passes of this bench (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950)
+    traffic = None
+    if n == 128 and args.dtype == "bf16" and os.path.exists(TRAFFIC_JSON):
+        with open(TRAFFIC_JSON) as fh:
+            traffic = json.load(fh)["hbm_bytes"]
+
     ms_per_step = 1000.0 * elapsed / args.steps
     value = world * args.steps / elapsed
     peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
@@ -181,7 +189,8 @@ def main():
         "sampling_wallclock_s_per_volume_1000_steps": round(1000 * ms_per_step / 1000.0, 2),
         "mfma_util_whole_step": round(step_flops * (value / world) / 1e12 / peak, 4),
         "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": None,
+                     "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "traffic_unit": "HBM bytes per step of the conv family (profiles/r01/pmc_traffic.json)",
                      "kernel": f"conv3d_kernel (all {n_conv} launches of one step; {conv_ms:.2f} ms, "
                                f"{conv_flops / 1e12:.2f} TFLOP)"},
     }
