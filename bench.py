@@ -107,6 +107,9 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-grid", type=int, default=0, help="0 = same grid as the GPU run")
+    ap.add_argument("--graph", type=int, default=1, help="replay one HIP-graph-captured step per timestep")
+    ap.add_argument("--respaced", type=int, default=1,
+                    help="also time config 4: a full 50-step respaced (ddim50) volume, graph-captured loop")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -131,7 +134,8 @@ def main():
     T = diffusion.num_timesteps
     total = args.warmup + args.steps
     assert total <= T
-    loop = diffusion._native_loop(model, x_T, list(range(T))[::-1][:total + 1], cond, True)
+    loop = diffusion._native_loop(model, x_T, list(range(T))[::-1][:total + 2], cond, True,
+                                  graph=bool(args.graph), fresh_outputs=False)
     for _ in range(args.warmup):
         next(loop)
     torch.cuda.synchronize()
@@ -150,13 +154,45 @@ def main():
         elapsed = float(tt)
 
     # roofline of the dominant kernel: per-conv hipEvents over one extra step
+    # (an eager step: event records are not part of the captured graph)
     plan = model.plan
     plan.set_profiling(True)
+    loop.close()
+    loop = diffusion._native_loop(model, x_T, [T - 1], cond, True, graph=False)
     next(loop)
     torch.cuda.synchronize()
     conv_ms, conv_flops, n_conv = plan.profile_read()
     plan.set_profiling(False)
     step_flops = plan.flops(1, n, n, n)
+
+    # config 4: respaced 50-step sampling of one whole volume (timestep_respacing
+    # "ddim50" = stride-20 subset of the 1000-step schedule), graph-captured loop
+    respaced = None
+    if args.respaced:
+        from guided_diffusion import respace
+        sp = respace.SpacedDiffusion(use_timesteps=respace.space_timesteps(1000, "ddim50"),
+                                     betas=diffusion.betas, model_mean_type=diffusion.model_mean_type,
+                                     model_var_type=diffusion.model_var_type, loss_type=diffusion.loss_type,
+                                     rescale_timesteps=diffusion.rescale_timesteps)
+        sp.mode = "i2i"
+        sp.use_hip_graph = bool(args.graph)
+        for rep in range(2):   # first pass warms the graph capture path
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t1 = time.perf_counter()
+            sp.p_sample_loop(model, tuple(x_T.shape), noise=x_T, cond=cond, progress=False)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            rs = time.perf_counter() - t1
+        if world > 1:
+            tt = torch.tensor([rs], device=device, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            rs = float(tt)
+        respaced = {"workload": "config4: timestep_respacing ddim50 (50 of 1000 steps), one volume per GPU, "
+                                f"{'HIP-graph-captured' if args.graph else 'eager'} step",
+                    "s_per_volume": round(rs, 4), "denoising_steps_per_s": round(world * 50 / rs, 3)}
 
     # HBM bytes of the same conv family per step, from the committed rocprofv3
     # PMC passes of this bench (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950)
@@ -187,6 +223,8 @@ def main():
                    "model": "UNetModel run.sh (mc 64, mult 1,2,2,4,4, 2 res blocks, 81.5M params)",
                    "global_batch": world, "seq_len": n ** 3, "parallelism": f"replicas{world}"},
         "sampling_wallclock_s_per_volume_1000_steps": round(1000 * ms_per_step / 1000.0, 2),
+        "hip_graph": bool(args.graph),
+        "respaced_ddim50": respaced,
         "mfma_util_whole_step": round(step_flops * (value / world) / 1e12 / peak, 4),
         "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,

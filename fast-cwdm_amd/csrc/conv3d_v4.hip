@@ -286,7 +286,7 @@ struct ApplySkipParams {
   void* skip;          // [B][vpb][cout]
 };
 
-template <typename T, int NF>
+template <typename T, int NF, int QT>
 __global__ void __launch_bounds__(256) gn_apply_skip_kernel(ApplySkipParams p) {
   constexpr int CK = ConvTr<T>::CK, EPQ = ConvTr<T>::EPQ, ES = sizeof(T);
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -300,22 +300,45 @@ __global__ void __launch_bounds__(256) gn_apply_skip_kernel(ApplySkipParams p) {
   unsigned char* xt = lds + wbytes + ((p.B * C * 8 + 15) & ~15);
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, hh = lane >> 5, wv = tid >> 6;
   const int q0 = p.c0 * ES / 16, q1 = p.c1 * ES / 16;   // 16-byte quads per row of each source
+  const int nq0 = 128 * q0, nqt = (q0 + q1) / 2;        // quads of source 0 per block; per thread
   const long long nblocks = p.nvox / 128;
+  // the next block's 128 x rows are loaded into registers while this block
+  // computes (consecutive lanes read consecutive 16-byte quads), then copied
+  // to LDS: HBM latency hides under the MFMA / store work
+  u32x4 pf[QT];
+  auto fetch = [&](long long blk) {
+    const long long v0 = blk * 128;
+#pragma unroll
+    for (int j = 0; j < QT; ++j) {
+      if (j >= nqt) break;
+      const int i = tid + 256 * j;
+      if (i < nq0) {
+        const int vl = i / q0, qq = i - vl * q0;
+        pf[j] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(p.x0) + ((v0 + vl) * q0 + qq) * 16);
+      } else {
+        const int i1 = i - nq0, vl = i1 / q1, qq = i1 - vl * q1;
+        pf[j] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(p.x1) + ((v0 + vl) * q1 + qq) * 16);
+      }
+    }
+  };
+  auto put = [&]() {
+#pragma unroll
+    for (int j = 0; j < QT; ++j) {
+      if (j >= nqt) break;
+      const int i = tid + 256 * j;
+      int vl, col;
+      if (i < nq0) { vl = i / q0; col = i - vl * q0; }
+      else { const int i1 = i - nq0; vl = i1 / q1; col = q0 + (i1 - vl * q1); }
+      *reinterpret_cast<u32x4*>(xt + vl * RS + col * 16) = pf[j];
+    }
+  };
+  if ((long long)blockIdx.x < nblocks) fetch(blockIdx.x);
   for (long long blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
     const long long v0 = blk * 128;
     __syncthreads();  // previous block's column reads are done (and W / gn staged, first time)
-    // stage the 128 x rows: consecutive lanes read consecutive 16-byte quads
-    for (int i = tid; i < 128 * q0; i += 256) {
-      const int vl = i / q0, qq = i - vl * q0;
-      *reinterpret_cast<u32x4*>(xt + vl * RS + qq * 16) =
-          *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(p.x0) + ((v0 + vl) * q0 + qq) * 16);
-    }
-    for (int i = tid; i < 128 * q1; i += 256) {
-      const int vl = i / q1, qq = i - vl * q1;
-      *reinterpret_cast<u32x4*>(xt + vl * RS + (q0 + qq) * 16) =
-          *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(p.x1) + ((v0 + vl) * q1 + qq) * 16);
-    }
+    put();
     __syncthreads();
+    if (blk + gridDim.x < nblocks) fetch(blk + gridDim.x);
     const int vl = wv * 32 + lr;
     const long long v = v0 + vl;
     const int b = (int)(v0 / p.vpb);
@@ -368,8 +391,9 @@ int64_t apply_skip_lds_bytes(int dtype, int C, int cout, int64_t B) {
 
 bool apply_skip_ok(int dtype, int C, int cout, int64_t B, int64_t vpb) {
   const int ck = dtype == CWDM_BF16 ? 16 : 8;
+  const int qt = C * (dtype == CWDM_BF16 ? 2 : 4) / 32;   // prefetch registers per thread (kernel's QT)
   return (dtype == CWDM_BF16 || dtype == CWDM_F32) && (cout == 64 || cout == 128) && vpb % 128 == 0 &&
-         C % ck == 0 && apply_skip_lds_bytes(dtype, C, cout, B) <= 160 * 1024;
+         C % ck == 0 && qt <= 16 && apply_skip_lds_bytes(dtype, C, cout, B) <= 160 * 1024;
 }
 
 int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
@@ -387,8 +411,8 @@ int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* g
     return CWDM_OK;
   };
   int rc;
-  if (dtype == CWDM_BF16) rc = cout == 64 ? go(gn_apply_skip_kernel<bf16_t, 2>) : go(gn_apply_skip_kernel<bf16_t, 4>);
-  else rc = cout == 64 ? go(gn_apply_skip_kernel<float, 2>) : go(gn_apply_skip_kernel<float, 4>);
+  if (dtype == CWDM_BF16) rc = cout == 64 ? go(gn_apply_skip_kernel<bf16_t, 2, 16>) : go(gn_apply_skip_kernel<bf16_t, 4, 16>);
+  else rc = cout == 64 ? go(gn_apply_skip_kernel<float, 2, 16>) : go(gn_apply_skip_kernel<float, 4, 16>);
   if (rc) return rc;
   CWDM_LAUNCHED();
   return CWDM_OK;

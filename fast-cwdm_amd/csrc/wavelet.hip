@@ -161,9 +161,12 @@ struct S3 { int64_t b, c, v; };
 inline S3 s3(const int64_t* p) { return p ? S3{p[0], p[1], p[2]} : S3{0, 0, 0}; }
 
 // Fused a3 + a7 + a9: one subband voxel (8 channels) per thread.
+// vec bit 0: model_out holds a voxel's 8 channels in 32 contiguous aligned bytes
+// (the U-Net's NDHWC fp32 output); bit 1: the same for the mirror (16 B bf16 /
+// 32 B fp32) -- one wide access instead of 8 strided scalars.
 template <typename MirT>
 __global__ void __launch_bounds__(256) sampler_kernel(cwdm_sampler_args a, S3 mo, S3 xt, S3 xp, S3 nz, S3 px,
-                                                     S3 mr_) {
+                                                     S3 mr_, int vec) {
   int64_t nvox = a.d * a.h * a.w;
   int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= a.B * nvox) return;
@@ -173,11 +176,17 @@ __global__ void __launch_bounds__(256) sampler_kernel(cwdm_sampler_args a, S3 mo
   const float* cf = a.coef + t * 8;
   const float c1 = cf[0], c2 = cf[1], sg = cf[2];
   float m[8], xv[8];
+  if (vec & 1) {
+    const float4* p4 = reinterpret_cast<const float4*>(a.model_out + b * mo.b + v * mo.v);
+    const float4 u0 = p4[0], u1 = p4[1];
+    m[0] = u0.x; m[1] = u0.y; m[2] = u0.z; m[3] = u0.w;
+    m[4] = u1.x; m[5] = u1.y; m[6] = u1.z; m[7] = u1.w;
+  } else {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    m[q] = a.model_out[b * mo.b + q * mo.c + v * mo.v];
-    xv[q] = a.x_t[b * xt.b + q * xt.c + v * xt.v];
+    for (int q = 0; q < 8; ++q) m[q] = a.model_out[b * mo.b + q * mo.c + v * mo.v];
   }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) xv[q] = a.x_t[b * xt.b + q * xt.c + v * xt.v];
   if (a.mean_type == 1) {
     // EPSILON: x0 = sqrt(1/acp) * x_t - sqrt(1/acp - 1) * eps (gaussian_diffusion.py:392-397)
 #pragma unroll
@@ -197,14 +206,32 @@ __global__ void __launch_bounds__(256) sampler_kernel(cwdm_sampler_args a, S3 mo
     for (int q = 0; q < 8; ++q) pred[q] = m[q];
   }
   const bool noisy = (t != 0) && a.noise;
+  float r[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     float mean = ad(mr(c1, pred[q]), mr(c2, xv[q]));
-    float r = mean;
-    if (noisy) r = ad(mean, mr(sg, a.noise[b * nz.b + q * nz.c + v * nz.v]));
-    a.x_prev[b * xp.b + q * xp.c + v * xp.v] = r;
+    r[q] = mean;
+    if (noisy) r[q] = ad(mean, mr(sg, a.noise[b * nz.b + q * nz.c + v * nz.v]));
+    a.x_prev[b * xp.b + q * xp.c + v * xp.v] = r[q];
     if (a.pred_xstart) a.pred_xstart[b * px.b + q * px.c + v * px.v] = pred[q];
-    if (a.mirror) st<MirT>(a.mirror, b * mr_.b + q * mr_.c + v * mr_.v, r);
+  }
+  if (!a.mirror) return;
+  if (vec & 2) {
+    if constexpr (sizeof(MirT) == 2) {
+      uint4 q;
+      q.x = (unsigned)f2bf(r[0]) | ((unsigned)f2bf(r[1]) << 16);
+      q.y = (unsigned)f2bf(r[2]) | ((unsigned)f2bf(r[3]) << 16);
+      q.z = (unsigned)f2bf(r[4]) | ((unsigned)f2bf(r[5]) << 16);
+      q.w = (unsigned)f2bf(r[6]) | ((unsigned)f2bf(r[7]) << 16);
+      *reinterpret_cast<uint4*>(reinterpret_cast<MirT*>(a.mirror) + b * mr_.b + v * mr_.v) = q;
+    } else {
+      float4* o = reinterpret_cast<float4*>(reinterpret_cast<MirT*>(a.mirror) + b * mr_.b + v * mr_.v);
+      o[0] = make_float4(r[0], r[1], r[2], r[3]);
+      o[1] = make_float4(r[4], r[5], r[6], r[7]);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) st<MirT>(a.mirror, b * mr_.b + q * mr_.c + v * mr_.v, r[q]);
   }
 }
 
@@ -267,10 +294,17 @@ extern "C" int cwdm_sampler_step(const cwdm_sampler_args* a, cwdm_stream_t strea
   dim3 grid((unsigned)ceil_div(n, 256));
   S3 mo = s3(a->mo_s), xt = s3(a->xt_s), xp = s3(a->xp_s), nz = s3(a->nz_s), px = s3(a->px_s),
      mi = s3(a->mr_s);
+  auto aligned = [](const void* p, int64_t bs, int64_t vs, int esz, int al) {
+    return ((uintptr_t)p % al) == 0 && (bs * esz) % al == 0 && (vs * esz) % al == 0;
+  };
+  const int mesz = a->mirror_dtype == CWDM_BF16 ? 2 : 4;
+  int vec = 0;
+  if (mo.c == 1 && aligned(a->model_out, mo.b, mo.v, 4, 16)) vec |= 1;
+  if (a->mirror && mi.c == 1 && aligned(a->mirror, mi.b, mi.v, mesz, 16)) vec |= 2;
   if (a->mirror && a->mirror_dtype == CWDM_BF16)
-    hipLaunchKernelGGL(sampler_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, *a, mo, xt, xp, nz, px, mi);
+    hipLaunchKernelGGL(sampler_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, *a, mo, xt, xp, nz, px, mi, vec);
   else if (!a->mirror || a->mirror_dtype == CWDM_F32)
-    hipLaunchKernelGGL(sampler_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *a, mo, xt, xp, nz, px, mi);
+    hipLaunchKernelGGL(sampler_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *a, mo, xt, xp, nz, px, mi, vec);
   else
     return fail(CWDM_E_INVALID, "cwdm_sampler_step: bad mirror dtype");
   CWDM_LAUNCHED();

@@ -119,6 +119,9 @@ class GaussianDiffusion:
         self.posterior_mean_coef2 = (1.0 - self.alphas_cumprod_prev) * np.sqrt(alphas) / (1.0 - self.alphas_cumprod)
         self._dev_cache = {}
 
+    # capture the native sampling step in a HIP graph (see _native_loop)
+    use_hip_graph = False
+
     # ---- tables -------------------------------------------------------------
     def _fixed_variance(self):
         if self.model_var_type == ModelVarType.FIXED_LARGE:
@@ -263,13 +266,14 @@ class GaussianDiffusion:
         for sample in self.p_sample_loop_progressive(model, shape, time=time, noise=noise,
                                                      clip_denoised=clip_denoised, denoised_fn=denoised_fn,
                                                      cond_fn=cond_fn, model_kwargs=model_kwargs, device=device,
-                                                     progress=progress, cond=cond, noise_fn=noise_fn):
+                                                     progress=progress, cond=cond, noise_fn=noise_fn,
+                                                     _reuse_outputs=True):
             final = sample
         return final["sample"]
 
     def p_sample_loop_progressive(self, model, shape, time=None, noise=None, clip_denoised=True, denoised_fn=None,
                                   cond_fn=None, model_kwargs=None, device=None, progress=True, cond=None,
-                                  noise_fn=None):
+                                  noise_fn=None, _reuse_outputs=False):
         """Reference :668-719.  ``noise_fn`` (extension, default ``th.randn_like``)
         supplies each step's noise; parity tests inject fixed noise through it."""
         if device is None:
@@ -288,7 +292,8 @@ class GaussianDiffusion:
                 pass
         unet = _native_unet(model)
         if unet is not None and denoised_fn is None and cond_fn is None and not model_kwargs:
-            yield from self._native_loop(unet, img, indices, cond, clip_denoised, noise_fn)
+            yield from self._native_loop(unet, img, indices, cond, clip_denoised, noise_fn,
+                                         fresh_outputs=not _reuse_outputs)
             return
         for i in indices:
             t = th.tensor([i] * shape[0], device=device)
@@ -298,8 +303,17 @@ class GaussianDiffusion:
                 yield out
                 img = out["sample"]
 
-    def _native_loop(self, unet, img, indices, cond, clip_denoised, noise_fn=None):
-        """Channels-last resident loop for the native UNetModel."""
+    def _native_loop(self, unet, img, indices, cond, clip_denoised, noise_fn=None, graph=None, fresh_outputs=True):
+        """Channels-last resident loop for the native UNetModel.
+
+        graph: capture one denoising step (U-Net launch list + noise draw +
+        fused sampler epilogue) in a HIP graph and replay it for every later
+        step (default: ``self.use_hip_graph``; only with the default noise
+        source, whose draw torch's graph-safe generator replays).  The timestep
+        is the only per-step input: two 8-byte device fills before each replay.
+        fresh_outputs=False lets the yielded tensors be the graph's static
+        buffers (overwritten by the next step; p_sample_loop only keeps the last).
+        """
         dev = img.device
         B, C, d, h, w = img.shape
         V = d * h * w
@@ -321,19 +335,61 @@ class GaussianDiffusion:
         coef = self.coef_table(dev)
         mean_type = self._mean_type_code()
         s = _ncdhw(img)
+        if graph is None:
+            graph = self.use_hip_graph
+        graph = graph and noise_fn is None
+        indices = list(indices)
+        t = th.empty((B,), dtype=th.int64, device=dev)
+        t_model = th.empty((B,), dtype=th.float32, device=dev)
+
+        def step(src, dst, pred, noise):
+            unet.forward_ndhwc(xin, t_model, out_nd)
+            if noise is None:
+                noise = (noise_fn or th.randn_like)(src)
+            else:
+                noise.normal_()
+            ops.sampler_step(out_nd, (V * C, 1, C), src, s, dst, s, noise, s, coef, t, self.num_timesteps,
+                             B, d, h, w, clip_denoised=clip_denoised, pred_xstart=pred, px_s=s,
+                             mirror=xin, mr_s=(V * cin, 1, cin), mean_type=mean_type)
+
         with th.no_grad():
-            for i in indices:
-                t = th.full((B,), i, dtype=th.int64, device=dev)
-                t_model = th.full((B,), self._model_timestep(i), dtype=th.float32, device=dev)
-                unet.forward_ndhwc(xin, t_model, out_nd)
-                noise = (noise_fn or th.randn_like)(img)
-                new = th.empty_like(img)
-                pred = th.empty_like(img)
-                ops.sampler_step(out_nd, (V * C, 1, C), img, s, new, s, noise, s, coef, t, self.num_timesteps,
-                                 B, d, h, w, clip_denoised=clip_denoised, pred_xstart=pred, px_s=s,
-                                 mirror=xin, mr_s=(V * cin, 1, cin), mean_type=mean_type)
-                yield {"sample": new, "pred_xstart": pred}
-                img = new
+            if not graph or len(indices) < 3:
+                for i in indices:
+                    t.fill_(i)
+                    t_model.fill_(self._model_timestep(i))
+                    new = th.empty_like(img)
+                    pred = th.empty_like(img)
+                    step(img, new, pred, None)
+                    yield {"sample": new, "pred_xstart": pred}
+                    img = new
+                return
+            # ping-pong state buffers; the first step runs eagerly (warms every
+            # lazily-built piece: workspace, packed weights, kernel attributes)
+            bufs = [img, th.empty_like(img)]
+            pred = th.empty_like(img)
+            noise = th.empty_like(img)
+            i0 = indices[0]
+            t.fill_(i0)
+            t_model.fill_(self._model_timestep(i0))
+            step(bufs[0], bufs[1], pred, noise)
+            yield {"sample": bufs[1].clone() if fresh_outputs else bufs[1],
+                   "pred_xstart": pred.clone() if fresh_outputs else pred}
+            graphs = []
+            cs = th.cuda.Stream(device=dev)
+            cs.wait_stream(th.cuda.current_stream(dev))
+            for k in (1, 0):    # graph 0: bufs[1] -> bufs[0]; graph 1: bufs[0] -> bufs[1]
+                g = th.cuda.CUDAGraph()
+                with th.cuda.graph(g, stream=cs):
+                    step(bufs[k], bufs[1 - k], pred, noise)
+                graphs.append(g)
+            th.cuda.current_stream(dev).wait_stream(cs)
+            for n, i in enumerate(indices[1:]):
+                t.fill_(i)
+                t_model.fill_(self._model_timestep(i))
+                graphs[n % 2].replay()
+                dst = bufs[0] if n % 2 == 0 else bufs[1]
+                yield {"sample": dst.clone() if fresh_outputs else dst,
+                       "pred_xstart": pred.clone() if fresh_outputs else pred}
 
     # ---- DDIM (i2i by spec; the reference raises NotImplementedError) --------
     def ddim_sample(self, model, x, t, t_cpu=None, t_prev=None, t_prev_cpu=None, clip_denoised=True,

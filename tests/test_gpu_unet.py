@@ -159,6 +159,37 @@ def test_respaced_ddim50_tables_and_loop_runs():
     assert torch.isfinite(out).all()
 
 
+@pytest.mark.parametrize("respacing,dtype", [("", "fp32"), ("ddim10", "bf16")])
+def test_hip_graph_loop_equals_eager_loop(respacing, dtype):
+    """The graph-captured sampling step (one capture, replayed per timestep,
+    noise from torch's graph-safe generator) reproduces the eager loop with
+    the same seed, for the full and a respaced schedule."""
+    from guided_diffusion import script_util
+    args = script_util.run_sh_model_args(num_channels=32, channel_mult="1,2", num_res_blocks=1, num_groups=8,
+                                         diffusion_steps=20, sample_schedule="direct",
+                                         timestep_respacing=respacing)
+    keys = script_util.model_and_diffusion_defaults().keys()
+    model, diffusion = script_util.create_model_and_diffusion(**{k: args[k] for k in keys}, compute_dtype=dtype)
+    model.load_state_dict(ou.random_params(seed=1, **cases.C1_CFG))
+    model.to(DEV)
+    g = torch.Generator().manual_seed(5)
+    cond = torch.rand(1, 24, 16, 16, 16, generator=g).to(DEV)
+    x_T = torch.randn(1, 8, 16, 16, 16, generator=g).to(DEV)
+
+    def run(graph):
+        diffusion.use_hip_graph = graph
+        torch.manual_seed(11)
+        outs = [o["sample"] for o in diffusion.p_sample_loop_progressive(model, x_T.shape, noise=x_T, cond=cond,
+                                                                        progress=False)]
+        return outs
+
+    eager, graph = run(False), run(True)
+    diffusion.use_hip_graph = False
+    assert len(eager) == len(graph) == diffusion.num_timesteps
+    for a, b in zip(eager, graph):
+        assert torch.equal(a, b), rel_err(b, a)
+
+
 def test_training_losses_forward_vs_oracle():
     from guided_diffusion import script_util
     vols = {k: v.to(DEV) for k, v in cases.data.brats_batch(32, seed=4, batch=2).items()}
