@@ -2,6 +2,8 @@
 // Kernels: conv3d_kernels.hpp, instantiated in conv3d_inst_*.hip.
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "conv3d_kernels.hpp"
 
 namespace cwdm {
@@ -63,8 +65,9 @@ int dispatch_brick(const ConvParams& p, const Brick& br, hipStream_t s) {
 // K-split factor: small grids (the U-Net's 32^3 .. 8^3 levels) get split-K so
 // that a launch has ~768 workgroups to spread over 256 CUs.
 inline int pick_ksplit(long long nblk, int total_chunks) {
-  if (nblk >= 512 || total_chunks <= 1) return 1;
-  int S = (int)((768 + nblk - 1) / nblk);
+  static const long long target = [] { const char* e = std::getenv("CWDM_KSPLIT_TARGET"); return e ? std::atoll(e) : 768LL; }();
+  if (nblk >= 512 || nblk >= target || total_chunks <= 1) return 1;
+  int S = (int)((target + nblk - 1) / nblk);
   if (S > total_chunks) S = total_chunks;
   const int per = (total_chunks + S - 1) / S;
   return (total_chunks + per - 1) / per;

@@ -81,14 +81,24 @@ int64_t v4_items(const cwdm_conv3d_desc* d) {
   return d->B * (d->W / 32) * (d->H / 4) * (d->D / 4) * (d->cout / 64);
 }
 
+// work items a launch aims for before it splits K (env CWDM_V4_KSPLIT_TARGET)
+int64_t v4_ksplit_target() {
+  static const int64_t t = [] {
+    const char* e = std::getenv("CWDM_V4_KSPLIT_TARGET");
+    return e ? (int64_t)std::atoll(e) : (int64_t)128;
+  }();
+  return t;
+}
+
 // K split of a grid with fewer tiles than two workgroups per CU (the 32^3
 // level): enough K slices for ~512 work items, at least two chunks per slice
 int v4_ksplit(const cwdm_conv3d_desc* d) {
   const int ck = d->dtype == CWDM_BF16 ? 16 : 8;
   const int nch = (d->a_c0 + d->a_c1) / ck;
   const int64_t nblk = v4_items(d);
-  if (nblk >= 512 || nch < 2) return 1;
-  int S = (int)std::min<int64_t>((512 + nblk - 1) / nblk, nch / 2);
+  const int64_t target = v4_ksplit_target();
+  if (nblk >= target || nch < 2) return 1;
+  int S = (int)std::min<int64_t>((target + nblk - 1) / nblk, nch / 2);
   if (S < 1) S = 1;
   const int per = (nch + S - 1) / S;
   return (nch + per - 1) / per;
@@ -103,7 +113,7 @@ bool v4_eligible(const cwdm_conv3d_desc* d) {
   if (d->res_mode < -1 || d->res_mode > 1) return false;
   if (d->out1 && d->out_c0 % 8) return false;
   const int64_t nblk = v4_items(d);
-  if (nblk * v4_ksplit(d) < 384 && path != 2) return false;  // too few work items even K-split: the brick kernels
+  if (nblk * v4_ksplit(d) < std::min<int64_t>(384, v4_ksplit_target()) && path != 2) return false;  // too few work items even K-split: the brick kernels
   const int esz = d->dtype == CWDM_BF16 ? 2 : 4;
   const int64_t sv = src_voxels(d);
   // the DMA range check works on 32-bit byte offsets per batch

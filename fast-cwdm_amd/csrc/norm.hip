@@ -26,10 +26,20 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restric
     int cc, cs;
     if (c < c0) { src = s0; parts = p0; cc = c; cs = c0; }
     else { src = s1; parts = p1; cc = c - c0; cs = c1; }
-    for (long long pi = threadIdx.x; pi < parts; pi += 256) {
-      const long long idx = (((long long)b * parts + pi) * cs + cc) * 2;
-      s += (double)src[idx];
-      q += (double)src[idx + 1];
+    // (sum, sum^2) pairs of part pi at base[pi * cs]; four parts per thread in
+    // flight per iteration (the loads are independent, the adds are fp64)
+    const float2* base = reinterpret_cast<const float2*>(src) + (long long)b * parts * cs + cc;
+    long long pi = threadIdx.x;
+    for (; pi + 768 < parts; pi += 1024) {
+      const float2 u0 = base[pi * cs], u1 = base[(pi + 256) * cs], u2 = base[(pi + 512) * cs],
+                   u3 = base[(pi + 768) * cs];
+      s += ((double)u0.x + (double)u1.x) + ((double)u2.x + (double)u3.x);
+      q += ((double)u0.y + (double)u1.y) + ((double)u2.y + (double)u3.y);
+    }
+    for (; pi < parts; pi += 256) {
+      const float2 u = base[pi * cs];
+      s += (double)u.x;
+      q += (double)u.y;
     }
   }
   rs[threadIdx.x] = s;
