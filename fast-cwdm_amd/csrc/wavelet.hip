@@ -285,6 +285,53 @@ extern "C" int cwdm_haar_idwt3d(const void* bands, int in_dtype, const int64_t* 
   return CWDM_OK;
 }
 
+// scripts/sample.py:113-135 after p_sample_loop: IDWT(3 * LLL, ...) -> clamp to
+// [0, 1] -> zero where the conditioning t1n volume is 0 -> keep z < keep_z.
+// One subband voxel (its 2x2x2 output block) per thread.
+__global__ void __launch_bounds__(256) sample_finish_kernel(const float* __restrict__ smp, int64_t B, int64_t d,
+                                                           int64_t h, int64_t w, const float* __restrict__ mask,
+                                                           int64_t keep_z, float* __restrict__ out) {
+  const int64_t nvox = d * h * w;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * nvox) return;
+  const int64_t b = idx / nvox, v = idx - b * nvox;
+  const int64_t k = v % w, j = (v / w) % h, i = v / (w * h);
+  float o[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = smp[(b * 8 + q) * nvox + v];
+  o[0] = mr(o[0], 3.0f);
+  float blk[8];
+  haar_inv8(o, blk);
+  const int64_t D = 2 * d, H = 2 * h, W = 2 * w;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int64_t z = 2 * k + c;
+        if (z >= keep_z) continue;
+        const int64_t x = 2 * i + a, y = 2 * j + bb;
+        float r = blk[a * 4 + bb * 2 + c];
+        r = r <= 0.0f ? 0.0f : r;   // sample[sample <= 0] = 0
+        r = r >= 1.0f ? 1.0f : r;   // sample[sample >= 1] = 1
+        if (mask && mask[((b * D + x) * H + y) * W + z] == 0.0f) r = 0.0f;
+        out[((b * D + x) * H + y) * keep_z + z] = r;
+      }
+}
+
+extern "C" int cwdm_sample_finish(const float* sample, int64_t B, int64_t d, int64_t h, int64_t w,
+                                  const float* mask, int64_t keep_z, float* out, cwdm_stream_t stream) {
+  CWDM_REQUIRE(sample && out, CWDM_E_INVALID, "cwdm_sample_finish: null pointer");
+  CWDM_REQUIRE(B > 0 && d > 0 && h > 0 && w > 0 && keep_z > 0 && keep_z <= 2 * w, CWDM_E_SHAPE,
+               "cwdm_sample_finish: bad shape");
+  const int64_t n = B * d * h * w;
+  hipLaunchKernelGGL(sample_finish_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     sample, B, d, h, w, mask, keep_z, out);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
 extern "C" int cwdm_sampler_step(const cwdm_sampler_args* a, cwdm_stream_t stream) {
   CWDM_REQUIRE(a && a->model_out && a->x_t && a->x_prev && a->coef && a->t, CWDM_E_INVALID,
                "cwdm_sampler_step: null pointer");

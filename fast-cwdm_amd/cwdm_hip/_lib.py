@@ -12,6 +12,7 @@ LIB_PATH = os.environ.get("CWDM_LIB", os.path.join(_HERE, "..", "lib", "libcwdm.
 
 CWDM_F32 = 0
 CWDM_BF16 = 1
+CWDM_F64 = 2
 
 E_INVALID, E_SHAPE, E_HIP, E_WORKSPACE, E_INDEX, E_UNSUPPORTED = -1, -2, -3, -4, -5, -6
 
@@ -92,6 +93,11 @@ _PROTOS = {
     "cwdm_haar_idwt3d": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i64), i64, i64, i64, i64, i64, vp,
                                         ctypes.c_int, ctypes.c_int, vp]),
     "cwdm_sampler_step": (ctypes.c_int, [ctypes.POINTER(SamplerArgs), vp]),
+    "cwdm_quantile_workspace_bytes": (i64, []),
+    "cwdm_quantiles": (ctypes.c_int, [vp, ctypes.c_int, i64, ctypes.POINTER(i64), ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_double), vp, vp, i64, vp]),
+    "cwdm_volume_prepare": (ctypes.c_int, [vp, ctypes.c_int, i64, i64, i64, vp, i64, i64, vp, ctypes.c_int, vp]),
+    "cwdm_sample_finish": (ctypes.c_int, [vp, i64, i64, i64, i64, vp, i64, vp, vp]),
     "cwdm_copy3": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i64), vp, ctypes.c_int, ctypes.POINTER(i64),
                                   i64, i64, i64, vp]),
     "cwdm_conv3d_packed_bytes": (i64, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),

@@ -5,11 +5,12 @@ step is a libcwdm kernel.  Inputs must live on a ROCm device -- there is no CPU
 path (``_need_cuda`` raises).
 """
 import ctypes
+import math
 
 import torch
 
 from . import _lib
-from ._lib import CWDM_BF16, CWDM_F32, check, lib, strides
+from ._lib import CWDM_BF16, CWDM_F32, CWDM_F64, check, lib, strides
 
 DT = {torch.float32: CWDM_F32, torch.bfloat16: CWDM_BF16}
 
@@ -100,3 +101,81 @@ def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t,
     a.clip_denoised = 1 if clip_denoised else 0
     a.mean_type = int(mean_type)
     check(lib().cwdm_sampler_step(ctypes.byref(a), _stream()), "sampler_step")
+
+
+# ---- volume I/O either side of the path ----------------
+_VOL_DT = {torch.float64: CWDM_F64, torch.float32: CWDM_F32}
+
+
+def quantile_ranks(n, qs):
+    """numpy 'linear' quantile bookkeeping (numpy/lib/_function_base_impl.py
+    _quantile): virtual index (n - 1) q in float64, its floor and floor + 1
+    (clamped to n - 1) as the two order statistics, gamma = index - floor."""
+    ranks, gammas = [], []
+    for q in qs:
+        q = float(q)
+        if not 0.0 <= q <= 1.0:
+            raise ValueError("Quantiles must be in the range [0, 1]")
+        vi = (n - 1) * q
+        lo = min(int(math.floor(vi)), n - 1)
+        ranks += [lo, min(lo + 1, n - 1)]
+        gammas.append(vi - lo if vi < n - 1 else 0.0)
+    return ranks, gammas
+
+
+def quantiles(x, qs, out=None):
+    """numpy.quantile(x, qs) (default 'linear') of a device fp64/fp32 tensor,
+    as a float64 device tensor of len(qs) <= 2 values."""
+    _need_cuda(x)
+    if x.dtype not in _VOL_DT:
+        raise TypeError("quantiles: float64 or float32 input")
+    x = x.contiguous()
+    qs = list(qs)
+    if not 1 <= len(qs) <= 2:
+        raise ValueError("quantiles: one or two quantiles per call")
+    n = x.numel()
+    if n == 0:
+        raise IndexError("cannot compute quantiles of an empty array")
+    ranks, gammas = quantile_ranks(n, qs)
+    if out is None:
+        out = torch.empty(len(qs), dtype=torch.float64, device=x.device)
+    ws = torch.empty(int(lib().cwdm_quantile_workspace_bytes()), dtype=torch.uint8, device=x.device)
+    rk = (ctypes.c_int64 * len(ranks))(*ranks)
+    gm = (ctypes.c_double * len(gammas))(*gammas)
+    check(lib().cwdm_quantiles(_p(x), _VOL_DT[x.dtype], n, rk, len(ranks), gm, _p(out), _p(ws), ws.numel(),
+                               _stream()), "quantile")
+    return out
+
+
+def volume_prepare(x, lohi, crop=0, out_z=None, out_dtype=torch.float32):
+    """(clip(x, lo, hi) - lo) / (hi - lo) in float64 over x[crop:-crop, crop:-crop, :],
+    zero-padded in z to out_z, cast to out_dtype."""
+    _need_cuda(x, lohi)
+    if x.dim() != 3:
+        raise AssertionError("volume_prepare expects an (X, Y, Z) volume")
+    x = x.contiguous()
+    X, Y, Z = x.shape
+    out_z = Z if out_z is None else out_z
+    out = torch.empty((X - 2 * crop, Y - 2 * crop, out_z), dtype=out_dtype, device=x.device)
+    check(lib().cwdm_volume_prepare(_p(x), _VOL_DT[x.dtype], X, Y, Z, _p(lohi.contiguous()), crop, out_z, _p(out),
+                                    _VOL_DT[out_dtype], _stream()), "volume_prepare")
+    return out
+
+
+def sample_finish(sample, mask=None, keep_z=None):
+    """sample (B, 8, d, h, w) fp32 subbands -> (B, 2d, 2h, keep_z) image:
+    IDWT(3 LLL, ...), clamp to [0, 1], zero where mask == 0, z cropped."""
+    _need_cuda(sample, mask)
+    if sample.dim() != 5 or sample.shape[1] != 8:
+        raise AssertionError("sample_finish expects (B, 8, d, h, w) subbands")
+    s = sample.contiguous().float()
+    B, _, d, h, w = s.shape
+    keep_z = 2 * w if keep_z is None else keep_z
+    m = None
+    if mask is not None:
+        m = mask.contiguous().float()
+        if m.numel() != B * 8 * d * h * w:
+            raise AssertionError("mask must have the image shape (B, 1, 2d, 2h, 2w)")
+    out = torch.empty((B, 2 * d, 2 * h, keep_z), dtype=torch.float32, device=s.device)
+    check(lib().cwdm_sample_finish(_p(s), B, d, h, w, _p(m), keep_z, _p(out), _stream()), "sample_finish")
+    return out

@@ -28,7 +28,7 @@ extern "C" {
 
 typedef struct ihipStream_t* cwdm_stream_t; /* == hipStream_t; NULL = default stream */
 
-enum { CWDM_F32 = 0, CWDM_BF16 = 1 };
+enum { CWDM_F32 = 0, CWDM_BF16 = 1, CWDM_F64 = 2 /* volume front end input only */ };
 
 enum {
   CWDM_OK = 0,
@@ -102,6 +102,37 @@ typedef struct {
   int mean_type;        /* 0 START_X (model predicts x0), 1 EPSILON */
 } cwdm_sampler_args;
 int cwdm_sampler_step(const cwdm_sampler_args* args, cwdm_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Volume I/O either side of the wavelet path.
+ *
+ * cwdm_quantiles: numpy.quantile(x, q) with the default 'linear' method for 1
+ * or 2 quantiles of a device array x (n elements, CWDM_F64 or CWDM_F32,
+ * computed in float64).  The caller passes the order-statistic ranks
+ * (floor((n-1) q), min(that + 1, n - 1)) per quantile and gamma = (n-1) q -
+ * floor((n-1) q), both host-computed exactly as numpy does; out: nranks / 2
+ * doubles on the device.  Exact order statistics by radix select (6 passes).
+ * Replaces the np.quantile calls of clip_and_normalize
+ * (guided_diffusion/bratsloader.py:117).
+ *
+ * cwdm_volume_prepare: out[i][j][k] = k < Z ? (clip(x[i+crop][j+crop][k], lo,
+ * hi) - lo) / (hi - lo) : 0 over (X - 2 crop, Y - 2 crop, out_z), lohi = the
+ * two quantiles on the device; float64 arithmetic, CWDM_F32 or CWDM_F64 out.
+ * Replaces clip_and_normalize (bratsloader.py:116-120) + the zero pad to 160
+ * and the [8:-8, 8:-8] crop of BRATSVolumes.__getitem__ (bratsloader.py:44-50).
+ *
+ * cwdm_sample_finish: sample (B, 8, d, h, w) fp32 subbands -> IDWT(3 LLL, ...)
+ * -> clamp [0, 1] -> 0 where mask (B, 2d, 2h, 2w; NULL = none) == 0 -> out
+ * (B, 2d, 2h, keep_z), z cropped.  Replaces scripts/sample.py:113-135.
+ * ------------------------------------------------------------------------- */
+int64_t cwdm_quantile_workspace_bytes(void);
+int cwdm_quantiles(const void* x, int dtype, int64_t n, const int64_t* ranks /* host [nranks] */, int nranks,
+                   const double* gammas /* host [nranks / 2] */, double* out, void* workspace, int64_t ws_bytes,
+                   cwdm_stream_t stream);
+int cwdm_volume_prepare(const void* x, int dtype, int64_t X, int64_t Y, int64_t Z, const double* lohi,
+                        int64_t crop, int64_t out_z, void* out, int out_dtype, cwdm_stream_t stream);
+int cwdm_sample_finish(const float* sample, int64_t B, int64_t d, int64_t h, int64_t w, const float* mask,
+                       int64_t keep_z, float* out, cwdm_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Strided 3-index copy with dtype conversion, (b, c, v) -> (b, c, v).  Used
