@@ -115,10 +115,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CWDM_BENCH_REHEARSE=1: every rank on cuda:0 with gloo (a 1-GPU rehearsal
+    # of the N-rank code path; the driver's N-GPU runs use RCCL, one GPU per rank)
+    rehearse = os.environ.get("CWDM_BENCH_REHEARSE") == "1"
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if rehearse else "nccl")
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
+
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        tt = torch.tensor([v], dtype=torch.float64, device="cpu" if rehearse else device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt)
 
     model, diffusion = build(args, device)
     n = args.grid
@@ -147,11 +159,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt)
+    elapsed = max_over_ranks(time.perf_counter() - t0)
 
     # roofline of the dominant kernel: per-conv hipEvents over one extra step
     # (an eager step: event records are not part of the captured graph)
@@ -186,10 +194,7 @@ def main():
             if world > 1:
                 dist.barrier()
             rs = time.perf_counter() - t1
-        if world > 1:
-            tt = torch.tensor([rs], device=device, dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            rs = float(tt)
+        rs = max_over_ranks(rs)
         respaced = {"workload": "config4: timestep_respacing ddim50 (50 of 1000 steps), one volume per GPU, "
                                 f"{'HIP-graph-captured' if args.graph else 'eager'} step",
                     "s_per_volume": round(rs, 4), "denoising_steps_per_s": round(world * 50 / rs, 3)}
