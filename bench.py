@@ -161,8 +161,10 @@ def main():
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
 
-    # roofline of the dominant kernel: per-conv hipEvents over one extra step
-    # (an eager step: event records are not part of the captured graph)
+    # roofline of the dominant kernel -- the implicit-GEMM MFMA conv kernels:
+    # hipEvents around each of their launches over one extra (eager) step, on
+    # the stream they run on; GroupNorm pre-passes, split-K finishes and the
+    # sampler are HBM-bound kernels outside this figure
     plan = model.plan
     plan.set_profiling(True)
     loop.close()
@@ -204,7 +206,7 @@ def main():
     traffic = None
     if n == 128 and args.dtype == "bf16" and os.path.exists(TRAFFIC_JSON):
         with open(TRAFFIC_JSON) as fh:
-            traffic = json.load(fh)["hbm_bytes"]
+            traffic = json.load(fh)["mfma_conv_kernels"]["hbm_bytes"]
 
     ms_per_step = 1000.0 * elapsed / args.steps
     value = world * args.steps / elapsed
@@ -233,9 +235,10 @@ def main():
         "mfma_util_whole_step": round(step_flops * (value / world) / 1e12 / peak, 4),
         "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
-                     "traffic_unit": "HBM bytes per step of the conv family (profiles/r01/pmc_traffic.json)",
-                     "kernel": f"conv3d_kernel (all {n_conv} launches of one step; {conv_ms:.2f} ms, "
-                               f"{conv_flops / 1e12:.2f} TFLOP)"},
+                     "traffic_unit": "HBM bytes per step of those launches (2 x FETCH_SIZE + WRITE_SIZE, "
+                                     "profiles/r01/pmc_traffic.json)",
+                     "kernel": f"implicit-GEMM MFMA conv kernels (conv3d_v4 DMA-staged + brick + output head: "
+                               f"{n_conv} launches per step, {conv_ms:.2f} ms, {conv_flops / 1e12:.2f} TFLOP)"},
     }
     if rank == 0 and world == 1 and args.cpu_baseline:
         threads = min(16, os.cpu_count() or 1)

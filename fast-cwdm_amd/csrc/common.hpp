@@ -28,6 +28,28 @@ int fail(int code, const std::string& msg);
 // After a kernel launch: report launch-configuration errors without syncing.
 #define CWDM_LAUNCHED() CWDM_HIP(hipGetLastError())
 
+// ---- per-conv profiling hook (cwdm_unet_set_profiling) --------------------
+// The plan arms it around one conv call; the launch sites of the MFMA conv
+// kernels (DMA-staged, brick/wide, head) record an event pair around their own
+// launch and the algorithmic flops it covers -- so the bench's roofline times
+// exactly those kernels, not the GroupNorm pre-passes or split-K finishes.
+struct ProfHook {
+  hipEvent_t ev[2][2];
+  double flops[2];
+  int n = 0;  // brackets used (<= 2 MFMA kernels per conv call)
+};
+inline thread_local ProfHook* g_prof = nullptr;
+inline void prof_begin(hipStream_t s) {
+  if (g_prof && g_prof->n < 2) (void)hipEventRecord(g_prof->ev[g_prof->n][0], s);
+}
+inline void prof_end(hipStream_t s, double flops) {
+  if (g_prof && g_prof->n < 2) {
+    (void)hipEventRecord(g_prof->ev[g_prof->n][1], s);
+    g_prof->flops[g_prof->n] = flops;
+    ++g_prof->n;
+  }
+}
+
 // ---- bf16 <-> f32 (storage = raw 16 bits) --------------------------------
 typedef unsigned short bf16_t;
 

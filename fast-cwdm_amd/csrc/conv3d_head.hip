@@ -176,7 +176,9 @@ int head_conv_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   p.out = d->out; p.out_f32 = d->out_dtype == CWDM_F32;
   const long long nblk = (long long)p.B * p.tx * p.ty * p.tz;
   CWDM_REQUIRE(nblk < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d head: grid too large");
+  prof_begin(s);
   hipLaunchKernelGGL(head_conv_kernel, dim3((unsigned)nblk), dim3(256), 0, s, p);
+  prof_end(s, 2.0 * p.B * p.D * p.H * p.W * (double)p.cout * 27.0 * p.C);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }

@@ -946,12 +946,19 @@ inline Brick pick_brick(int64_t D, int64_t H, int64_t W) {
   return {8, 8, 4};
 }
 
+// algorithmic flops of one conv launch: 2 x output voxels x cout x K
+inline double conv_flops(const ConvParams& p) {
+  const double K = 27.0 * (p.ac0 + p.ac1) + (p.bw ? (double)(p.bc0 + p.bc1) : 0.0);
+  return 2.0 * p.B * p.D * p.H * p.W * (double)p.cout * K;
+}
+
 template <typename T, int BX, int BY, int BZ, int NF>
 int launch_conv(const ConvParams& p, hipStream_t s) {
   const long long nblk = (long long)p.B * p.tx * p.ty * p.tz * p.nct;
   CWDM_REQUIRE(nblk * p.ksplit < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d: grid too large");
   const dim3 grid((unsigned)(nblk * p.ksplit));
   const bool gn = p.agn != nullptr;
+  prof_begin(s);
   if (p.amode == 0) {
     if (gn) hipLaunchKernelGGL((conv3d_kernel<T, BX, BY, BZ, NF, 0, true>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((conv3d_kernel<T, BX, BY, BZ, NF, 0, false>), grid, dim3(256), 0, s, p);
@@ -962,6 +969,7 @@ int launch_conv(const ConvParams& p, hipStream_t s) {
     if (gn) hipLaunchKernelGGL((conv3d_kernel<T, BX, BY, BZ, NF, 2, true>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((conv3d_kernel<T, BX, BY, BZ, NF, 2, false>), grid, dim3(256), 0, s, p);
   }
+  prof_end(s, conv_flops(p));
   CWDM_LAUNCHED();
   if (p.ksplit > 1) {
     const long long n4 = (long long)p.B * p.D * p.H * p.W * p.cout / 4;
@@ -981,6 +989,7 @@ int launch_wide(const ConvParams& p, hipStream_t s) {
   CWDM_REQUIRE(nblk * p.ksplit < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d: grid too large");
   const dim3 grid((unsigned)(nblk * p.ksplit));
   const bool gn = p.agn != nullptr;
+  prof_begin(s);
   if (p.amode == 0) {
     if (gn) hipLaunchKernelGGL((conv3d_wide_kernel<T, NF, 0, true>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((conv3d_wide_kernel<T, NF, 0, false>), grid, dim3(256), 0, s, p);
@@ -991,6 +1000,7 @@ int launch_wide(const ConvParams& p, hipStream_t s) {
     if (gn) hipLaunchKernelGGL((conv3d_wide_kernel<T, NF, 2, true>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((conv3d_wide_kernel<T, NF, 2, false>), grid, dim3(256), 0, s, p);
   }
+  prof_end(s, conv_flops(p));
   CWDM_LAUNCHED();
   if (p.ksplit > 1) {
     const long long n4 = (long long)p.B * p.D * p.H * p.W * p.cout / 4;

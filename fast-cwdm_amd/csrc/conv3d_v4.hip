@@ -201,6 +201,7 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   static const int stagger_env = [] { const char* e = std::getenv("CWDM_CONV_STAGGER"); return e ? std::atoi(e) : -1; }();
   p.stagger_cycles = nblk > 2LL * ncu ? (stagger_env >= 0 ? stagger_env : (p.nch * 17000 + 12000) / 2) : 0;
   const bool fast = !p.out_f32 && !p.accumulate && !p.out1;
+  prof_begin(s);
   if (d->dtype == CWDM_BF16) {
     if (fast) {
       if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 1, true>), grid, dim3(256), 0, s, p);
@@ -213,6 +214,7 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
     if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<float, 1, false>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((conv3d_v4_kernel<float, 0, false>), grid, dim3(256), 0, s, p);
   }
+  prof_end(s, 2.0 * p.B * p.D * p.H * p.W * (double)p.cout * 27.0 * (c0 + c1));
   CWDM_LAUNCHED();
   if (S > 1) {
     // finish: slice sum over the whole chip, then the per-tile epilogue

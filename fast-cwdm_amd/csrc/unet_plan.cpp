@@ -113,6 +113,7 @@ struct cwdm_unet {
   bool profiling = false;
   std::vector<hipEvent_t> ev;
   std::vector<double> ev_flops;
+  std::vector<cwdm::ProfHook> hooks;  // per conv: the MFMA kernel launches inside it
   int ev_used = 0;
 
   int add_param(const std::string& n, std::vector<int64_t> s) {
@@ -575,16 +576,22 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
     return wb + L.t_off[id];
   };
   int conv_i = 0;
+  struct ProfReset {
+    ~ProfReset() { cwdm::g_prof = nullptr; }  // also on an early error return
+  } prof_reset;
   const int es = esize(u->cfg.dtype);
   (void)es;
   if (u->profiling) {
-    const size_t need = u->convs.size() * 2;
+    const size_t need = u->convs.size() * 4;
     while (u->ev.size() < need) {
       hipEvent_t e;
       CWDM_HIP(hipEventCreate(&e));
       u->ev.push_back(e);
     }
     u->ev_flops.assign(u->convs.size(), 0.0);
+    u->hooks.assign(u->convs.size(), cwdm::ProfHook{});
+    for (size_t i = 0; i < u->convs.size(); ++i)
+      for (int k = 0; k < 4; ++k) u->hooks[i].ev[k >> 1][k & 1] = u->ev[4 * i + k];
     u->ev_used = 0;
   }
   for (const auto& st : u->steps) {
@@ -629,7 +636,7 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
     if (cs.out < 0) { d.out = out; d.out_dtype = CWDM_F32; }
     else { d.out = wb + L.t_off[cs.out]; d.out_dtype = u->cfg.dtype; }
     d.stats = (cs.stats && cs.out >= 0) ? reinterpret_cast<float*>(wb + L.s_off[cs.out]) : nullptr;
-    if (u->profiling) CWDM_HIP(hipEventRecord(u->ev[2 * conv_i], s));
+    if (u->profiling) cwdm::g_prof = &u->hooks[conv_i];
     if (L.skip_fused[st.idx]) {
       // conv1 of a skip block: SiLU(GN1(x)) for this conv and W_skip . x for conv2 in one pass
       const auto& c2 = u->convs[cs.skip_conv];
@@ -649,8 +656,7 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
       if ((rc = cwdm_conv3d_forward(&d, stream))) return rc;
     }
     if (u->profiling) {
-      CWDM_HIP(hipEventRecord(u->ev[2 * conv_i + 1], s));
-      u->ev_flops[conv_i] = 2.0 * B * d.D * d.H * d.W * cs.cout * (27.0 * cs.cin_a + cs.cin_b);
+      cwdm::g_prof = nullptr;
       u->ev_used = conv_i + 1;
     }
     ++conv_i;
@@ -680,15 +686,20 @@ extern "C" int cwdm_unet_set_profiling(cwdm_unet* u, int on) {
 extern "C" int cwdm_unet_profile_read(cwdm_unet* u, double* ms, double* flops, int* n) {
   CWDM_REQUIRE(u, CWDM_E_INVALID, "cwdm_unet_profile_read: null plan");
   double tot = 0, fl = 0;
+  int launches = 0;
   for (int i = 0; i < u->ev_used; ++i) {
-    float m = 0;
-    CWDM_HIP(hipEventElapsedTime(&m, u->ev[2 * i], u->ev[2 * i + 1]));
-    tot += m;
-    fl += u->ev_flops[i];
+    const cwdm::ProfHook& h = u->hooks[i];
+    for (int k = 0; k < h.n; ++k) {
+      float m = 0;
+      CWDM_HIP(hipEventElapsedTime(&m, h.ev[k][0], h.ev[k][1]));
+      tot += m;
+      fl += h.flops[k];
+      ++launches;
+    }
   }
   if (ms) *ms = tot;
   if (flops) *flops = fl;
-  if (n) *n = u->ev_used;
+  if (n) *n = launches;
   return CWDM_OK;
 }
 

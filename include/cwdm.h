@@ -361,6 +361,8 @@ double cwdm_unet_flops(const cwdm_unet* plan, int64_t B, int64_t D, int64_t H, i
 /* Optional per-conv hipEvent timing (profiling only; adds events to the stream). */
 int cwdm_unet_set_profiling(cwdm_unet* plan, int on);
 int cwdm_unet_profile_read(cwdm_unet* plan, double* conv_ms, double* conv_flops, int* launches);
+/* (with profiling on, each conv call brackets only its MFMA conv kernel launches -- DMA-staged,
+ * brick/wide, output head -- with HIP events; conv_ms / conv_flops / launches sum over those) */
 
 #ifdef __cplusplus
 }

@@ -58,7 +58,11 @@ def main():
         e[0] += 1
         e[1] += rb
         e[2] += wb
+    mfma = ("conv3d_v4_kernel", "conv3d_kernel", "conv3d_wide_kernel", "head_conv_kernel")
+    mk = {k: v for k, v in per.items() if k in mfma}
     res = {"scope": "conv family of one 128^3 bf16 denoising step (bench.py)", "launches": n,
+           "mfma_conv_kernels": {"kernels": sorted(mk), "launches": sum(v[0] for v in mk.values()),
+                                 "hbm_bytes": sum(v[1] + v[2] for v in mk.values())},
            "read_bytes": tot_r, "write_bytes": tot_w, "hbm_bytes": tot_r + tot_w,
            "correction": "read = 2 x FETCH_SIZE(KB) x 1024; write = WRITE_SIZE(KB) x 1024 (MI355X_MICROARCH.md)",
            "per_kernel": {k: {"launches": v[0], "read_bytes": v[1], "write_bytes": v[2]} for k, v in per.items()}}
