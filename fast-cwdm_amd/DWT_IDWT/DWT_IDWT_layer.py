@@ -43,3 +43,32 @@ class IDWT_3D(Module):
         self.input_height = LLL.size()[-2] + HHH.size()[-2]
         self.input_width = LLL.size()[-1] + HHH.size()[-1]
         return IDWTFunction_3D.apply(LLL, LLH, LHL, LHH, HLL, HLH, HHL, HHH)
+
+
+class DWT_3D_Multilevel(Module):
+    """J-level Haar analysis for the multi-level wavelet diffusion of BASELINE
+    config 5 (no reference module: README.md:3-9 names it).
+    forward(x) -> [LLL_J, {LLH..HHH} level J, ..., level 1] (pywt.wavedecn
+    order and semantics, band letters in (D, H, W) order)."""
+
+    def __init__(self, wavename, level=2):
+        super().__init__()
+        _check_wavelet(wavename)
+        self.wavename, self.level = wavename, level
+
+    def forward(self, input):
+        from cwdm_hip import ops
+        return ops.wavedec3(input, self.level)
+
+
+class IDWT_3D_Multilevel(Module):
+    """Inverse of DWT_3D_Multilevel (pywt.waverecn)."""
+
+    def __init__(self, wavename):
+        super().__init__()
+        _check_wavelet(wavename)
+        self.wavename = wavename
+
+    def forward(self, coeffs):
+        from cwdm_hip import ops
+        return ops.waverec3(coeffs)

@@ -103,6 +103,44 @@ def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t,
     check(lib().cwdm_sampler_step(ctypes.byref(a), _stream()), "sampler_step")
 
 
+# ---- multi-level Haar (BASELINE config 5) ---------------
+HIGH_BANDS = ("LLH", "LHL", "LHH", "HLL", "HLH", "HHL", "HHH")
+
+
+def wavedec3(x, level):
+    """J-level 3D Haar analysis (pywt.wavedecn(x, 'haar', level=J) with the
+    reference's single-level kernel applied to the LLL band J times): returns
+    [LLL_J, {band: tensor} of level J, ..., of level 1], every tensor
+    (B, C, D / 2^j, H / 2^j, W / 2^j) fp32, band letters in (D, H, W) order."""
+    _need_cuda(x)
+    if x.dim() != 5:
+        raise AssertionError("wavedec3 expects a 5-D (N, C, D, H, W) tensor")
+    if level < 1:
+        raise ValueError("level must be >= 1")
+    for s in x.shape[2:]:
+        if s % (1 << level):
+            raise AssertionError(f"every spatial size must be divisible by 2^level = {1 << level}")
+    details = []
+    cur = x.contiguous().float()
+    for _ in range(level):
+        b = dwt3d(cur)
+        details.append({k: b[1 + i] for i, k in enumerate(HIGH_BANDS)})
+        cur = b[0].contiguous()
+    return [cur] + details[::-1]
+
+
+def waverec3(coeffs):
+    """Inverse of wavedec3 (pywt.waverecn)."""
+    cur = coeffs[0]
+    _need_cuda(cur)
+    for d in coeffs[1:]:
+        B, C, h0, h1, h2 = cur.shape
+        bands = torch.stack([cur.contiguous()] + [d[k].contiguous() for k in HIGH_BANDS])  # (8, B, C, d, h, w)
+        v = h0 * h1 * h2
+        cur = idwt3d(bands, (B * C * v, C * v, v, 1), B, C, h0, h1, h2)
+    return cur
+
+
 # ---- volume I/O either side of the path (SURVEY.md §8(f) f3) ----------------
 _VOL_DT = {torch.float64: CWDM_F64, torch.float32: CWDM_F32}
 

@@ -100,3 +100,21 @@ def test_matrix_form_depth_quirk():
 def test_odd_sizes_rejected():
     with pytest.raises(AssertionError):
         haar.dwt3d(torch.rand(1, 1, 3, 4, 4))
+
+
+def test_oracle_two_level_matches_pywt_wavedecn_golden():
+    """The oracle's single-level restatement applied twice to the LLL band is
+    pywt.wavedecn(level=2) (the multi-level DWT of BASELINE config 5)."""
+    import os
+    import numpy as np
+    from conftest import GOLDEN
+    from oracle import haar as oh
+    g = np.load(os.path.join(GOLDEN, "pywt_haar3d_wavedec2.npz"), allow_pickle=False)
+    for n in range(3):
+        x = torch.from_numpy(g[f"x{n}"]).view(1, 1, *g[f"x{n}"].shape)
+        b1 = oh.dwt3d(x)
+        b2 = oh.dwt3d(b1[0])
+        assert np.allclose(b2[0].numpy()[0, 0], g[f"x{n}_L2_LLL"], atol=1e-12)
+        for i, b in enumerate(("LLH", "LHL", "LHH", "HLL", "HLH", "HHL", "HHH")):
+            assert np.allclose(b1[1 + i].numpy()[0, 0], g[f"x{n}_L1_{b}"], atol=1e-12)
+            assert np.allclose(b2[1 + i].numpy()[0, 0], g[f"x{n}_L2_{b}"], atol=1e-12)
