@@ -198,7 +198,9 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   }();
   const dim3 grid((unsigned)std::min<long long>(nblk, 2LL * ncu));
   // half a tile: ~17k cycles per chunk and ~12k for the epilogue when shared (tools/conv_stamps.py)
-  static const int stagger_env = [] { const char* e = std::getenv("CWDM_CONV_STAGGER"); return e ? std::atoi(e) : -1; }();
+  // CWDM_CONV_STAGGER=-1 restores the half-tile delay; measured (r01 v7 kernel,
+  // bench.py A/B on one MI355X): no delay 57.15 vs half-tile 56.80 steps/s
+  static const int stagger_env = [] { const char* e = std::getenv("CWDM_CONV_STAGGER"); return e ? std::atoi(e) : 0; }();
   p.stagger_cycles = nblk > 2LL * ncu ? (stagger_env >= 0 ? stagger_env : (p.nch * 17000 + 12000) / 2) : 0;
   const bool fast = !p.out_f32 && !p.accumulate && !p.out1;
   prof_begin(s);
