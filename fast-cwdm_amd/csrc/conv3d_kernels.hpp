@@ -677,6 +677,31 @@ __global__ void __launch_bounds__(256) conv3d_reduce_kernel(ConvParams p, int S)
   const int cg = tid % CG;
   const int cbase = ct * NT + cg * 8;
   const int nvalid = min(8, p.cout - cbase);
+  if (S == 1 && ct * NT + NT <= p.cout) {  // workgroup-uniform: the whole channel tile is valid
+    // pre-summed slice: every row's loads in flight at once (fully unrolled)
+    constexpr int IT = ROWS * CG / 256;
+    static_assert(ROWS * CG % 256 == 0, "rows per thread");
+    float4 va[IT], vb[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int row = (tid + 256 * k) / CG;
+      const int rx = row % BX, ry = (row / BX) % BY, rz = row / (BX * BY);
+      const int ox = min(x0 + rx, p.W - 1), oy = min(y0 + ry, p.H - 1), oz = min(z0 + rz, p.D - 1);
+      const float* src = p.partial + ((((long long)b * p.D + oz) * p.H + oy) * p.W + ox) * p.cout + cbase;
+      va[k] = *reinterpret_cast<const float4*>(src);
+      vb[k] = *reinterpret_cast<const float4*>(src + 4);
+    }
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int row = (tid + 256 * k) / CG;
+      float* e = E + row * LD + cg * 8;
+      *reinterpret_cast<float4*>(e) = va[k];
+      *reinterpret_cast<float4*>(e + 4) = vb[k];
+    }
+    __syncthreads();
+    epilogue_rows<T, BX, BY, BZ, NF, ROWS>(p, E, b, st, ct, x0, y0, z0, tid);
+    return;
+  }
   for (int u = tid; u < ROWS * CG; u += 256) {
     const int row = u / CG;
     const int rx = row % BX, ry = (row / BX) % BY, rz = row / (BX * BY);
