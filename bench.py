@@ -110,6 +110,9 @@ def main():
     ap.add_argument("--graph", type=int, default=1, help="replay one HIP-graph-captured step per timestep")
     ap.add_argument("--respaced", type=int, default=1,
                     help="also time config 4: a full 50-step respaced (ddim50) volume, graph-captured loop")
+    ap.add_argument("--batched", type=int, default=2,
+                    help="also time B volumes denoised together in one batched step (serving throughput; "
+                         "0 = skip); reported beside, never as, the B=1 metric")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,6 +178,34 @@ def main():
     plan.set_profiling(False)
     step_flops = plan.flops(1, n, n, n)
 
+    # serving side-figure: B volumes per batched step (the 16^3 / 8^3 levels of
+    # a single volume leave the chip idle; a batch fills them)
+    batched = None
+    if args.batched > 1:
+        Bv = args.batched
+        xb = x_T.expand(Bv, -1, -1, -1, -1).contiguous()
+        cb = cond.expand(Bv, -1, -1, -1, -1).contiguous()
+        nb = 6
+        lb = diffusion._native_loop(model, xb, list(range(T))[::-1][:nb + 3], cb, True, graph=bool(args.graph),
+                                    fresh_outputs=False)
+        for _ in range(2):
+            next(lb)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(nb):
+            next(lb)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tb = max_over_ranks(time.perf_counter() - t1)
+        lb.close()
+        batched = {"batch_per_gpu": Bv, "ms_per_batched_step": round(1000 * tb / nb, 3),
+                   "volume_steps_per_s": round(world * Bv * nb / tb, 3)}
+        del xb, cb
+        torch.cuda.empty_cache()
+
     # config 4: respaced 50-step sampling of one whole volume (timestep_respacing
     # "ddim50" = stride-20 subset of the 1000-step schedule), graph-captured loop
     respaced = None
@@ -232,6 +263,7 @@ def main():
         "sampling_wallclock_s_per_volume_1000_steps": round(1000 * ms_per_step / 1000.0, 2),
         "hip_graph": bool(args.graph),
         "respaced_ddim50": respaced,
+        "batched_serving": batched,
         "mfma_util_whole_step": round(step_flops * (value / world) / 1e12 / peak, 4),
         "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
