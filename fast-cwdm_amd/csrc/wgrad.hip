@@ -62,9 +62,13 @@ __device__ __forceinline__ v4s tr_read(const unsigned char* lds) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(lds));
 }
 
+// two transposed 64-bit reads -> one 8 x bf16 operand, as whole dwords (an
+// element-wise shuffle of the 16-bit lanes made the compiler repack every
+// dword with v_lshrrev + v_perm: 48 VALU per K-step)
 __device__ __forceinline__ bf16x8 join(v4s a, v4s b) {
-  typedef short v8s __attribute__((ext_vector_type(8)));
-  v8s r = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 lo = __builtin_bit_cast(u32x2, a), hi = __builtin_bit_cast(u32x2, b);
+  const u32x4 r = {lo.x, lo.y, hi.x, hi.y};
   return __builtin_bit_cast(bf16x8, r);
 }
 
@@ -187,12 +191,13 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradParams p) {
           a[m] = join(lo, hi);
         }
         const int hrow = (z * WHY + y) * WHX + 8 * h + q;
+        // every wave reads NT fragments (a wave with 6 taps reads a valid
+        // dummy 7th, toff = tap 0, and skips its MFMAs): no divergent phi on
+        // the operand registers
 #pragma unroll
         for (int k = 0; k < NT; ++k) {
-          if (k < ntap) {
-            const unsigned char* bp = bimg + (hrow + toff[k]) * 32;
-            bfr[k] = join(tr_read(bp), tr_read(bp + 4 * 32));
-          }
+          const unsigned char* bp = bimg + (hrow + toff[k]) * 32;
+          bfr[k] = join(tr_read(bp), tr_read(bp + 4 * 32));
         }
       };
       // software pipeline: K-step s+1's LDS reads are in flight during K-step s's MFMAs
@@ -200,21 +205,37 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradParams p) {
       auto mfmas = [&](const bf16x8* a, const bf16x8* bfr) {
 #pragma unroll
         for (int k = 0; k < NT; ++k) {
-          if (k < ntap) {
+          if (k + 1 < NT || k < ntap) {
 #pragma unroll
             for (int m = 0; m < MC; ++m)
               acc[k][m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m], bfr[k], acc[k][m], 0, 0, 0);
           }
         }
       };
+      // the next K-step's transposed reads interleaved with this step's MFMAs
+      // (2 reads per MFMA pair): at most 15 LDS reads may be tracked by
+      // lgkmcnt, so a block of 18 reads ahead of the MFMAs made every step wait
+      auto interleave = [&]() {
+#pragma unroll
+        for (int r = 0; r < (2 * MC + 2 * NT + 1) / 2; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        }
+      };
       load_frags(s0, fa0, fb0);
 #pragma unroll 1
-      for (int i = 0; i < NS; i += 2) {
+      for (int i = 0; i < NS - 2; i += 2) {
         load_frags(s0 + i + 1, fa1, fb1);
         mfmas(fa0, fb0);
-        if (i + 2 < NS) load_frags(s0 + i + 2, fa0, fb0);
+        interleave();
+        load_frags(s0 + i + 2, fa0, fb0);
         mfmas(fa1, fb1);
+        interleave();
       }
+      load_frags(s0 + NS - 1, fa1, fb1);
+      mfmas(fa0, fb0);
+      interleave();
+      mfmas(fa1, fb1);
     } else {
       const int col = lane & 31, hh = lane >> 5;
       const int s_begin = TAPS == 27 ? 0 : 32 * wv, s_end = TAPS == 27 ? 128 : 32 * wv + 32;
