@@ -20,43 +20,65 @@ template __global__ void conv3d_v4_kernel<float, 1, false>(V4Params);
 
 namespace {
 
-// one thread per (voxel, 8-channel group): out[v][c] = SiLU(x[v][c] * sc[b][c] + sh[b][c])
+// out[v][c] = SiLU(x[v][c] * sc[b][c] + sh[b][c]); a thread handles one
+// 8-channel group of VPT voxels a quarter of the volume apart (each load /
+// store instruction still covers consecutive voxels across the lanes), so
+// VPT loads are in flight together and the scale/shift reload only when the
+// batch index changes.
 // cm: write the chunk-major layout [B][C / CK][V][CK] the DMA-staged conv reads
 // as contiguous halo rows (CK = 16 bf16 / 8 fp32 channels = 32 bytes per voxel)
-template <typename T>
+template <typename T, int VPT>
 __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x0, int c0, const T* __restrict__ x1,
                                                       int c1, const float* __restrict__ gn, long long vpb,
                                                       long long n8, T* __restrict__ out, int cm) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n8) return;
   const int C = c0 + c1, G8 = C >> 3;
-  const int g = (int)(i % G8);
-  const long long v = i / G8;
-  const long long b = v / vpb;
+  const long long nvox = n8 / G8;
+  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // (voxel slot, group)
+  const int g = (int)(i0 % G8);
+  const long long vq = i0 / G8, nq = (nvox + VPT - 1) / VPT;   // voxels vq, vq + nq, ...
+  if (vq >= nq) return;
   const int c = g * 8;
-  const T* src = c < c0 ? x0 + v * c0 + c : x1 + v * c1 + (c - c0);
-  float xv[8];
-  if constexpr (sizeof(T) == 2) {
-    unpack<bf16_t>(*reinterpret_cast<const u32x4*>(src), xv);
-  } else {
-    unpack<float>(*reinterpret_cast<const u32x4*>(src), xv);
-    unpack<float>(*reinterpret_cast<const u32x4*>(src + 4), xv + 4);
-  }
-  const float4* g4 = reinterpret_cast<const float4*>(gn + (b * C + c) * 2);
-  float y[8];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float4 s = g4[e];  // (sc, sh) of channels c + 2e, c + 2e + 1
-    y[2 * e] = silu(xv[2 * e] * s.x + s.y);
-    y[2 * e + 1] = silu(xv[2 * e + 1] * s.z + s.w);
-  }
   constexpr int CK = 32 / sizeof(T);
-  T* dst = cm ? out + ((b * (C / CK) + c / CK) * vpb + (v - b * vpb)) * CK + (c % CK) : out + v * C + c;
-  if constexpr (sizeof(T) == 2) {
-    *reinterpret_cast<u32x4*>(dst) = pack<bf16_t>(y);
-  } else {
-    *reinterpret_cast<u32x4*>(dst) = pack<float>(y);
-    *reinterpret_cast<u32x4*>(dst + 4) = pack<float>(y + 4);
+  float xv[VPT][8];
+  long long vs[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const long long v = vq + k * nq < nvox ? vq + k * nq : nvox - 1;
+    vs[k] = v;
+    const T* src = c < c0 ? x0 + v * c0 + c : x1 + v * c1 + (c - c0);
+    if constexpr (sizeof(T) == 2) {
+      unpack<bf16_t>(*reinterpret_cast<const u32x4*>(src), xv[k]);
+    } else {
+      unpack<float>(*reinterpret_cast<const u32x4*>(src), xv[k]);
+      unpack<float>(*reinterpret_cast<const u32x4*>(src + 4), xv[k] + 4);
+    }
+  }
+  long long bprev = -1;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    if (vq + k * nq >= nvox) break;
+    const long long v = vs[k];
+    const long long b = v / vpb;
+    if (b != bprev) {
+      const float4* g4 = reinterpret_cast<const float4*>(gn + (b * C + c) * 2);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float4 t = g4[e];  // (sc, sh) of channels c + 2e, c + 2e + 1
+        sc[2 * e] = t.x; sh[2 * e] = t.y; sc[2 * e + 1] = t.z; sh[2 * e + 1] = t.w;
+      }
+      bprev = b;
+    }
+    float y[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) y[e] = silu(xv[k][e] * sc[e] + sh[e]);
+    T* dst = cm ? out + ((b * (C / CK) + c / CK) * vpb + (v - b * vpb)) * CK + (c % CK) : out + v * C + c;
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<u32x4*>(dst) = pack<bf16_t>(y);
+    } else {
+      *reinterpret_cast<u32x4*>(dst) = pack<float>(y);
+      *reinterpret_cast<u32x4*>(dst + 4) = pack<float>(y + 4);
+    }
   }
 }
 
@@ -136,14 +158,16 @@ int legacy_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream);
 
 int gn_apply(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
              void* out, hipStream_t s, int cm = 0) {
-  const int64_t n8 = B * vpb * ((c0 + c1) / 8);
-  const dim3 grid((unsigned)ceil_div(n8, 256));
+  constexpr int VPT = 4;
+  const int G8 = (c0 + c1) / 8;
+  const int64_t n8 = B * vpb * G8;
+  const dim3 grid((unsigned)ceil_div(ceil_div(B * vpb, VPT) * G8, 256));
   if (dtype == CWDM_BF16)
-    hipLaunchKernelGGL(gn_apply_kernel<bf16_t>, grid, dim3(256), 0, s, reinterpret_cast<const bf16_t*>(x0), c0,
+    hipLaunchKernelGGL((gn_apply_kernel<bf16_t, VPT>), grid, dim3(256), 0, s, reinterpret_cast<const bf16_t*>(x0), c0,
                        reinterpret_cast<const bf16_t*>(x1), c1, gn, (long long)vpb, (long long)n8,
                        reinterpret_cast<bf16_t*>(out), cm);
   else
-    hipLaunchKernelGGL(gn_apply_kernel<float>, grid, dim3(256), 0, s, reinterpret_cast<const float*>(x0), c0,
+    hipLaunchKernelGGL((gn_apply_kernel<float, VPT>), grid, dim3(256), 0, s, reinterpret_cast<const float*>(x0), c0,
                        reinterpret_cast<const float*>(x1), c1, gn, (long long)vpb, (long long)n8,
                        reinterpret_cast<float*>(out), cm);
   CWDM_LAUNCHED();
