@@ -220,7 +220,9 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
       return 256;
     return n > 0 ? n : 256;
   }();
-  const dim3 grid((unsigned)std::min<long long>(nblk, 2LL * ncu));
+  // workgroups per CU slot of the persistent grid (env CWDM_V4_GRID_MULT, A/B knob)
+  static const long long gmul = [] { const char* e = std::getenv("CWDM_V4_GRID_MULT"); return e ? std::atoll(e) : 4LL; }();
+  const dim3 grid((unsigned)std::min<long long>(nblk, gmul * ncu));
   // half a tile: ~17k cycles per chunk and ~12k for the epilogue when shared (tools/conv_stamps.py)
   // CWDM_CONV_STAGGER=-1 restores the half-tile delay; measured (r01 v7 kernel,
   // bench.py A/B on one MI355X): no delay 57.15 vs half-tile 56.80 steps/s
@@ -442,7 +444,8 @@ int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* g
   p.act = act; p.ws = reinterpret_cast<const unsigned char*>(wskip); p.cout = cout; p.skip = skip;
   const int64_t lds = apply_skip_lds_bytes(dtype, c0 + c1, cout, B);
   const int64_t nblocks = p.nvox / 128;
-  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(nblocks, 1024)));
+  static const int64_t cap = [] { const char* e = std::getenv("CWDM_SKIP_GRID"); return e ? (int64_t)std::atoll(e) : (int64_t)512; }();
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(nblocks, cap)));
   auto go = [&](auto kern) -> int {
     CWDM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(kern, grid, dim3(256), (unsigned)lds, s, p);
