@@ -25,7 +25,9 @@ def main():
     spec = conv_bench.CASES[case]
     n, cout = spec[0], spec[3]
     nblk = (n // 32) * (n // 4) * (n // 4) * (cout // 64)
-    nblk = min(nblk, 2 * torch.cuda.get_device_properties(0).multi_processor_count)  # persistent grid
+    # persistent grid: CWDM_V4_GRID_MULT (default 4) workgroups per CU (conv3d_v4.hip)
+    mult = int(os.environ.get("CWDM_V4_GRID_MULT", "4"))
+    nblk = min(nblk, mult * torch.cuda.get_device_properties(0).multi_processor_count)
     buf = torch.zeros(nblk * 24, dtype=torch.int64, device="cuda")
     conv_bench.run_case(case, spec, 3, 1)  # warm
     lib().cwdm_debug_conv_stamps(ctypes.c_void_p(buf.data_ptr()))
