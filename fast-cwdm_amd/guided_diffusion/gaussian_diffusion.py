@@ -120,7 +120,7 @@ class GaussianDiffusion:
         self._dev_cache = {}
 
     # capture the native sampling step in a HIP graph (see _native_loop)
-    use_hip_graph = False
+    use_hip_graph = True
 
     # ---- tables -------------------------------------------------------------
     def _fixed_variance(self):

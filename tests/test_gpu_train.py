@@ -424,3 +424,6 @@ def test_trainloop_runs_and_learns(tmp_path, monkeypatch):
     assert os.path.exists(os.path.join(tmp_path, "checkpoints", "brats_t1n_BEST_direct_1000.pt"))
     sd = torch.load(os.path.join(tmp_path, "checkpoints", "brats_t1n_BEST_direct_1000.pt"), weights_only=True)
     assert set(sd) == set(P)
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.destroy_process_group()
