@@ -15,5 +15,11 @@ int fail(int code, const std::string& msg) {
 const char* last_error() { return g_err.c_str(); }
 }  // namespace cwdm
 
-extern "C" int cwdm_version(void) { return 1000; }  // 0.1.0
+#ifndef CWDM_SRC_HASH
+#define CWDM_SRC_HASH "unknown"
+#endif
+
+extern "C" int cwdm_version(void) { return 2000; }  // 0.2.0
+// sha256 prefix of the sources this library was built from (cwdm_hip/srchash.py)
+extern "C" const char* cwdm_build_id(void) { return CWDM_SRC_HASH; }
 extern "C" const char* cwdm_last_error(void) { return cwdm::last_error(); }

@@ -205,13 +205,29 @@ __global__ void __launch_bounds__(256) sampler_kernel(cwdm_sampler_args a, S3 mo
 #pragma unroll
     for (int q = 0; q < 8; ++q) pred[q] = m[q];
   }
-  const bool noisy = (t != 0) && a.noise;
   float r[8];
+  if (a.update == 1) {
+    // DDIM (ddim_sample, gaussian_diffusion.py:753-784): eps from x_t and the
+    // projected x0 (_predict_eps_from_xstart, :407-415), then
+    // x0 * sqrt(acp_prev) + sqrt(1 - acp_prev - sigma^2) * eps, returned
+    // without noise like the reference (:784); cf[5], cf[6] hold the two roots
+    const float c3 = cf[3], c4 = cf[4], c5 = cf[5], c6 = cf[6];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float eps = __fdiv_rn(sb(mr(c3, xv[q]), pred[q]), c4);
+      r[q] = ad(mr(pred[q], c5), mr(c6, eps));
+    }
+  } else {
+    const bool noisy = (t != 0) && a.noise;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float mean = ad(mr(c1, pred[q]), mr(c2, xv[q]));
+      r[q] = mean;
+      if (noisy) r[q] = ad(mean, mr(sg, a.noise[b * nz.b + q * nz.c + v * nz.v]));
+    }
+  }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    float mean = ad(mr(c1, pred[q]), mr(c2, xv[q]));
-    r[q] = mean;
-    if (noisy) r[q] = ad(mean, mr(sg, a.noise[b * nz.b + q * nz.c + v * nz.v]));
     a.x_prev[b * xp.b + q * xp.c + v * xp.v] = r[q];
     if (a.pred_xstart) a.pred_xstart[b * px.b + q * px.c + v * px.v] = pred[q];
   }

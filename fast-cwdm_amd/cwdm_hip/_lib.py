@@ -34,6 +34,7 @@ class SamplerArgs(ctypes.Structure):
         ("T", i64), ("B", i64), ("d", i64), ("h", i64), ("w", i64),
         ("clip_denoised", ctypes.c_int),
         ("mean_type", ctypes.c_int),
+        ("update", ctypes.c_int),
     ]
 
 
@@ -88,6 +89,7 @@ class UNetConfig(ctypes.Structure):
 _PROTOS = {
     "cwdm_version": (ctypes.c_int, []),
     "cwdm_last_error": (ctypes.c_char_p, []),
+    "cwdm_build_id": (ctypes.c_char_p, []),
     "cwdm_haar_dwt3d": (ctypes.c_int, [vp, i64, i64, i64, i64, i64, vp, ctypes.c_int, ctypes.POINTER(i64),
                                        ctypes.c_int, vp]),
     "cwdm_haar_idwt3d": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i64), i64, i64, i64, i64, i64, vp,
@@ -171,8 +173,21 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        check_build_id(L)
         _lib = L
     return _lib
+
+
+def check_build_id(L):
+    """Refuse a library built from other sources than the tree's (the .so is
+    untracked and travels to the GPU box as a file; CWDM_ALLOW_STALE_LIB=1
+    skips the check for kernel experiments)."""
+    from .srchash import source_hash
+    built = L.cwdm_build_id().decode()
+    want = source_hash()
+    if built != want and os.environ.get("CWDM_ALLOW_STALE_LIB") != "1":
+        raise OSError(f"{LIB_PATH} was built from sources {built}, the tree has {want}: "
+                      f"rebuild with `make -C fast-cwdm_amd/csrc`")
 
 
 def check(rc, what=""):

@@ -64,3 +64,4 @@ def broadcast_params(params, src=0, group=None):
     with torch.no_grad():
         for p in params:
             dist.broadcast(p.data, src, group=group)
+            torch.autograd.graph.increment_version(p)

@@ -82,8 +82,9 @@ def ndhwc_strides(B, C, V, c_total=None):
 
 def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t, T, B, d, h, w,
                  clip_denoised=True, pred_xstart=None, px_s=(0, 0, 0), mirror=None, mr_s=(0, 0, 0),
-                 mean_type=0):
-    """Fused process_xstart + posterior mean + noise (cwdm_sampler_step)."""
+                 mean_type=0, update=0):
+    """Fused process_xstart + posterior mean + noise (cwdm_sampler_step);
+    update=1: the DDIM step instead of the posterior mean + noise."""
     _need_cuda(model_out, x_t, x_prev, noise, coef, t, pred_xstart, mirror)
     a = _lib.SamplerArgs()
     a.model_out, a.mo_s = model_out.data_ptr(), _lib.I64x3(*mo_s)
@@ -100,6 +101,7 @@ def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t,
     a.T, a.B, a.d, a.h, a.w = T, B, d, h, w
     a.clip_denoised = 1 if clip_denoised else 0
     a.mean_type = int(mean_type)
+    a.update = int(update)
     check(lib().cwdm_sampler_step(ctypes.byref(a), _stream()), "sampler_step")
 
 

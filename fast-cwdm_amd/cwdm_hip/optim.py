@@ -57,9 +57,11 @@ class FlatAdamW(torch.optim.Optimizer):
         check(lib().cwdm_adamw(self._flat.data_ptr(), g.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
                                self._flat.numel(), float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
                                float(grp["weight_decay"]), self._step, _stream()), "AdamW.step")
-        # the kernel wrote through raw pointers: bump the shared version counter so
-        # the model re-packs its kernel-layout weights
+        # the kernel wrote through raw pointers: the model must re-pack its
+        # kernel-layout weights (the parameters' own version counters do not
+        # see writes to the flat buffer)
         torch.autograd.graph.increment_version(self._flat)
+        self._model.mark_params_changed()
         for st in self.state.values():
             st["step"].fill_(float(self._step))
         return loss

@@ -46,10 +46,29 @@ def finish_sample(sample, cond_1=None, keep_z=155):
     return ops.sample_finish(sample, cond_1, keep_z)
 
 
+def _prepare_modality_host(img, pad_z=160, crop=8):
+    """prepare_modality for DataLoader worker processes, which cannot own a HIP
+    context: the reference's own numpy arithmetic (bratsloader.py:40-50,
+    116-120) on the host.  Data plumbing either side of the hot path, never
+    the sampling/training step itself."""
+    import numpy as np
+    a = np.asarray(img, dtype=np.float64)
+    c = np.clip(a, np.quantile(a, 0.001), np.quantile(a, 0.999))
+    c = (c - np.min(c)) / (np.max(c) - np.min(c))
+    X, Y, Z = a.shape
+    out = torch.zeros(1, X, Y, pad_z)
+    out[:, :, :, :Z] = torch.tensor(c)
+    return out[:, crop:X - crop, crop:Y - crop, :].contiguous()
+
+
 class BRATSVolumes(torch.utils.data.Dataset):
     """Same directory walk and item dict as the reference (bratsloader.py:9-113);
-    decoding needs nibabel (not part of this image), normalisation runs on
-    ``device`` through prepare_modality."""
+    decoding needs nibabel (not part of this image).  In the main process the
+    normalisation runs on ``device`` through prepare_modality; inside a
+    DataLoader worker (the reference scripts use num_workers=12, and a forked
+    worker cannot initialise the GPU) it runs the reference's numpy arithmetic
+    on the host and returns CPU tensors, which the caller moves with
+    ``.to(dev)`` exactly as the reference scripts do."""
 
     def __init__(self, directory, mode="train", gen_type=None, device="cuda"):
         super().__init__()
@@ -77,10 +96,14 @@ class BRATSVolumes(torch.utils.data.Dataset):
         filedict = self.database[x]
         missing = "none"
         out = {}
+        in_worker = torch.utils.data.get_worker_info() is not None
         for key in ("t1n", "t1c", "t2w", "t2f"):
             if key in filedict:
-                vol = torch.from_numpy(nibabel.load(filedict[key]).get_fdata()).to(self.device)
-                out[key] = prepare_modality(vol)
+                arr = nibabel.load(filedict[key]).get_fdata()
+                if in_worker or not str(self.device).startswith("cuda"):
+                    out[key] = _prepare_modality_host(arr)
+                else:
+                    out[key] = prepare_modality(torch.from_numpy(arr).to(self.device))
             else:
                 missing = key
                 out[key] = torch.zeros(1)

@@ -75,9 +75,12 @@ def load_state_dict(path, **kwargs):
 
 
 def sync_params(params):
-    """Broadcast rank 0's parameters to every rank."""
+    """Broadcast rank 0's parameters to every rank (in place; each parameter's
+    version counter is bumped so caches keyed on it -- the native UNetModel's
+    packed weights -- see the new values)."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return
     with th.no_grad():
         for p in params:
             dist.broadcast(p.data, 0)
+            th.autograd.graph.increment_version(p)

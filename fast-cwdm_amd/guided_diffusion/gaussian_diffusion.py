@@ -131,11 +131,13 @@ class GaussianDiffusion:
             return self.posterior_variance, self.posterior_log_variance_clipped
         raise NotImplementedError(f"{self.model_var_type} (learned variances are not on the fast-cwdm path)")
 
-    def coef_table(self, device):
+    def coef_table(self, device, eta=0.0):
         """[T][8] fp32 device table read by cwdm_sampler_step: coef1, coef2,
         exp(0.5*log_var) (computed like the reference, in fp32 from the fp32
-        log-variance), sqrt(1/acp), sqrt(1/acp-1)."""
-        key = ("coef", str(device), self.model_var_type)
+        log-variance), sqrt(1/acp), sqrt(1/acp-1), and the two DDIM roots
+        sqrt(acp_prev), sqrt(1 - acp_prev - sigma_eta^2) -- evaluated in fp32
+        from the fp32-extracted tables, the order ddim_sample uses (:770-781)."""
+        key = ("coef", str(device), self.model_var_type, float(eta))
         if key not in self._dev_cache:
             _, logv = self._fixed_variance()
             sig = th.exp(0.5 * th.from_numpy(logv).float())
@@ -145,6 +147,11 @@ class GaussianDiffusion:
             tab[:, 2] = sig
             tab[:, 3] = th.from_numpy(self.sqrt_recip_alphas_cumprod).float()
             tab[:, 4] = th.from_numpy(self.sqrt_recipm1_alphas_cumprod).float()
+            ab = th.from_numpy(self.alphas_cumprod).float()
+            abp = th.from_numpy(self.alphas_cumprod_prev).float()
+            sigma = eta * ((1 - abp) / (1 - ab)) ** 0.5 * (1 - ab / abp) ** 0.5
+            tab[:, 5] = abp ** 0.5
+            tab[:, 6] = (1 - abp - sigma ** 2) ** 0.5
             self._dev_cache[key] = tab.to(device)
         return self._dev_cache[key]
 
@@ -206,8 +213,9 @@ class GaussianDiffusion:
         if tmin < 0 or tmax >= self.num_timesteps:
             raise IndexError(f"Timesteps out of bounds: min={tmin}, max={tmax}, arr len={self.num_timesteps}")
 
-    def _epilogue(self, model_output, x, t, clip_denoised, denoised_fn, noise):
-        """cwdm_sampler_step on NCDHW tensors; returns (sample_or_mean, pred_xstart)."""
+    def _epilogue(self, model_output, x, t, clip_denoised, denoised_fn, noise, update=0, eta=0.0):
+        """cwdm_sampler_step on NCDHW tensors; returns (sample_or_mean, pred_xstart)
+        (update=1: (DDIM x_prev, pred_xstart))."""
         B, C = x.shape[:2]
         d, h, w = x.shape[2:]
         if clip_denoised and C != 8:
@@ -224,9 +232,10 @@ class GaussianDiffusion:
         pred = th.empty_like(xt)
         nz = noise.contiguous().float() if noise is not None else None
         s = _ncdhw(xt)
-        ops.sampler_step(mo, s, xt, s, out, s, nz, s if nz is not None else (0, 0, 0), self.coef_table(x.device),
-                         t_dev, self.num_timesteps, B, d, h, w, clip_denoised=clip_denoised, pred_xstart=pred,
-                         px_s=s, mean_type=mean_type)
+        ops.sampler_step(mo, s, xt, s, out, s, nz, s if nz is not None else (0, 0, 0),
+                         self.coef_table(x.device, eta), t_dev, self.num_timesteps, B, d, h, w,
+                         clip_denoised=clip_denoised, pred_xstart=pred, px_s=s, mean_type=mean_type,
+                         update=update)
         return out, pred
 
     def p_mean_variance(self, model, x, t, clip_denoised=True, denoised_fn=None, model_kwargs=None, cond=None):
@@ -276,6 +285,11 @@ class GaussianDiffusion:
                                   noise_fn=None, _reuse_outputs=False):
         """Reference :668-719.  ``noise_fn`` (extension, default ``th.randn_like``)
         supplies each step's noise; parity tests inject fixed noise through it."""
+        yield from self._sample_loop(model, shape, time, noise, clip_denoised, denoised_fn, cond_fn, model_kwargs,
+                                     device, progress, cond, noise_fn, _reuse_outputs, update=0, eta=0.0)
+
+    def _sample_loop(self, model, shape, time, noise, clip_denoised, denoised_fn, cond_fn, model_kwargs, device,
+                     progress, cond, noise_fn, reuse_outputs, update, eta):
         if device is None:
             device = next(model.parameters()).device
         assert isinstance(shape, (tuple, list))
@@ -284,26 +298,46 @@ class GaussianDiffusion:
         if time > self.num_timesteps:
             raise IndexError(f"Timesteps out of bounds: max={time - 1}, arr len={self.num_timesteps}")
         indices = list(range(time))[::-1]
+        bar = None
         if progress:
             try:
                 from tqdm.auto import tqdm
-                indices = tqdm(indices)
+                bar = tqdm(total=len(indices))
             except ImportError:  # pragma: no cover
                 pass
         unet = _native_unet(model)
         if unet is not None and denoised_fn is None and cond_fn is None and not model_kwargs:
-            yield from self._native_loop(unet, img, indices, cond, clip_denoised, noise_fn,
-                                         fresh_outputs=not _reuse_outputs)
-            return
+            steps = self._native_loop(unet, img, indices, cond, clip_denoised, noise_fn,
+                                      fresh_outputs=not reuse_outputs, need_pred=not reuse_outputs,
+                                      update=update, eta=eta)
+        else:
+            steps = self._generic_loop(model, img, indices, shape[0], device, clip_denoised, denoised_fn,
+                                       cond_fn, model_kwargs, cond, noise_fn, update, eta)
+        try:
+            for out in steps:
+                if bar is not None:
+                    bar.update(1)
+                yield out
+        finally:
+            if bar is not None:
+                bar.close()
+
+    def _generic_loop(self, model, img, indices, B, device, clip_denoised, denoised_fn, cond_fn, model_kwargs,
+                      cond, noise_fn, update, eta):
         for i in indices:
-            t = th.tensor([i] * shape[0], device=device)
+            t = th.tensor([i] * B, device=device)
             with th.no_grad():
-                out = self.p_sample(model, img, t, clip_denoised=clip_denoised, denoised_fn=denoised_fn,
-                                    cond_fn=cond_fn, model_kwargs=model_kwargs, cond=cond, noise_fn=noise_fn)
+                if update == 1:
+                    out = self.ddim_sample(model, img, t, clip_denoised=clip_denoised, denoised_fn=denoised_fn,
+                                           cond_fn=cond_fn, model_kwargs=model_kwargs, eta=eta, cond=cond)
+                else:
+                    out = self.p_sample(model, img, t, clip_denoised=clip_denoised, denoised_fn=denoised_fn,
+                                        cond_fn=cond_fn, model_kwargs=model_kwargs, cond=cond, noise_fn=noise_fn)
                 yield out
                 img = out["sample"]
 
-    def _native_loop(self, unet, img, indices, cond, clip_denoised, noise_fn=None, graph=None, fresh_outputs=True):
+    def _native_loop(self, unet, img, indices, cond, clip_denoised, noise_fn=None, graph=None, fresh_outputs=True,
+                     need_pred=True, update=0, eta=0.0):
         """Channels-last resident loop for the native UNetModel.
 
         graph: capture one denoising step (U-Net launch list + noise draw +
@@ -313,6 +347,9 @@ class GaussianDiffusion:
         is the only per-step input: two 8-byte device fills before each replay.
         fresh_outputs=False lets the yielded tensors be the graph's static
         buffers (overwritten by the next step; p_sample_loop only keeps the last).
+        need_pred=False skips the pred_xstart store (p_sample_loop never reads
+        it; yields pred_xstart=None).  update=1 runs the DDIM step (no noise).
+        The caller's ``img`` is never written.
         """
         dev = img.device
         B, C, d, h, w = img.shape
@@ -332,7 +369,7 @@ class GaussianDiffusion:
             cnd = cond.contiguous().float()
             ops.copy3(cnd, _ncdhw(cnd), xin[..., C:], (V * cin, 1, cin), B, ccond, V)
         out_nd = th.empty((B, d, h, w, C), dtype=th.float32, device=dev)
-        coef = self.coef_table(dev)
+        coef = self.coef_table(dev, eta)
         mean_type = self._mean_type_code()
         s = _ncdhw(img)
         if graph is None:
@@ -341,16 +378,23 @@ class GaussianDiffusion:
         indices = list(indices)
         t = th.empty((B,), dtype=th.int64, device=dev)
         t_model = th.empty((B,), dtype=th.float32, device=dev)
+        ddim = update == 1
 
         def step(src, dst, pred, noise):
             unet.forward_ndhwc(xin, t_model, out_nd)
-            if noise is None:
+            if ddim:
+                noise = None
+            elif noise is None:
                 noise = (noise_fn or th.randn_like)(src)
             else:
                 noise.normal_()
-            ops.sampler_step(out_nd, (V * C, 1, C), src, s, dst, s, noise, s, coef, t, self.num_timesteps,
-                             B, d, h, w, clip_denoised=clip_denoised, pred_xstart=pred, px_s=s,
-                             mirror=xin, mr_s=(V * cin, 1, cin), mean_type=mean_type)
+            ops.sampler_step(out_nd, (V * C, 1, C), src, s, dst, s, noise, s if noise is not None else (0, 0, 0),
+                             coef, t, self.num_timesteps, B, d, h, w, clip_denoised=clip_denoised,
+                             pred_xstart=pred, px_s=s, mirror=xin, mr_s=(V * cin, 1, cin), mean_type=mean_type,
+                             update=update)
+
+        def fresh(x):
+            return x.clone() if (fresh_outputs and x is not None) else x
 
         with th.no_grad():
             if not graph or len(indices) < 3:
@@ -358,22 +402,22 @@ class GaussianDiffusion:
                     t.fill_(i)
                     t_model.fill_(self._model_timestep(i))
                     new = th.empty_like(img)
-                    pred = th.empty_like(img)
+                    pred = th.empty_like(img) if need_pred else None
                     step(img, new, pred, None)
                     yield {"sample": new, "pred_xstart": pred}
                     img = new
                 return
             # ping-pong state buffers; the first step runs eagerly (warms every
             # lazily-built piece: workspace, packed weights, kernel attributes)
-            bufs = [img, th.empty_like(img)]
-            pred = th.empty_like(img)
-            noise = th.empty_like(img)
+            # and reads the caller's tensor, which no graph ever writes
+            bufs = [th.empty_like(img), th.empty_like(img)]
+            pred = th.empty_like(img) if need_pred else None
+            noise = None if ddim else th.empty_like(img)
             i0 = indices[0]
             t.fill_(i0)
             t_model.fill_(self._model_timestep(i0))
-            step(bufs[0], bufs[1], pred, noise)
-            yield {"sample": bufs[1].clone() if fresh_outputs else bufs[1],
-                   "pred_xstart": pred.clone() if fresh_outputs else pred}
+            step(img, bufs[1], pred, noise)
+            yield {"sample": fresh(bufs[1]), "pred_xstart": fresh(pred)}
             graphs = []
             cs = th.cuda.Stream(device=dev)
             cs.wait_stream(th.cuda.current_stream(dev))
@@ -388,45 +432,50 @@ class GaussianDiffusion:
                 t_model.fill_(self._model_timestep(i))
                 graphs[n % 2].replay()
                 dst = bufs[0] if n % 2 == 0 else bufs[1]
-                yield {"sample": dst.clone() if fresh_outputs else dst,
-                       "pred_xstart": pred.clone() if fresh_outputs else pred}
+                yield {"sample": fresh(dst), "pred_xstart": fresh(pred)}
 
     # ---- DDIM (i2i by spec; the reference raises NotImplementedError) --------
     def ddim_sample(self, model, x, t, t_cpu=None, t_prev=None, t_prev_cpu=None, clip_denoised=True,
                     denoised_fn=None, cond_fn=None, model_kwargs=None, eta=0.0, sampling_steps=0, cond=None):
-        out = self.p_mean_variance(model, x, t, clip_denoised=clip_denoised, denoised_fn=denoised_fn,
-                                   model_kwargs=model_kwargs, cond=cond)
+        """Reference :721-784 in i2i mode (which the reference rejects, :752-757):
+        p_mean_variance with the [x | cond] input, then one fused kernel --
+        process_xstart, eps from x_t and x0, x0 sqrt(acp_prev) +
+        sqrt(1 - acp_prev - sigma^2) eps.  Like the reference it returns
+        mean_pred as the sample for any eta (:784); its unused noise draw is
+        skipped.  ``sampling_steps`` (the interp1d path, :761-767, which crashes
+        on numpy >= 1.24) is not supported."""
+        if cond_fn is not None:
+            raise NotImplementedError("cond_fn guidance is not on the fast-cwdm path")
+        if sampling_steps:
+            raise NotImplementedError("ddim_sample(sampling_steps>0) (reference :761-767 needs np.float)")
+        if model_kwargs is None:
+            model_kwargs = {}
+        B = x.shape[0]
+        assert t.shape == (B,)
+        x_cond = th.cat([x, cond], dim=1) if self.mode == "i2i" else x
+        model_output = model(x_cond, self._scale_timesteps(t), **model_kwargs)
+        self._check_t(t)
         x8 = x[:, :8] if self.mode == "i2i" else x
-        eps = self._predict_eps_from_xstart(x8, t, out["pred_xstart"])
-        ab = _extract_into_tensor(self.alphas_cumprod, t, x8.shape)
-        abp = _extract_into_tensor(self.alphas_cumprod_prev, t, x8.shape)
-        sigma = eta * ((1 - abp) / (1 - ab)) ** 0.5 * (1 - ab / abp) ** 0.5
-        mean_pred = out["pred_xstart"] * abp ** 0.5 + (1 - abp - sigma ** 2) ** 0.5 * eps
-        return {"sample": mean_pred, "pred_xstart": out["pred_xstart"]}
+        sample, pred = self._epilogue(model_output, x8, t, clip_denoised, denoised_fn, None, update=1, eta=eta)
+        return {"sample": sample, "pred_xstart": pred}
 
     def ddim_sample_loop(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None, cond_fn=None,
-                         model_kwargs=None, device=None, progress=False, eta=0.0, cond=None):
+                         model_kwargs=None, device=None, progress=False, eta=0.0, cond=None, time=None):
         final = None
-        for s in self.ddim_sample_loop_progressive(model, shape, noise=noise, clip_denoised=clip_denoised,
-                                                   denoised_fn=denoised_fn, cond_fn=cond_fn,
-                                                   model_kwargs=model_kwargs, device=device, progress=progress,
-                                                   eta=eta, cond=cond):
+        for s in self._sample_loop(model, shape, time, noise, clip_denoised, denoised_fn, cond_fn, model_kwargs,
+                                   device, progress, cond, None, True, update=1, eta=eta):
             final = s
         return final["sample"]
 
     def ddim_sample_loop_progressive(self, model, shape, noise=None, clip_denoised=True, denoised_fn=None,
                                      cond_fn=None, model_kwargs=None, device=None, progress=False, eta=0.0,
-                                     cond=None):
-        if device is None:
-            device = next(model.parameters()).device
-        img = noise if noise is not None else th.randn(*shape, device=device)
-        for i in list(range(self.num_timesteps))[::-1]:
-            t = th.tensor([i] * shape[0], device=device)
-            with th.no_grad():
-                out = self.ddim_sample(model, img, t, clip_denoised=clip_denoised, denoised_fn=denoised_fn,
-                                       model_kwargs=model_kwargs, eta=eta, cond=cond)
-                yield out
-                img = out["sample"]
+                                     cond=None, time=None):
+        """Reference :974-1047 (``time`` defaults to num_timesteps, not 1000;
+        respaced tables come from SpacedDiffusion).  With the native UNetModel
+        this is the resident, HIP-graph-captured loop of p_sample_loop with the
+        DDIM update."""
+        yield from self._sample_loop(model, shape, time, noise, clip_denoised, denoised_fn, cond_fn, model_kwargs,
+                                     device, progress, cond, None, False, update=1, eta=eta)
 
     # ---- training -----------------------------------------------------------
     def training_losses(self, model, x_start, t, classifier=None, model_kwargs=None, noise=None, labels=None,

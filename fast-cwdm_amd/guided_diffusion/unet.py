@@ -110,6 +110,7 @@ class UNetModel(nn.Module):
         for name, shape in spec_plan.param_specs:
             _register(self, name, nn.Parameter(th.empty(shape, dtype=th.float32)))
         self._reset_parameters()
+        self._param_gen = 0
         self._packed = None
         self._packed_key = None
         self._packed_bwd = None
@@ -194,10 +195,25 @@ class UNetModel(nn.Module):
         self._packed = None
         return self
 
+    def mark_params_changed(self):
+        """Tell the model its parameters were written behind autograd's back
+        (raw-pointer kernels, collectives into ``p.data``): the next forward /
+        backward re-packs the kernel-layout weights."""
+        self._param_gen += 1
+
+    def _weights_key(self):
+        # parameters are views of self._flat but each has its own version
+        # counter (set_data); writers of the flat buffer bump the flat's, in-place
+        # ops on a parameter bump that parameter's, raw writers call
+        # mark_params_changed -- the key covers all three
+        params = list(self.parameters())
+        return (self.compute_dtype, self._param_gen, self._flat._version) + \
+            tuple((p.data_ptr(), p._version) for p in params)
+
     def packed_weights(self):
         """Packed kernel-layout weights; re-packed whenever a parameter changed."""
         params = list(self.parameters())
-        key = (self.compute_dtype,) + tuple((p.data_ptr(), p._version) for p in params)
+        key = self._weights_key()
         if self._packed is None or self._packed_key != key:
             ops._need_cuda(*params)
             flat = [p.detach().float().contiguous() for p in params]
@@ -208,7 +224,7 @@ class UNetModel(nn.Module):
     def packed_bwd_weights(self):
         """Transposed/flipped dgrad weight layouts for the native backward."""
         params = list(self.parameters())
-        key = (self.compute_dtype,) + tuple((p.data_ptr(), p._version) for p in params)
+        key = self._weights_key()
         if self._packed_bwd is None or self._packed_bwd_key != key:
             ops._need_cuda(*params)
             self._packed_bwd = self.plan.pack_bwd([p.detach() for p in params])

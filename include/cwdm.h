@@ -42,6 +42,10 @@ enum {
 
 int cwdm_version(void);
 const char* cwdm_last_error(void);
+/* sha256 prefix (16 hex) of the sources the library was built from
+ * (fast-cwdm_amd/cwdm_hip/srchash.py); the Python loader refuses a library
+ * whose id differs from the tree it runs in. */
+const char* cwdm_build_id(void);
 
 /* ---------------------------------------------------------------------------
  * Haar wavelets.
@@ -80,11 +84,17 @@ int cwdm_haar_idwt3d(const void* bands, int in_dtype, const int64_t* in_strides 
  * v = (z*h + y)*w + x over the subband grid.  coef is a device table
  * [T][8] = {posterior_mean_coef1, posterior_mean_coef2,
  * exp(0.5*log_variance), sqrt_recip_alphas_cumprod,
- * sqrt_recipm1_alphas_cumprod, 0, 0, 0} in fp32 ([T][8]); t is a device
+ * sqrt_recipm1_alphas_cumprod, ddim sqrt(acp_prev), ddim sqrt(1 - acp_prev - sigma^2), 0}
+ * in fp32 ([T][8]); t is a device
  * int64[B] of (spaced) timestep indices.  Out-of-range t values cannot raise on device: callers
  * validate t on the host (the reference raises IndexError in
  * _extract_into_tensor, :1257-1259).  noise == NULL returns the posterior
  * mean (p_mean_variance's "mean") instead of a sample.
+ * update 1 replaces the posterior mean + noise by the DDIM step of
+ * ddim_sample (:753-784): eps = (coef[3] x_t - x0) / coef[4], x_prev =
+ * x0 coef[5] + coef[6] eps with coef[5] = sqrt(acp_prev), coef[6] =
+ * sqrt(1 - acp_prev - sigma_eta^2); noise is not read (the reference returns
+ * mean_pred, :784).
  * x_prev may alias x_t.  mirror (optional) receives a second copy of x_prev,
  * e.g. the first 8 channels of the NDHWC U-Net input buffer.
  * ------------------------------------------------------------------------- */
@@ -100,6 +110,7 @@ typedef struct {
   int64_t T, B, d, h, w;
   int clip_denoised;
   int mean_type;        /* 0 START_X (model predicts x0), 1 EPSILON */
+  int update;           /* 0 ancestral p_sample, 1 DDIM */
 } cwdm_sampler_args;
 int cwdm_sampler_step(const cwdm_sampler_args* args, cwdm_stream_t stream);
 

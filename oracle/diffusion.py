@@ -188,3 +188,14 @@ def ddim_sample(tab, model, x, t, cond, clip_denoised=True, eta=0.0):
     sigma = eta * ((1 - abp) / (1 - ab)) ** 0.5 * (1 - ab / abp) ** 0.5
     mean_pred = out["pred_xstart"] * abp ** 0.5 + (1 - abp - sigma ** 2) ** 0.5 * eps
     return {"sample": mean_pred, "pred_xstart": out["pred_xstart"]}
+
+
+def ddim_sample_loop(tab, model, x_T, cond, clip_denoised=True, eta=0.0, time=None):
+    """ddim_sample_loop_progressive (gaussian_diffusion.py:974-1047) over the
+    (respaced) tables, t = time-1 ... 0, each step feeding mean_pred back."""
+    time = tab.num_timesteps if time is None else time
+    img = x_T
+    for i in range(time - 1, -1, -1):
+        t = torch.full((x_T.shape[0],), i, dtype=torch.int64)
+        img = ddim_sample(tab, model, img, t, cond, clip_denoised, eta)["sample"]
+    return img

@@ -94,6 +94,28 @@ def test_sampler_step_vs_oracle(clip, mean_type):
     assert torch.equal(sample[0].cpu(), mean[0]) or rel_err(sample[0], mean[0]) < 1e-6  # t = 0: no noise
 
 
+@pytest.mark.parametrize("eta", [0.0, 0.5])
+def test_ddim_step_vs_oracle(eta):
+    """The DDIM update of the fused kernel (update=1) vs oracle.ddim_sample on
+    respaced ddim10 tables, model output injected: bit-level agreement."""
+    from oracle import diffusion as od
+    from guided_diffusion import script_util
+    d = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
+                                              timestep_respacing="ddim10")
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"), use_timesteps=od.space_timesteps(1000, "ddim10"))
+    g = torch.Generator().manual_seed(3)
+    B, n = 3, 6
+    mo = torch.randn(B, 8, n, n, n, generator=g) * 0.5 + 0.2
+    x = torch.randn(B, 8, n, n, n, generator=g)
+    cond = torch.zeros(B, 24, n, n, n)
+    t = torch.tensor([0, 4, 9])
+    sample, pred = d._epilogue(mo.to(DEV), x.to(DEV), t.to(DEV), True, None, None, update=1, eta=eta)
+    ref = od.ddim_sample(tab, lambda xc, tt: mo, x, t, cond, clip_denoised=True, eta=eta)
+    assert rel_err(pred, ref["pred_xstart"]) < 1e-6
+    assert rel_err(sample, ref["sample"]) < 1e-6
+    assert torch.equal(sample[0].cpu(), pred[0].cpu())   # t = 0: acp_prev = 1, the sample is x0
+
+
 # --------------------------------------------------------------------------- conv3d
 def _conv_call(dtype, out_grid, a0, a1, amode, gn, w, bias, bvec_bstride=0, b0=None, b1=None, wb=None, res=None,
                rmode=-1, out_f32=False, stats=True, split=True):

@@ -397,10 +397,31 @@ def test_training_step_vs_oracle():
     ref.grad = g.cpu()
     topt.step()
     assert rel_err(model.flat_params, ref.detach()) < 1e-6
-    # the packed kernel weights follow the update
+    # the packed kernel weights follow the update: the stepped model equals a
+    # fresh model loaded with the updated parameters, forward and gradient
+    xq = torch.randn(1, 32, 16, 16, 16, device=DEV)
+    tq = torch.tensor([3], device=DEV)
+    Pn = {n: p.detach().cpu().clone() for n, p in model.named_parameters()}
+    fresh, _ = _c1_model_and_diffusion(Pn)
     with torch.no_grad():
-        o2 = model(torch.randn(1, 32, 16, 16, 16, device=DEV), torch.tensor([3], device=DEV))
-    assert torch.isfinite(o2).all()
+        o2, o2_ref = model(xq, tq), fresh(xq, tq)
+    assert rel_err(o2, o2_ref) < 1e-6
+    assert rel_err(o2.cpu(), ou.unet_forward(Pn, xq.cpu(), tq.cpu(), num_groups=8, **cases.C1_CFG)) < 1e-3
+    # a second training step's gradient is taken at the updated weights
+    opt.zero_grad()
+    terms2, _, _ = diffusion.training_losses(model, vols, t, mode="i2i", contr="t2w", noise=noise)
+    terms2["mse_wav"].mean().backward()
+    Pr2 = {k: v.clone().requires_grad_(True) for k, v in Pn.items()}
+
+    def om2(x, tt, **kw):
+        return ou.unet_forward(Pr2, x, tt, num_groups=8, **cases.C1_CFG)
+    r2, _, _ = od.training_losses(tab, om2, {k: v.cpu() for k, v in vols.items()}, t.cpu(), noise.cpu(),
+                                  contr="t2w")
+    r2["mse_wav"].mean().backward()
+    for n, p in model.named_parameters():
+        err = float((p.grad.double().cpu() - Pr2[n].grad.double()).norm() /
+                    Pr2[n].grad.double().norm().clamp_min(1e-30))
+        assert err < 1e-3, ("step 2", n, err)
 
 
 def test_trainloop_runs_and_learns(tmp_path, monkeypatch):

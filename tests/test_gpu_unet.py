@@ -159,14 +159,100 @@ def test_respaced_ddim50_tables_and_loop_runs():
     assert torch.isfinite(out).all()
 
 
+def _c1_respaced(respacing, dtype="fp32", steps=1000, schedule="direct"):
+    from guided_diffusion import script_util
+    args = script_util.run_sh_model_args(num_channels=32, channel_mult="1,2", num_res_blocks=1, num_groups=8,
+                                         diffusion_steps=steps, sample_schedule=schedule,
+                                         timestep_respacing=respacing)
+    keys = script_util.model_and_diffusion_defaults().keys()
+    model, diffusion = script_util.create_model_and_diffusion(**{k: args[k] for k in keys}, compute_dtype=dtype)
+    return model, diffusion
+
+
+def _c1_loop_inputs(n=16, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    vols = cases.data.brats_batch(2 * n, seed=seed, batch=1)
+    cond = torch.cat([haar.dwt_cat(vols[k]) for k in ("t1c", "t2w", "t2f")], dim=1)
+    x_T = torch.randn(1, 8, n, n, n, generator=g)
+    return cond, x_T, g
+
+
+@pytest.mark.parametrize("respacing", ["ddim10", "25,15"])
+def test_respaced_ancestral_loop_vs_oracle(respacing):
+    """SpacedDiffusion's p_sample_loop (native resident loop, fp32) over
+    respaced tables vs oracle.p_sample_loop on Tables(use_timesteps=...),
+    same injected noise: 1e-3 (respace.py:65-132, gaussian_diffusion.py:668-719)."""
+    P = ou.random_params(seed=1, **cases.C1_CFG)
+    model, diffusion = _c1_respaced(respacing)
+    model.load_state_dict(P)
+    model.to(DEV)
+    cond, x_T, g = _c1_loop_inputs()
+    T = diffusion.num_timesteps
+    noises = [torch.randn(x_T.shape, generator=g) for _ in range(T)]
+    it = iter([z.to(DEV) for z in noises])
+    out = diffusion.p_sample_loop(model, x_T.shape, noise=x_T.to(DEV), cond=cond.to(DEV), progress=False,
+                                  noise_fn=lambda x: next(it))
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"),
+                    use_timesteps=od.space_timesteps(1000, respacing))
+    assert tab.timestep_map == diffusion.timestep_map
+    ref = od.p_sample_loop(tab, ou.OracleUNet(P, num_groups=8, **cases.C1_CFG), x_T, cond, noises)
+    assert rel_err(out, ref) < 1e-3
+
+
+@pytest.mark.parametrize("eta", [0.0, 0.3])
+def test_ddim_loop_vs_oracle(eta):
+    """i2i DDIM (config 4's sampler; the reference raises for i2i, so the
+    oracle restates ddim_sample by spec): the native HIP-graph-captured DDIM
+    loop over ddim10 tables vs oracle.ddim_sample_loop, fp32, 1e-3; the eager
+    loop is bit-identical to the graph replay."""
+    P = ou.random_params(seed=1, **cases.C1_CFG)
+    model, diffusion = _c1_respaced("ddim10")
+    model.load_state_dict(P)
+    model.to(DEV)
+    cond, x_T, _ = _c1_loop_inputs(seed=7)
+    x_dev = x_T.to(DEV)
+    diffusion.use_hip_graph = True
+    out = diffusion.ddim_sample_loop(model, x_T.shape, noise=x_dev, cond=cond.to(DEV), eta=eta)
+    diffusion.use_hip_graph = False
+    eager = diffusion.ddim_sample_loop(model, x_T.shape, noise=x_dev, cond=cond.to(DEV), eta=eta)
+    diffusion.use_hip_graph = True
+    assert torch.equal(out, eager)
+    assert torch.equal(x_dev.cpu(), x_T)    # the caller's x_T is never written
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"), use_timesteps=od.space_timesteps(1000, "ddim10"))
+    ref = od.ddim_sample_loop(tab, ou.OracleUNet(P, num_groups=8, **cases.C1_CFG), x_T, cond, eta=eta)
+    assert rel_err(out, ref) < 1e-3
+    # the progressive generator yields every step, and the generic-model seam agrees
+    steps = list(diffusion.ddim_sample_loop_progressive(model, x_T.shape, noise=x_dev, cond=cond.to(DEV), eta=eta))
+    assert len(steps) == 10 and torch.equal(steps[-1]["sample"], out)
+    generic = diffusion.ddim_sample_loop(lambda x, t: model(x, t), x_T.shape, noise=x_dev, cond=cond.to(DEV),
+                                         eta=eta, device=DEV)
+    assert rel_err(generic, out) < 1e-6
+
+
+def test_graph_loop_leaves_caller_noise_unchanged():
+    """p_sample_loop with HIP-graph replay must not write into the x_T tensor
+    it was given (the first step reads it; the graphs ping-pong their own)."""
+    P = ou.random_params(seed=1, **cases.C1_CFG)
+    model, diffusion = _c1_respaced("ddim10")
+    model.load_state_dict(P)
+    model.to(DEV)
+    cond, x_T, _ = _c1_loop_inputs()
+    x_dev = x_T.to(DEV)
+    diffusion.use_hip_graph = True
+    out = diffusion.p_sample_loop(model, x_T.shape, noise=x_dev, cond=cond.to(DEV), progress=False)
+    assert torch.equal(x_dev.cpu(), x_T)
+    assert out.data_ptr() != x_dev.data_ptr() and torch.isfinite(out).all()
+
+
 @pytest.mark.parametrize("respacing,dtype", [("", "fp32"), ("ddim10", "bf16")])
 def test_hip_graph_loop_equals_eager_loop(respacing, dtype):
     """The graph-captured sampling step (one capture, replayed per timestep,
     noise from torch's graph-safe generator) reproduces the eager loop with
-    the same seed, for the full and a respaced schedule."""
+    the same seed, for the full and a respaced schedule (a 50-step direct
+    schedule: beta_T = 0.4, every table column finite)."""
     from guided_diffusion import script_util
     args = script_util.run_sh_model_args(num_channels=32, channel_mult="1,2", num_res_blocks=1, num_groups=8,
-                                         diffusion_steps=20, sample_schedule="direct",
+                                         diffusion_steps=50, sample_schedule="direct",
                                          timestep_respacing=respacing)
     keys = script_util.model_and_diffusion_defaults().keys()
     model, diffusion = script_util.create_model_and_diffusion(**{k: args[k] for k in keys}, compute_dtype=dtype)

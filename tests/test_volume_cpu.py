@@ -59,3 +59,39 @@ def test_oracle_sample_finish_roundtrip():
     assert out.shape == (2, 8, 6, 9)
     ref = (img.clamp(0, 1) * mask).squeeze(1)[..., :9]
     assert (out - ref).abs().max() < 1e-6
+
+
+def test_worker_host_path_matches_oracle_and_loads_in_workers(tmp_path, monkeypatch):
+    """BRATSVolumes inside DataLoader workers (the reference scripts use
+    num_workers=12; a forked worker cannot own a HIP context) runs the
+    reference's numpy arithmetic and returns CPU tensors equal to the oracle's
+    modality tensor.  nibabel is absent here: a stub module decodes .npy files."""
+    import sys
+    import types
+    from guided_diffusion import bratsloader
+    img = brain_like((40, 36, 31), 1)
+    assert torch.equal(bratsloader._prepare_modality_host(img, pad_z=32, crop=4),
+                       ov.modality_tensor(img, pad_z=32, crop=4))
+    subj = tmp_path / "BraTS-GLI-00000-000"
+    subj.mkdir()
+    vols = {}
+    for k, key in enumerate(("t1n", "t1c", "t2w", "t2f")):
+        v = brain_like((240, 240, 155), 10 + k)
+        vols[key] = v
+        np.save(subj / f"BraTS-GLI-00000-000-{key}.npy", v)
+    stub = types.ModuleType("nibabel")
+
+    class _Img:
+        def __init__(self, path):
+            self.path = path
+
+        def get_fdata(self):
+            return np.load(self.path)
+    stub.load = _Img
+    monkeypatch.setitem(sys.modules, "nibabel", stub)
+    ds = bratsloader.BRATSVolumes(str(tmp_path), mode="train")
+    dl = torch.utils.data.DataLoader(ds, batch_size=1, num_workers=2, multiprocessing_context="fork")
+    batch = next(iter(dl))
+    for key, v in vols.items():
+        assert batch[key].shape == (1, 1, 224, 224, 160) and not batch[key].is_cuda
+        assert torch.equal(batch[key][0], ov.modality_tensor(v)), key
