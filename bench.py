@@ -10,7 +10,11 @@ the GPU before the timed region.
 
 Multi-GPU: sampling shards by volume ("replicas only"): each rank
 denoises its own volume, no collective on the data path; value = all ranks'
-steps / max-over-ranks time.
+steps / max-over-ranks time.  `--gpus N` without torchrun's environment
+launches the N ranks itself (fresh child processes, started before this
+process touches the GPU).  The config-3 side figure `train_ddp` is the one
+leg with a real exchange: TrainLoop.run_step at 128^3 bf16, batch 1 per GPU,
+the bucketed gradient all-reduce over RCCL overlapped with the backward.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including
 `roofline` for the dominant kernel (conv3d implicit GEMM, all launches of a
@@ -20,7 +24,8 @@ import argparse
 import json
 import math
 import os
-import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,7 +37,7 @@ for _p in (os.path.join(ROOT, "fast-cwdm_amd"), ROOT):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r02", "r01")]
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3
 
@@ -79,23 +84,119 @@ def build(args, device):
     return model, diffusion
 
 
-def cpu_baseline(n, threads):
-    """The oracle (PyTorch-CPU fp32 restatement of the reference path) on this
-    host: one full denoising step (U-Net forward + p_sample epilogue) at n^3."""
+def cpu_threads():
+    """Host cores this process may use: its CPU affinity, capped by a cgroup
+    CPU quota when one is set (the GPU box's share of a larger machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(state, cond, x_T, threads, T=1000, warmup=1, steps=2):
+    """the oracle (PyTorch-CPU fp32 restatement of the
+    reference path) on this host with the GPU leg's own inputs -- the same
+    seeded weights (state_dict of the benchmarked model), phantom cond and x_T
+    -- 1 warm-up step (t = T-1) then 2 timed steps (t = T-2, T-3)."""
     from oracle import diffusion as od, unet as ou
     torch.set_num_threads(threads)
-    P = ou.random_params(seed=1)
-    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"))
-    model = ou.OracleUNet(P)
-    x = torch.randn(1, 8, n, n, n)
-    cond = torch.rand(1, 24, n, n, n)
-    noise = torch.randn(1, 8, n, n, n)
-    t = torch.tensor([999])
-    t0 = time.perf_counter()
+    tab = od.Tables(od.beta_schedule("linear", T, "direct"))
+    model = ou.OracleUNet(state)
+    g = torch.Generator().manual_seed(7)
+    x = x_T
+    dts = []
     with torch.no_grad():
-        od.p_sample(tab, model, x, t, cond, noise)
-    dt = time.perf_counter() - t0
-    return dt
+        for k in range(warmup + steps):
+            t = torch.tensor([T - 1 - k])
+            noise = torch.randn(x.shape, generator=g)
+            t0 = time.perf_counter()
+            x = od.p_sample(tab, model, x, t, cond, noise)["sample"]
+            dts.append(time.perf_counter() - t0)
+    return dts[warmup:]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """`--gpus N` outside torchrun: start N fresh rank processes (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_* set) and return the worst exit code.
+    This process never touches the GPU and never execs."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
+def time_loop(loop, n, world, sync):
+    for _ in range(n[0]):
+        next(loop)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(n[1]):
+        next(loop)
+    sync()
+    return time.perf_counter() - t0
+
+
+def train_leg(model, diffusion, n, rank, world, device, steps, warmup, sync, max_over_ranks):
+    """Config 3: TrainLoop.run_step (4 Haar DWTs + q_sample into the 32-channel
+    input, native forward, MSE, segmented native backward with the bucketed
+    gradient all-reduce over RCCL overlapped, fused AdamW), batch 1 per GPU."""
+    import numpy as np
+    from guided_diffusion import train_util
+    os.environ.setdefault("CWDM_LOGDIR", os.path.join(ROOT, "gpurun_out", "bench_train"))
+    np.random.seed(3)
+    n2 = 2 * n
+    batch = {k: phantom_gpu(n2, 1000 + 100 * rank + j, device) for j, k in enumerate(("t1n", "t1c", "t2w", "t2f"))}
+    loop = train_util.TrainLoop(model=model, diffusion=diffusion, data=[batch], batch_size=1, in_channels=32,
+                                image_size=n2, microbatch=-1, lr=1e-5, ema_rate="0.9999", log_interval=10 ** 9,
+                                contr="t1n", save_interval=10 ** 9, resume_checkpoint="", resume_step=0,
+                                mode="i2i", diffusion_steps=1000)
+    for _ in range(warmup):
+        loop.run_step(batch, {})
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss, _, _ = loop.run_step(batch, {})
+    sync()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    plan = model.plan
+    fl = plan.flops(1, n, n, n) + plan.backward_flops(1, n, n, n)
+    per = dt / steps
+    return {"workload": "config3: TrainLoop.run_step, 128^3 subbands (256^3 phantoms x 4 modalities), batch 1 per GPU, "
+                        f"{model.compute_dtype}, bucketed gradient all-reduce "
+                        f"({'RCCL' if world > 1 and dist.get_backend() == 'nccl' else dist.get_backend() if world > 1 else 'none'})"
+                        " overlapped with the segmented native backward, fused AdamW",
+            "volumes_per_s": round(world * steps / dt, 4), "ms_per_step": round(1000 * per, 2), "steps": steps,
+            "warmup": warmup, "n_gpus": world, "conv_tflop_per_step": round(fl / 1e12, 2),
+            "mfma_frac": round(fl / per / 1e12 / BF16_PEAK_TFLOPS, 4), "loss": round(float(loss), 6),
+            "scaling": "weak"}
 
 
 def main():
@@ -106,23 +207,44 @@ def main():
     ap.add_argument("--grid", type=int, default=128, help="subband edge (image edge = 2x)")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-grid", type=int, default=0, help="0 = same grid as the GPU run")
     ap.add_argument("--graph", type=int, default=1, help="replay one HIP-graph-captured step per timestep")
     ap.add_argument("--respaced", type=int, default=1,
-                    help="also time config 4: a full 50-step respaced (ddim50) volume, graph-captured loop")
+                    help="also time config 4: a full 50-step respaced DDIM (ddim50) volume, graph-captured loop")
     ap.add_argument("--batched", type=int, default=2,
                     help="also time B volumes denoised together in one batched step (serving throughput; "
                          "0 = skip); reported beside, never as, the B=1 metric")
+    ap.add_argument("--fp32", type=int, default=3, help="also time K steps of the fp32 parity mode (0 = skip)")
+    ap.add_argument("--train", type=int, default=5, help="config-3 train_ddp side figure: timed steps (0 = skip)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: exercise the rank launch / barrier / max-over-ranks plumbing only")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # CWDM_BENCH_REHEARSE=1: every rank on cuda:0 with gloo (a 1-GPU rehearsal
     # of the N-rank code path; the driver's N-GPU runs use RCCL, one GPU per rank)
-    rehearse = os.environ.get("CWDM_BENCH_REHEARSE") == "1"
+    rehearse = os.environ.get("CWDM_BENCH_REHEARSE") == "1" or args.dry_run
     if world > 1:
         dist.init_process_group("gloo" if rehearse else "nccl")
+    if args.dry_run:
+        def mor(v):
+            tt = torch.tensor([v], dtype=torch.float64)
+            if world > 1:
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            return float(tt)
+        if world > 1:
+            dist.barrier()
+        v = mor(float(rank))
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "max_rank": v,
+                              "backend": dist.get_backend() if world > 1 else None}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if rehearse:
         local = 0
     torch.cuda.set_device(local)
@@ -134,6 +256,11 @@ def main():
         tt = torch.tensor([v], dtype=torch.float64, device="cpu" if rehearse else device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return float(tt)
+
+    def sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
 
     model, diffusion = build(args, device)
     n = args.grid
@@ -150,19 +277,16 @@ def main():
     total = args.warmup + args.steps
     assert total <= T
     loop = diffusion._native_loop(model, x_T, list(range(T))[::-1][:total + 2], cond, True,
-                                  graph=bool(args.graph), fresh_outputs=False)
+                                  graph=bool(args.graph), fresh_outputs=False, need_pred=False)
     for _ in range(args.warmup):
         next(loop)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         next(loop)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync()
     elapsed = max_over_ranks(time.perf_counter() - t0)
+    loop.close()
 
     # roofline of the dominant kernel -- the implicit-GEMM MFMA conv kernels:
     # hipEvents around each of their launches over one extra (eager) step, on
@@ -170,12 +294,12 @@ def main():
     # sampler are HBM-bound kernels outside this figure
     plan = model.plan
     plan.set_profiling(True)
-    loop.close()
     loop = diffusion._native_loop(model, x_T, [T - 1], cond, True, graph=False)
     next(loop)
     torch.cuda.synchronize()
     conv_ms, conv_flops, n_conv = plan.profile_read()
     plan.set_profiling(False)
+    loop.close()
     step_flops = plan.flops(1, n, n, n)
 
     # serving side-figure: B volumes per batched step (the 16^3 / 8^3 levels of
@@ -187,27 +311,17 @@ def main():
         cb = cond.expand(Bv, -1, -1, -1, -1).contiguous()
         nb = 6
         lb = diffusion._native_loop(model, xb, list(range(T))[::-1][:nb + 3], cb, True, graph=bool(args.graph),
-                                    fresh_outputs=False)
-        for _ in range(2):
-            next(lb)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t1 = time.perf_counter()
-        for _ in range(nb):
-            next(lb)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        tb = max_over_ranks(time.perf_counter() - t1)
+                                    fresh_outputs=False, need_pred=False)
+        tb = max_over_ranks(time_loop(lb, (2, nb), world, sync))
         lb.close()
         batched = {"batch_per_gpu": Bv, "ms_per_batched_step": round(1000 * tb / nb, 3),
                    "volume_steps_per_s": round(world * Bv * nb / tb, 3)}
         del xb, cb
         torch.cuda.empty_cache()
 
-    # config 4: respaced 50-step sampling of one whole volume (timestep_respacing
-    # "ddim50" = stride-20 subset of the 1000-step schedule), graph-captured loop
+    # config 4: respaced 50-step DDIM sampling of one whole volume (timestep_respacing
+    # "ddim50" = stride-20 subset of the 1000-step schedule; i2i DDIM update in the
+    # fused sampler kernel), graph-captured loop
     respaced = None
     if args.respaced:
         from guided_diffusion import respace
@@ -218,26 +332,50 @@ def main():
         sp.mode = "i2i"
         sp.use_hip_graph = bool(args.graph)
         for rep in range(2):   # first pass warms the graph capture path
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
+            sync()
             t1 = time.perf_counter()
-            sp.p_sample_loop(model, tuple(x_T.shape), noise=x_T, cond=cond, progress=False)
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
+            sp.ddim_sample_loop(model, tuple(x_T.shape), noise=x_T, cond=cond, eta=0.0)
+            sync()
             rs = time.perf_counter() - t1
         rs = max_over_ranks(rs)
-        respaced = {"workload": "config4: timestep_respacing ddim50 (50 of 1000 steps), one volume per GPU, "
-                                f"{'HIP-graph-captured' if args.graph else 'eager'} step",
+        respaced = {"workload": "config4: timestep_respacing ddim50 (50 of 1000 steps), i2i DDIM (eta 0), one volume "
+                                f"per GPU, {'HIP-graph-captured' if args.graph else 'eager'} step",
                     "s_per_volume": round(rs, 4), "denoising_steps_per_s": round(world * 50 / rs, 3)}
+
+    # fp32 parity mode (the numerics the 1e-3 parity tests pin): same weights,
+    # same inputs, exact-fp32 MFMA
+    fp32 = None
+    if args.fp32 and args.dtype != "fp32":
+        model.set_compute_dtype("fp32")
+        lf = diffusion._native_loop(model, x_T, list(range(T))[::-1][:args.fp32 + 3], cond, True,
+                                    graph=bool(args.graph), fresh_outputs=False, need_pred=False)
+        tf = max_over_ranks(time_loop(lf, (1, args.fp32), world, sync))
+        lf.close()
+        model.set_compute_dtype(args.dtype)
+        fp32 = {"denoising_steps_per_s": round(world * args.fp32 / tf, 4), "ms_per_step": round(1000 * tf / args.fp32, 2),
+                "steps": args.fp32, "mfma_frac_of_fp32_peak": round(step_flops * args.fp32 / tf / 1e12 / F32_PEAK_TFLOPS, 4)}
+        torch.cuda.empty_cache()
+
+    # snapshot for the CPU baseline before the training leg moves the weights
+    cpu_state = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        cpu_state = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+        cpu_cond, cpu_x = cond.cpu(), x_T.cpu()
+
+    train = None
+    if args.train:
+        train = train_leg(model, diffusion, n, rank, world, device, args.train, 2, sync, max_over_ranks)
 
     # HBM bytes of the same conv family per step, from the committed rocprofv3
     # PMC passes of this bench (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950)
-    traffic = None
-    if n == 128 and args.dtype == "bf16" and os.path.exists(TRAFFIC_JSON):
-        with open(TRAFFIC_JSON) as fh:
-            traffic = json.load(fh)["mfma_conv_kernels"]["hbm_bytes"]
+    traffic, traffic_src = None, None
+    if n == 128 and args.dtype == "bf16":
+        for tj in TRAFFIC_JSONS:
+            if os.path.exists(tj):
+                with open(tj) as fh:
+                    traffic = json.load(fh)["mfma_conv_kernels"]["hbm_bytes"]
+                traffic_src = os.path.relpath(tj, ROOT)
+                break
 
     ms_per_step = 1000.0 * elapsed / args.steps
     value = world * args.steps / elapsed
@@ -264,25 +402,31 @@ def main():
         "hip_graph": bool(args.graph),
         "respaced_ddim50": respaced,
         "batched_serving": batched,
+        "fp32_parity_mode": fp32,
+        "train_ddp": train,
         "mfma_util_whole_step": round(step_flops * (value / world) / 1e12 / peak, 4),
         "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_unit": "HBM bytes per step of those launches (2 x FETCH_SIZE + WRITE_SIZE, "
-                                     "profiles/r01/pmc_traffic.json)",
+                                     f"{traffic_src})",
                      "kernel": f"implicit-GEMM MFMA conv kernels (conv3d_v4 DMA-staged + brick + output head: "
                                f"{n_conv} launches per step, {conv_ms:.2f} ms, {conv_flops / 1e12:.2f} TFLOP)"},
     }
-    if rank == 0 and world == 1 and args.cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        cg = args.cpu_grid or n
-        dt = cpu_baseline(cg, threads)
-        scale = (cg / n) ** 3
-        res["cpu_baseline"] = {"value": round(scale / dt, 6), "unit": "denoising-steps/s", "cores": threads,
+    if cpu_state is not None:
+        threads = cpu_threads()
+        dts = cpu_baseline(cpu_state, cpu_cond, cpu_x, threads)
+        per = sum(dts) / len(dts)
+        res["cpu_baseline"] = {"value": round(1.0 / per, 6), "unit": "denoising-steps/s", "cores": threads,
                                "kind": "port",
-                               "sample": f"1 oracle p_sample step (fp32 PyTorch-CPU restatement) at {cg}^3"
-                                         + ("" if cg == n else f", scaled by ({cg}/{n})^3")
-                                         + f" on {platform.processor() or platform.machine()}",
-                               "seconds": round(dt, 2)}
+                               "sample": f"oracle p_sample (fp32 PyTorch-CPU restatement of the reference path) at "
+                                         f"{n}^3 with this run's weights, phantom cond and x_T: 1 warm-up + "
+                                         f"{len(dts)} timed steps (t=998, 997), torch threads = the cores this "
+                                         f"process may use (affinity/cgroup quota; the host has "
+                                         f"{os.cpu_count()} CPUs)",
+                               "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+                               "seconds_per_step": [round(d, 2) for d in dts],
+                               "extrapolated_s_per_volume": {"1000_steps": round(1000 * per, 1),
+                                                             "50_steps": round(50 * per, 1)}}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

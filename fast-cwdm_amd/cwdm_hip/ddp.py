@@ -18,9 +18,14 @@ import torch.distributed as dist
 
 
 class GradBucketReducer:
-    def __init__(self, group=None, bucket_bytes=64 << 20):
+    """``force``: run the collectives even at world size 1 (tests exercise the
+    RCCL path on a one-GPU box that way)."""
+
+    def __init__(self, group=None, bucket_bytes=64 << 20, force=False):
         self.group = group
         self.bucket = max(int(bucket_bytes) // 4, 1)
+        self.force = force
+        self.launched = 0
         self._works = []
         self._lo = self._hi = None
 
@@ -31,11 +36,12 @@ class GradBucketReducer:
     def _flush(self, flat):
         if self._lo is not None and self._hi > self._lo:
             self._works.append(dist.all_reduce(flat[self._lo:self._hi], group=self.group, async_op=True))
+            self.launched += 1
         self._lo = self._hi = None
 
     def __call__(self, seg, flat, off, n):
         """UNetModel._grad_hook: (seg, flat grad buffer, offset, count); seg None = end."""
-        if self.world == 1:
+        if self.world == 1 and not (self.force and dist.is_initialized()):
             return
         if seg is None:
             self._flush(flat)
