@@ -20,11 +20,7 @@ def _dwt(x):
 
 
 def _idwt(bands):
-    b0 = bands[0]
-    B, C, d, h, w = b0.shape
-    stacked = torch.stack([b.to(torch.float32) for b in bands], 0).contiguous()
-    v = d * h * w
-    return ops.idwt3d(stacked, (B * C * v, C * v, v, 1), B, C, d, h, w)
+    return ops.idwt3d_planes(list(bands))
 
 
 class DWTFunction_3D(Function):

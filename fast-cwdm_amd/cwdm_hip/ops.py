@@ -61,6 +61,47 @@ def idwt3d(bands, band_strides, B, C, d, h, w, lll_mul3=False, clamp01=False, ou
     return out
 
 
+def idwt3d_planes(bands, lll_mul3=False):
+    """IDWT of 8 separate (B, C, d, h, w) band tensors (same dtype, same strides
+    up to the base pointer) without stacking them."""
+    _need_cuda(*bands)
+    if len(bands) != 8:
+        raise AssertionError("IDWT_3D takes the 8 subbands")
+    b0 = bands[0]
+    if lll_mul3:
+        raise NotImplementedError("lll_mul3 on separate planes")
+    bands = [b.contiguous() if b.dtype in DT else b.float().contiguous() for b in bands]
+    dt = bands[0].dtype
+    bands = [b if b.dtype == dt else b.to(dt) for b in bands]
+    for b in bands:
+        if b.shape != b0.shape:
+            raise AssertionError("IDWT_3D: all subbands must have one shape")
+    B, C, d, h, w = b0.shape
+    out = torch.empty((B, C, 2 * d, 2 * h, 2 * w), device=b0.device, dtype=torch.float32)
+    v = d * h * w
+    arr = (ctypes.c_void_p * 8)(*[b.data_ptr() for b in bands])
+    check(lib().cwdm_haar_idwt3d_planes(arr, DT[dt], strides(C * v, v, 1), B, C, d, h, w, _p(out), _stream()),
+          "IDWT_3D")
+    return out
+
+
+def prepare_batch(target, c1, c2, c3, eps_img, coef, t, T):
+    """training_losses front end in one kernel (cwdm_prepare_batch): returns
+    (x_in (B, 32, d, h, w) = [q_sample | 3 condition DWTs], x0 (B, 8, d, h, w))."""
+    vols = [v.contiguous().float() for v in (target, c1, c2, c3, eps_img)]
+    _need_cuda(*vols, coef, t)
+    for v in vols:
+        if v.dim() != 5 or v.shape[1] != 1 or v.shape != vols[0].shape:
+            raise AssertionError("prepare_batch: five (B, 1, D, H, W) volumes of one shape")
+    B, _, D, H, W = vols[0].shape
+    x_in = torch.empty((B, 32, D // 2, H // 2, W // 2), device=vols[0].device, dtype=torch.float32)
+    x0 = torch.empty((B, 8, D // 2, H // 2, W // 2), device=vols[0].device, dtype=torch.float32)
+    t = t.to(dtype=torch.int64).contiguous()
+    check(lib().cwdm_prepare_batch(*[_p(v) for v in vols], B, D, H, W, _p(coef), _p(t), T, _p(x_in), _p(x0),
+                                   _stream()), "training_losses")
+    return x_in, x0
+
+
 def copy3(src, src_strides, dst, dst_strides, B, C, V):
     _need_cuda(src, dst)
     check(lib().cwdm_copy3(_p(src), DT[src.dtype], strides(*src_strides), _p(dst), DT[dst.dtype],
@@ -136,10 +177,7 @@ def waverec3(coeffs):
     cur = coeffs[0]
     _need_cuda(cur)
     for d in coeffs[1:]:
-        B, C, h0, h1, h2 = cur.shape
-        bands = torch.stack([cur.contiguous()] + [d[k].contiguous() for k in HIGH_BANDS])  # (8, B, C, d, h, w)
-        v = h0 * h1 * h2
-        cur = idwt3d(bands, (B * C * v, C * v, v, 1), B, C, h0, h1, h2)
+        cur = idwt3d_planes([cur] + [d[k] for k in HIGH_BANDS])
     return cur
 
 

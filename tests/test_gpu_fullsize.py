@@ -92,3 +92,88 @@ def test_fullsize_bf16_step_close_to_fp32():
         print(f"bf16 vs fp32 full size, output {k}: rel L2 {l2:.3e}, rel max {rel_err(a, b):.3e}")
         assert l2 < 4e-2, l2
         assert rel_err(a, b) < 0.25
+
+
+def _image(sample):
+    """scripts/sample.py:113-121: IDWT with LLL x 3, clamp to [0, 1]."""
+    from cwdm_hip import ops
+    return ops.sample_finish(sample.to(DEV).float().contiguous()).cpu()
+
+
+@pytest.mark.parametrize("sampler", ["ddpm", "ddim"])
+def test_fullsize_respaced50_volume_bf16_vs_fp32(sampler):
+    """A whole 50-step respaced volume (timestep_respacing ddim50) at config-2
+    size, bf16 throughput mode vs fp32 parity mode, same weights, x_T and step
+    noise: the numerics of the headline over a full trajectory.
+    Measured on the final image (IDWT, clamp) and the subbands."""
+    from guided_diffusion import respace
+    P = ou.random_params(seed=5)
+    cond, x_t, _ = _step_inputs()
+    g = torch.Generator().manual_seed(77)
+    noises = [torch.randn(1, 8, N, N, N, generator=g) for _ in range(50)]
+    finals = {}
+    # "fp32_xq": fp32 again with x_T rounded to bf16 -- the trajectory's
+    # sensitivity to a bf16-sized input perturbation alone (the seeded-random
+    # U-Net is not a trained denoiser: its sensitivity sets the scale)
+    for dt in ("fp32", "bf16", "fp32_xq"):
+        model, base = _production(dt[:4], P)
+        sp = respace.SpacedDiffusion(use_timesteps=respace.space_timesteps(1000, "ddim50"), betas=base.betas,
+                                     model_mean_type=base.model_mean_type, model_var_type=base.model_var_type,
+                                     loss_type=base.loss_type)
+        sp.mode = "i2i"
+        x0 = x_t.to(torch.bfloat16).float() if dt == "fp32_xq" else x_t
+        if sampler == "ddim":
+            out = sp.ddim_sample_loop(model, tuple(x_t.shape), noise=x0.to(DEV), cond=cond.to(DEV))
+        else:
+            it = iter([z.to(DEV) for z in noises])
+            out = sp.p_sample_loop(model, tuple(x_t.shape), noise=x0.to(DEV), cond=cond.to(DEV), progress=False,
+                                   noise_fn=lambda x: next(it))
+        finals[dt] = out.cpu()
+        del model
+        torch.cuda.empty_cache()
+    img = {k: _image(v) for k, v in finals.items()}
+    res = {}
+    for k in ("bf16", "fp32_xq"):
+        a, b = img[k].double(), img["fp32"].double()
+        sa, sb = finals[k].double(), finals["fp32"].double()
+        res[k] = (float((a - b).norm() / b.norm()), float((a - b).abs().max()), float((a - b).abs().mean()),
+                  float((sa - sb).norm() / sb.norm()))
+        print(f"{sampler} 50-step volume, {k} vs fp32: image rel L2 {res[k][0]:.3e}, max abs {res[k][1]:.3e} "
+              f"(image range [0, 1]), mean abs {res[k][2]:.3e}, subband rel L2 {res[k][3]:.3e}")
+        assert torch.isfinite(a).all()
+    # regression bounds at the measured values (DESIGN.md §4: bf16 does NOT
+    # hold 1e-3 over a trajectory -- each bf16 layer adds ~1e-3 relative error,
+    # 1.5e-2 at the U-Net output, and 50 steps accumulate it; fp32 is the
+    # parity mode): ddpm 0.29 / ddim 0.22 image rel L2 measured
+    assert res["bf16"][0] < 0.4, res
+    assert res["fp32_xq"][0] < 0.15, res
+
+
+def test_fullsize_bf16_error_by_layer():
+    """Where the bf16 error of one forward comes from: every block output of
+    the bf16 U-Net vs the fp32 one (same weights and input, 128^3), rel L2;
+    printed for DESIGN.md §4."""
+    P = ou.random_params(seed=5)
+    cond, x_t, _ = _step_inputs()
+    x = torch.cat([x_t, cond], 1)
+    t = torch.tensor([640])
+    traces = {}
+    outs = {}
+    for dt in ("fp32", "bf16"):
+        model, _ = _production(dt, P)
+        with torch.no_grad():
+            outs[dt] = model(x.to(DEV), t.to(DEV)).cpu()
+        ws = model.plan.workspace(1, N, N, N, DEV)
+        traces[dt] = [None if tt is None else tt.float().cpu() for tt in model.plan.trace_tensors(ws, 1, N, N, N)]
+        del model, ws
+        torch.cuda.empty_cache()
+    rows = []
+    for i, (a, b) in enumerate(zip(traces["bf16"], traces["fp32"])):
+        if a is None or b is None:
+            continue
+        rows.append((i, tuple(b.shape[1:]), float((a.double() - b.double()).norm() / b.double().norm())))
+    for i, shp, e in rows:
+        print(f"block {i:2d} {str(shp):22s} rel L2 {e:.3e}")
+    o = float((outs["bf16"].double() - outs["fp32"].double()).norm() / outs["fp32"].double().norm())
+    print(f"model output rel L2 {o:.3e}")
+    assert o < 5e-2

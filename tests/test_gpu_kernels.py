@@ -35,6 +35,41 @@ def test_dwt_idwt_bitexact_vs_oracle(shape):
     assert (rec - x).abs().max() < 1e-5
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_idwt_from_separate_planes_bitexact(dtype):
+    """IDWT_3D's eight arguments go to the kernel as eight pointers (no stack
+    copy): bit-exact vs the oracle on the same (dtype-rounded) bands."""
+    from cwdm_hip import ops
+    g = torch.Generator().manual_seed(4)
+    bands = [torch.randn(2, 3, 4, 6, 5, generator=g).to(dtype) for _ in range(8)]
+    got = ops.idwt3d_planes([b.to(DEV) for b in bands]).cpu()
+    assert torch.equal(got, haar.idwt3d(*[b.float() for b in bands]))
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 8, 8, 8), (2, 1, 16, 12, 20)])
+def test_prepare_batch_bitexact_vs_oracle(shape):
+    """cwdm_prepare_batch (training_losses front end, gaussian_diffusion.py:1131-1149):
+    the 32-channel model input and the x0 target equal the oracle's DWTs and
+    q_sample bit for bit."""
+    from cwdm_hip import ops
+    from oracle import diffusion as od
+    from guided_diffusion import script_util
+    d = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i")
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"))
+    g = torch.Generator().manual_seed(6)
+    vols = [torch.rand(shape, generator=g) for _ in range(4)]
+    eps = torch.randn(shape, generator=g)
+    t = torch.tensor([0, 999][:shape[0]]) if shape[0] <= 2 else torch.randint(0, 1000, (shape[0],))
+    x_in, x0 = ops.prepare_batch(*[v.to(DEV) for v in vols], eps.to(DEV), d.q_coef_table(DEV), t.to(DEV), 1000)
+    rx0 = haar.dwt_cat(vols[0])
+    cond = torch.cat([haar.dwt_cat(v) for v in vols[1:]], 1)
+    reps = torch.cat(list(haar.dwt3d(eps)), 1)
+    rxt = od.q_sample(tab, rx0, t, reps)
+    assert torch.equal(x0.cpu(), rx0)
+    assert torch.equal(x_in[:, 8:].cpu(), cond)
+    assert torch.equal(x_in[:, :8].cpu(), rxt)
+
+
 def test_dwt_module_api_and_autograd():
     from DWT_IDWT.DWT_IDWT_layer import DWT_3D, IDWT_3D
     x = torch.rand(2, 1, 8, 8, 8, device=DEV, requires_grad=True)
