@@ -1,0 +1,43 @@
+"""Per-launch timeline of one denoising step from a rocprofv3 kernel trace of
+bench.py (the last complete step: between the last two sampler launches).
+usage: python tools/trace_step.py gpurun_out/TAG/trace [--agg]"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def load(d):
+    f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
+    rows = list(csv.DictReader(open(f)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    return rows
+
+
+def short(n):
+    n = n.replace("void ", "").replace("cwdm::", "").replace("(anonymous namespace)::", "")
+    return n.split("(")[0][:60]
+
+
+def main():
+    rows = load(sys.argv[1])
+    samp = [i for i, r in enumerate(rows) if "sampler_kernel" in r["Kernel_Name"]]
+    a, b = samp[-2] + 1, samp[-1] + 1
+    step = rows[a:b]
+    tot = 0.0
+    agg = defaultdict(lambda: [0, 0.0])
+    for i, r in enumerate(step):
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
+        tot += d
+        agg[short(r["Kernel_Name"])][0] += 1
+        agg[short(r["Kernel_Name"])][1] += d
+        if "--agg" not in sys.argv:
+            print(f"{d:9.1f} {i:4d} {short(r['Kernel_Name'])} grid={r.get('Grid_Size', '')}")
+    print(f"total {tot:.1f} us over {len(step)} launches; wall {(int(step[-1]['End_Timestamp']) - int(step[0]['Start_Timestamp'])) / 1000:.1f} us")
+    for k, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print(f"{t:9.1f} us {n:4d}x  {k}")
+
+
+if __name__ == "__main__":
+    main()
