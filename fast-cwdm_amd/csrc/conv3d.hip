@@ -24,9 +24,20 @@ extern template int launch_conv<float, 32, 4, 2, 2>(const ConvParams&, hipStream
 extern template int launch_conv<float, 16, 4, 4, 2>(const ConvParams&, hipStream_t);
 extern template int launch_conv<float, 8, 8, 4, 2>(const ConvParams&, hipStream_t);
 // ---- weight packing: OIDHW fp32 -> [ct][chunk][tap][n][2 quads, swizzled] ----
+// stride-2 conv as a stride-1 conv over the space-to-depth input (stride2.hip):
+// expanded weight We[co][ph ci0 + ci][t] of w[co][ci][k] (ci0 original input channels)
+__device__ __forceinline__ int s2_k(int t, int p) { return t == 1 ? 1 + p : ((t == 0 && p == 1) ? 0 : -1); }
+__device__ __forceinline__ float s2_weight(const float* w, int ci0, int co, int ci_e, int t) {
+  const int ph = ci_e / ci0, ci = ci_e % ci0;
+  const int kz = s2_k(t / 9, ph >> 2), ky = s2_k((t / 3) % 3, (ph >> 1) & 1), kx = s2_k(t % 3, ph & 1);
+  if (kz < 0 || ky < 0 || kx < 0) return 0.f;
+  return w[((long long)co * ci0 + ci) * 27 + (kz * 3 + ky) * 3 + kx];
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, int cout, int cin, int ntaps, int NT,
-                                                   int nct, T* __restrict__ out, int transpose, int cin_real) {
+                                                   int nct, T* __restrict__ out, int transpose, int cin_real,
+                                                   int s2_ci0) {
   constexpr int CK = ConvTr<T>::CK, EPQ = ConvTr<T>::EPQ;
   const int nch = cin / CK;
   const long long total = (long long)nct * nch * ntaps * NT * CK;
@@ -48,7 +59,8 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, 
   // transpose: pack the input-gradient conv of a (cin -> cout) conv, i.e. weights
   // W'[co'=ci][ci'=co][tap] = W[co][ci][ntaps-1-tap] (w is then cin x cout OIDHW)
   if (co < cout && ci < cin_real) {
-    if (transpose) v = w[((long long)ci * cout + co) * ntaps + (ntaps - 1 - tap)];
+    if (s2_ci0) v = transpose ? s2_weight(w, s2_ci0, ci, co, ntaps - 1 - tap) : s2_weight(w, s2_ci0, co, ci, tap);
+    else if (transpose) v = w[((long long)ci * cout + co) * ntaps + (ntaps - 1 - tap)];
     else v = w[((long long)co * cin + ci) * ntaps + tap];
   }
   out[i] = Elem<T>::from_f(v);
@@ -91,11 +103,18 @@ extern "C" int64_t cwdm_conv3d_packed_bytes(int cout, int cin, int ksize, int dt
 }
 
 static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, void* packed, int transpose,
-                     cwdm_stream_t stream);
+                     cwdm_stream_t stream, int s2_ci0 = 0);
 
 extern "C" int cwdm_conv3d_pack(const float* w, int cout, int cin, int ksize, int dtype, void* packed,
                                 cwdm_stream_t stream) {
   return pack_impl(w, cout, cin, ksize, dtype, packed, 0, stream);
+}
+
+extern "C" int cwdm_conv3d_pack_s2(const float* w, int cout, int cin, int dtype, void* packed, int transpose,
+                                   cwdm_stream_t stream) {
+  // forward: a (cout -> 8 cin) conv over the space-to-depth input; transpose: its dgrad (8 cin outputs)
+  return transpose ? pack_impl(w, 8 * cin, cout, 3, dtype, packed, 1, stream, cin)
+                   : pack_impl(w, cout, 8 * cin, 3, dtype, packed, 0, stream, cin);
 }
 
 extern "C" int cwdm_conv3d_pack_dgrad(const float* w, int cout, int cin, int ksize, int dtype, void* packed,
@@ -107,7 +126,7 @@ extern "C" int cwdm_conv3d_pack_dgrad(const float* w, int cout, int cin, int ksi
 }
 
 static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, void* packed, int transpose,
-                     cwdm_stream_t stream) {
+                     cwdm_stream_t stream, int s2_ci0) {
   CWDM_REQUIRE(w && packed, CWDM_E_INVALID, "cwdm_conv3d_pack: null pointer");
   CWDM_REQUIRE(ksize == 1 || ksize == 3, CWDM_E_UNSUPPORTED, "cwdm_conv3d_pack: kernel size must be 1 or 3");
   CWDM_REQUIRE(dtype == CWDM_F32 || dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_conv3d_pack: bad dtype");
@@ -123,10 +142,10 @@ static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, vo
   dim3 grid((unsigned)ceil_div(total, 256));
   if (dtype == CWDM_BF16)
     hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, w, cout, cin, ntaps, NT, nct,
-                       reinterpret_cast<bf16_t*>(packed), transpose, cin_real);
+                       reinterpret_cast<bf16_t*>(packed), transpose, cin_real, s2_ci0);
   else
     hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, w, cout, cin, ntaps, NT, nct,
-                       reinterpret_cast<float*>(packed), transpose, cin_real);
+                       reinterpret_cast<float*>(packed), transpose, cin_real, s2_ci0);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }

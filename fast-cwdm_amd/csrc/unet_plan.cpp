@@ -65,19 +65,25 @@ struct ConvStep {
   int level;                    // output level
   bool stats;
   int skip_conv = -1;           // conv1 of a block with a 1x1 skip: index of the block's conv2
+  int s2 = 0;                   // stride-2 conv (Downsample.op) over a space-to-depth input: cin_a = 8 x its channels
+};
+
+struct S2dStep {  // space-to-depth of a Downsample conv's input (stride2.hip)
+  int src, out, level_out, channels;
 };
 
 struct PoolStep {  // down-ResBlock pre-pass (cwdm_gn_silu_pool)
   int src, ss_id, out_h, out_x, level_out, channels;
 };
 
-struct Step { int kind; int idx; };  // kind 0 = gn, 1 = conv, 2 = pool pre-pass
+struct Step { int kind; int idx; };  // kind 0 = gn, 1 = conv, 2 = pool pre-pass, 3 = space-to-depth
 
 // one ResBlock, for the backward (reverse order) and the gradient segments
 struct Block {
   int g1, pool, c1, g2, c2;   // step indices (pool = -1 unless down)
   int x0, x1;                 // input tensors (x1 = -1 unless decoder concat)
-  int updown;                 // 0 none, 1 up, 2 down
+  int updown;                 // 0 none, 1 up, 2 down; layers without a ResBlock (resblock_updown=False):
+                              // 3 Downsample stride-2 conv (c1, pool = its S2dStep), 4 Upsample nearest + conv (c1)
   int p_begin, p_end;         // parameter index range
   int emb_k;                  // index into emb_rows_*
 };
@@ -92,6 +98,7 @@ struct cwdm_unet {
   std::vector<GnStep> gns;
   std::vector<ConvStep> convs;
   std::vector<PoolStep> pools;
+  std::vector<S2dStep> s2ds;
   std::vector<Step> steps;
   std::vector<int> trace;         // tensor id per topology block (-1 = final output)
   std::vector<int> trace_level;
@@ -243,6 +250,37 @@ void build(cwdm_unet* u) {
     return o;
   };
 
+  // resblock_updown=False: Downsample(use_conv=True) = a stride-2 conv, run as
+  // a stride-1 conv over the space-to-depth input; Upsample(use_conv=True) =
+  // nearest x2 folded into the conv's gather (a_mode 1).  unet.py:40-100, :606-612, :700-706.
+  auto resample_layer = [&](const std::string& p, int x, int down) {
+    Block blk{};
+    blk.p_begin = (int)u->params.size();
+    blk.x0 = x; blk.x1 = -1; blk.updown = down ? 3 : 4; blk.pool = -1; blk.g1 = blk.g2 = blk.c2 = -1; blk.emb_k = -1;
+    const int lin = u->tensors[x].level, chn = u->tensors[x].channels;
+    const int lout = down ? lin + 1 : lin - 1;
+    ConvStep cs{};
+    conv_params(p, chn, chn, 3, &cs.w_p, &cs.b_p);
+    cs.a1 = -1; cs.gn = -1; cs.sb0 = cs.sb1 = -1; cs.ws_p = cs.wsb_p = -1; cs.cin_b = 0;
+    cs.bias_kind = 0; cs.res = -1; cs.rmode = -1; cs.cout = chn; cs.level = lout; cs.stats = true;
+    if (down) {
+      S2dStep sd{x, new_tensor(lout, 8 * chn), lout, chn};
+      u->s2ds.push_back(sd);
+      u->steps.push_back({3, (int)u->s2ds.size() - 1});
+      blk.pool = (int)u->s2ds.size() - 1;
+      cs.a0 = sd.out; cs.amode = 0; cs.cin_a = 8 * chn; cs.s2 = 1;
+    } else {
+      cs.a0 = x; cs.amode = 1; cs.cin_a = chn;
+    }
+    const int o = cs.out = new_tensor(lout, chn);
+    u->convs.push_back(cs);
+    u->steps.push_back({1, (int)u->convs.size() - 1});
+    blk.c1 = (int)u->convs.size() - 1;
+    blk.p_end = (int)u->params.size();
+    u->blocks.push_back(blk);
+    return o;
+  };
+
   int ch = mc, idx = 1;
   const int nl = c.num_levels;
   for (int l = 0; l < nl; ++l) {
@@ -255,7 +293,8 @@ void build(cwdm_unet* u) {
       ++idx;
     }
     if (l != nl - 1) {
-      h = resblock("input_blocks." + std::to_string(idx) + ".0", h, -1, ch, 2);
+      const std::string p = "input_blocks." + std::to_string(idx) + ".0";
+      h = c.resblock_updown ? resblock(p, h, -1, ch, 2) : resample_layer(p + ".op", h, 1);
       ++level;
       stack.push_back(h);
       u->trace.push_back(h); u->trace_level.push_back(level);
@@ -276,7 +315,8 @@ void build(cwdm_unet* u) {
       ch = mc * mult;
       u->trace.push_back(h); u->trace_level.push_back(level);
       if (l && i == c.num_res_blocks) {
-        h = resblock("output_blocks." + std::to_string(idx) + ".1", h, -1, ch, 1);
+        const std::string p = "output_blocks." + std::to_string(idx) + ".1";
+        h = c.resblock_updown ? resblock(p, h, -1, ch, 1) : resample_layer(p + ".conv", h, 0);
         --level;
         u->trace.push_back(h); u->trace_level.push_back(level);
       }
@@ -512,7 +552,12 @@ extern "C" int cwdm_unet_pack(const cwdm_unet* u, const float* const* P, void* p
     if ((rc = launch_vec_add(P[u->emb_rows_b[k]], P[u->emb_rows_cb[k]], eb + o, n, s))) return rc;
   }
   for (const auto& cs : u->convs) {
-    if ((rc = cwdm_conv3d_pack(P[cs.w_p], cs.cout, cs.cin_a, 3, u->cfg.dtype, base + cs.w_off, stream))) return rc;
+    if (cs.s2) {
+      if ((rc = cwdm_conv3d_pack_s2(P[cs.w_p], cs.cout, cs.cin_a / 8, u->cfg.dtype, base + cs.w_off, 0, stream)))
+        return rc;
+    } else if ((rc = cwdm_conv3d_pack(P[cs.w_p], cs.cout, cs.cin_a, 3, u->cfg.dtype, base + cs.w_off, stream))) {
+      return rc;
+    }
     if (cs.ws_p >= 0 &&
         (rc = cwdm_conv3d_pack(P[cs.ws_p], cs.cout, cs.cin_b, 1, u->cfg.dtype, base + cs.wsk_off, stream)))
       return rc;
@@ -541,7 +586,7 @@ extern "C" double cwdm_unet_flops(const cwdm_unet* u, int64_t B, int64_t D, int6
   double f = 0;
   for (const auto& cs : u->convs) {
     const double v = (double)B * (D >> cs.level) * (H >> cs.level) * (W >> cs.level);
-    f += 2.0 * v * cs.cout * (27.0 * cs.cin_a + cs.cin_b);
+    f += 2.0 * v * cs.cout * (27.0 * (cs.s2 ? cs.cin_a / 8 : cs.cin_a) + cs.cin_b);  // algorithmic (stride-2: 27 C taps)
   }
   return f;
 }
@@ -601,6 +646,14 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
       if ((rc = cwdm_gn_silu_pool(tptr(ps.src), ps.channels, reinterpret_cast<const float*>(wb + L.ss_off[ps.ss_id]),
                                   B, D >> lv, H >> lv, W >> lv, u->cfg.dtype, wb + L.t_off[ps.out_h],
                                   wb + L.t_off[ps.out_x], stream)))
+        return rc;
+      continue;
+    }
+    if (st.kind == 3) {
+      const auto& sd = u->s2ds[st.idx];
+      const int lv = sd.level_out;
+      if ((rc = cwdm_space_to_depth(tptr(sd.src), sd.channels, B, D >> lv, H >> lv, W >> lv, u->cfg.dtype,
+                                    wb + L.t_off[sd.out], 1, 0, stream)))
         return rc;
       continue;
     }
@@ -720,7 +773,7 @@ namespace {
 
 struct GLayout {
   std::vector<int64_t> g_off;
-  int64_t tmp, dout, deb, dsil, gnws, gnws_bytes, split, split_bytes, wgws, total;
+  int64_t tmp, dout, deb, dsil, gnws, gnws_bytes, split, split_bytes, wgws, dwe, total;
 };
 
 int ckpad(const cwdm_unet* u, int c) {
@@ -778,6 +831,10 @@ GLayout glayout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) 
   G.split_bytes = split;
   G.split = take(split);
   G.wgws = take(wgws);
+  int64_t dwe = 0;   // expanded weight gradient of a stride-2 conv before folding
+  for (const auto& cs : u->convs)
+    if (cs.s2) dwe = std::max(dwe, (int64_t)cs.cout * cs.cin_a * 27 * 4);
+  G.dwe = take(dwe);
   G.total = off;
   return G;
 }
@@ -792,7 +849,10 @@ extern "C" int cwdm_unet_pack_bwd(const cwdm_unet* u, const float* const* P, voi
   int rc;
   for (size_t i = 0; i < u->convs.size(); ++i) {
     const auto& cs = u->convs[i];
-    if (u->dg_off[i] >= 0 &&
+    if (u->dg_off[i] >= 0 && cs.s2 &&
+        (rc = cwdm_conv3d_pack_s2(P[cs.w_p], cs.cout, cs.cin_a / 8, u->cfg.dtype, base + u->dg_off[i], 1, stream)))
+      return rc;
+    if (u->dg_off[i] >= 0 && !cs.s2 &&
         (rc = cwdm_conv3d_pack_dgrad(P[cs.w_p], cs.cout, cs.cin_a, 3, u->cfg.dtype, base + u->dg_off[i], stream)))
       return rc;
     if (u->dgs_off[i] >= 0 &&
@@ -829,7 +889,7 @@ extern "C" double cwdm_unet_backward_flops(const cwdm_unet* u, int64_t B, int64_
   for (size_t i = 0; i < u->convs.size(); ++i) {
     const auto& cs = u->convs[i];
     const double v = (double)B * (D >> cs.level) * (H >> cs.level) * (W >> cs.level);
-    const double fwd = 2.0 * v * cs.cout * (27.0 * cs.cin_a + cs.cin_b);
+    const double fwd = 2.0 * v * cs.cout * (27.0 * (cs.s2 ? cs.cin_a / 8 : cs.cin_a) + cs.cin_b);
     f += i == 0 ? fwd : 2 * fwd;  // wgrad (+ dgrad)
   }
   return f;
@@ -936,6 +996,35 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
         return rc;
       if ((rc = dgrad(u->head_c, d16))) return rc;
       if ((rc = gn_bwd(u->head_g, hg.src0, -1, 0))) return rc;
+      continue;
+    }
+    if (seg <= nb && u->blocks[nb - seg].updown >= 3) {
+      // Downsample stride-2 conv / Upsample nearest + conv (resblock_updown=False)
+      const Block& bk = u->blocks[nb - seg];
+      const auto& cs = u->convs[bk.c1];
+      const int o = cs.out, xt = bk.x0;
+      const int chn = u->tensors[xt].channels, lx = u->tensors[xt].level;
+      if ((rc = cwdm_channel_sum(grd(o), dt, B, vox(cs.level), cs.cout, cs.cout, nullptr, 0, GR(cs.b_p), nullptr,
+                                 stream)))
+        return rc;
+      if (bk.updown == 4) {
+        if ((rc = wgrad(cs.level, 3, act(xt), chn, nullptr, 0, 1, nullptr, grd(o), cs.cout, cs.cout, GR(cs.w_p))))
+          return rc;
+        if ((rc = dgrad(bk.c1, grd(o)))) return rc;
+        if ((rc = cwdm_resample_add(grd(xt), tmp, chn, B, D >> lx, H >> lx, W >> lx, 1, take_acc(xt), dt, stream)))
+          return rc;
+      } else {
+        const auto& sd = u->s2ds[bk.pool];
+        float* dwe = reinterpret_cast<float*>(gb + G.dwe);
+        CWDM_HIP(hipMemsetAsync(dwe, 0, (int64_t)cs.cout * cs.cin_a * 27 * 4, s));
+        if ((rc = wgrad(cs.level, 3, act(sd.out), cs.cin_a, nullptr, 0, 0, nullptr, grd(o), cs.cout, cs.cout, dwe)))
+          return rc;
+        if ((rc = cwdm_conv3d_s2_fold_dw(dwe, cs.cout, chn, GR(cs.w_p), 1, stream))) return rc;
+        if ((rc = dgrad(bk.c1, grd(o)))) return rc;
+        if ((rc = cwdm_space_to_depth(tmp, chn, B, D >> cs.level, H >> cs.level, W >> cs.level, dt, grd(xt), 0,
+                                      take_acc(xt), stream)))
+          return rc;
+      }
       continue;
     }
     if (seg <= nb) {

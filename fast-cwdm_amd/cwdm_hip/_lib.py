@@ -82,6 +82,7 @@ class UNetConfig(ctypes.Structure):
         ("out_channels", ctypes.c_int), ("num_res_blocks", ctypes.c_int),
         ("num_levels", ctypes.c_int), ("channel_mult", ctypes.c_int * 8),
         ("num_groups", ctypes.c_int), ("dtype", ctypes.c_int),
+        ("resblock_updown", ctypes.c_int),
     ]
 
 
@@ -109,6 +110,10 @@ _PROTOS = {
     "cwdm_conv3d_pack": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]),
     "cwdm_conv3d_pack_dgrad": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]),
     "cwdm_conv3d_parts": (i64, [ctypes.c_int, i64, i64, i64, ctypes.c_int]),
+    "cwdm_space_to_depth": (ctypes.c_int, [vp, ctypes.c_int, i64, i64, i64, i64, ctypes.c_int, vp, ctypes.c_int,
+                                           ctypes.c_int, vp]),
+    "cwdm_conv3d_pack_s2": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp]),
+    "cwdm_conv3d_s2_fold_dw": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp]),
     "cwdm_conv3d_forward": (ctypes.c_int, [ctypes.POINTER(ConvDesc), vp]),
     "cwdm_conv3d_workspace_bytes": (i64, [ctypes.POINTER(ConvDesc)]),
     "cwdm_gn_finalize": (ctypes.c_int, [vp, i64, ctypes.c_int, vp, i64, ctypes.c_int, vp, vp, ctypes.c_int, i64, i64,

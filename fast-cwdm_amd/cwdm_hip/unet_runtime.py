@@ -26,7 +26,7 @@ def parse_dtype(d):
 
 class UNetPlan:
     def __init__(self, in_channels, model_channels, out_channels, num_res_blocks, channel_mult, num_groups,
-                 dtype="fp32"):
+                 dtype="fp32", resblock_updown=True):
         cfg = _lib.UNetConfig()
         cfg.in_channels, cfg.model_channels, cfg.out_channels = in_channels, model_channels, out_channels
         cfg.num_res_blocks, cfg.num_levels = num_res_blocks, len(channel_mult)
@@ -36,6 +36,7 @@ class UNetPlan:
             cfg.channel_mult[i] = int(m)
         cfg.num_groups = num_groups
         cfg.dtype = parse_dtype(dtype)
+        cfg.resblock_updown = 1 if resblock_updown else 0
         self.dtype = cfg.dtype
         self.torch_dtype = TORCH_DT[cfg.dtype]
         self.num_levels = len(channel_mult)

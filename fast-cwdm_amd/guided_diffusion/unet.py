@@ -10,8 +10,10 @@ compute dtype (``compute_dtype`` = "fp32" for reference numerics, "bf16" for
 throughput); parameters stay fp32 masters and are re-packed when they change.
 
 Supported configuration family: the one run.sh uses (dims=3, no attention,
-resblock_updown=True, use_scale_shift_norm=False, additive_skips=False,
-resample_2d=False).  Anything else raises NotImplementedError at construction.
+use_scale_shift_norm=False, additive_skips=False, resample_2d=False), with
+either resblock_updown=True (run.sh: ResBlock down/up) or resblock_updown=False
+with conv_resample=True (Downsample = stride-2 Conv3d, Upsample = nearest x2 +
+Conv3d; unet.py:40-100).  Anything else raises NotImplementedError.
 """
 import math
 import os
@@ -70,8 +72,8 @@ class UNetModel(nn.Module):
             unsupported.append("attention blocks")
         if bottleneck_attention:
             unsupported.append("bottleneck_attention=True")
-        if not resblock_updown:
-            unsupported.append("resblock_updown=False")
+        if not resblock_updown and not conv_resample:
+            unsupported.append("resblock_updown=False with conv_resample=False (parameter-free pool / nearest layers)")
         if use_scale_shift_norm:
             unsupported.append("use_scale_shift_norm=True")
         if additive_skips:
@@ -98,6 +100,7 @@ class UNetModel(nn.Module):
         self.use_checkpoint = use_checkpoint
         self.num_heads = num_heads
         self.num_groups = num_groups
+        self.resblock_updown = bool(resblock_updown)
         self.bottleneck_attention = bottleneck_attention
         self.additive_skips = additive_skips
         self.decoder_device_thresh = decoder_device_thresh
@@ -183,7 +186,8 @@ class UNetModel(nn.Module):
         key = str(dtype)
         if key not in self._plans:
             self._plans[key] = UNetPlan(self.in_channels, self.model_channels, self.out_channels,
-                                        self.num_res_blocks, self.channel_mult, self.num_groups, dtype)
+                                        self.num_res_blocks, self.channel_mult, self.num_groups, dtype,
+                                        resblock_updown=self.resblock_updown)
         return self._plans[key]
 
     @property

@@ -226,6 +226,23 @@ int cwdm_conv3d_pack(const float* w_oidhw, int cout, int cin, int ksize, int dty
  * K chunk (16 bf16 / 8 fp32): size cwdm_conv3d_packed_bytes(cin, pad(cout), ksize, dtype). */
 int cwdm_conv3d_pack_dgrad(const float* w_oidhw, int cout, int cin, int ksize, int dtype,
                            void* packed, cwdm_stream_t stream);
+/* Stride-2 Conv3d (Downsample(use_conv=True), guided_diffusion/unet.py:73-100:
+ * conv_nd(3, C, C_out, 3, stride=2, padding=1)) as a stride-1 conv over the
+ * space-to-depth input X'[b][o][ph*C + c] = x[b][2o + p][c], ph = 4 pz + 2 py + px
+ * (fast-cwdm_amd/csrc/stride2.hip).
+ * cwdm_space_to_depth: to_depth 1: x (B, 2d, 2h, 2w, C) -> X' (B, d, h, w, 8C);
+ *   to_depth 0: the inverse (depth-to-space, the dgrad's last step), accumulate
+ *   adds into the fine-grid output.  NDHWC, C * esize a multiple of 16 bytes.
+ * cwdm_conv3d_pack_s2: packs w (cout, cin, 3,3,3) fp32 as that (cout, 8 cin)
+ *   stride-1 conv (transpose 0; cwdm_conv3d_packed_bytes(cout, 8 cin, 3, dtype))
+ *   or as its dgrad conv (transpose 1; packed_bytes(8 cin, pad(cout), 3)).
+ * cwdm_conv3d_s2_fold_dw: dw (cout, cin, 27) (+)= the 27 original taps of the
+ *   expanded stride-1 weight gradient dwe (cout, 8 cin, 27). */
+int cwdm_space_to_depth(const void* x, int C, int64_t B, int64_t d, int64_t h, int64_t w, int dtype, void* out,
+                        int to_depth, int accumulate, cwdm_stream_t stream);
+int cwdm_conv3d_pack_s2(const float* w_oidhw, int cout, int cin, int dtype, void* packed, int transpose,
+                        cwdm_stream_t stream);
+int cwdm_conv3d_s2_fold_dw(const float* dwe, int cout, int cin, float* dw, int accumulate, cwdm_stream_t stream);
 int64_t cwdm_conv3d_parts(int dtype, int64_t D, int64_t H, int64_t W, int cout);
 /* Workspace that lets cwdm_conv3d_forward split K over workgroups on small
  * grids (0 when it would not split; without it the launch runs unsplit). */
@@ -345,6 +362,8 @@ typedef struct {
   int channel_mult[8];
   int num_groups;
   int dtype;          /* storage/compute dtype of activations and weights */
+  int resblock_updown; /* 1: ResBlock(down/up=True) resampling (run.sh); 0: Downsample(use_conv=True) stride-2
+                          conv / Upsample(use_conv=True) nearest + conv (unet.py:40-100, conv_resample) */
 } cwdm_unet_config;
 
 int cwdm_unet_create(const cwdm_unet_config* cfg, cwdm_unet** plan);

@@ -17,12 +17,15 @@ import torch.nn.functional as F
 
 
 def topology(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2,
-             channel_mult=(1, 2, 2, 4, 4)):
+             channel_mult=(1, 2, 2, 4, 4), resblock_updown=True):
     """List of blocks in execution order.
 
-    Each entry is a dict: kind in {"conv_in", "res", "out"}, key prefix,
-    cin/cout, updown in {None, "down", "up"}, and for decoder blocks
-    ``concat`` = channels popped from the skip stack.
+    Each entry is a dict: kind in {"conv_in", "res", "down", "up", "out"},
+    key prefix, cin/cout, updown in {None, "down", "up"}, and for decoder
+    blocks ``concat`` = channels popped from the skip stack.  With
+    resblock_updown=False the resampling layers are Downsample(use_conv=True)
+    (kind "down": stride-2 Conv3d, prefix ...op) and Upsample(use_conv=True)
+    (kind "up": nearest x2 + Conv3d, prefix ...conv), unet.py:40-100, :606-612, :700-706.
     """
     blocks = [dict(kind="conv_in", prefix="input_blocks.0.0", cin=in_channels, cout=model_channels)]
     chans = [model_channels]
@@ -36,7 +39,11 @@ def topology(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2
             chans.append(ch)
             idx += 1
         if level != len(channel_mult) - 1:
-            blocks.append(dict(kind="res", prefix=f"input_blocks.{idx}.0", cin=ch, cout=ch, updown="down", push=True))
+            if resblock_updown:
+                blocks.append(dict(kind="res", prefix=f"input_blocks.{idx}.0", cin=ch, cout=ch, updown="down",
+                                   push=True))
+            else:
+                blocks.append(dict(kind="down", prefix=f"input_blocks.{idx}.0.op", cin=ch, cout=ch, push=True))
             chans.append(ch)
             idx += 1
     blocks.append(dict(kind="res", prefix="middle_block.0", cin=ch, cout=ch, updown=None))
@@ -50,21 +57,24 @@ def topology(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2
                                updown=None, pop=ich))
             ch = mid
             if level and i == num_res_blocks:
-                blocks.append(dict(kind="res", prefix=f"output_blocks.{idx}.1", cin=ch, cout=ch, updown="up"))
+                if resblock_updown:
+                    blocks.append(dict(kind="res", prefix=f"output_blocks.{idx}.1", cin=ch, cout=ch, updown="up"))
+                else:
+                    blocks.append(dict(kind="up", prefix=f"output_blocks.{idx}.1.conv", cin=ch, cout=ch))
             idx += 1
     blocks.append(dict(kind="out", prefix="out", cin=ch, cout=out_channels))
     return blocks
 
 
 def param_shapes(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2,
-                 channel_mult=(1, 2, 2, 4, 4)):
+                 channel_mult=(1, 2, 2, 4, 4), resblock_updown=True):
     """Ordered (name, shape) list matching the reference state_dict."""
     ted = 4 * model_channels
     out = [("time_embed.0.weight", (ted, model_channels)), ("time_embed.0.bias", (ted,)),
            ("time_embed.2.weight", (ted, ted)), ("time_embed.2.bias", (ted,))]
-    for b in topology(in_channels, model_channels, out_channels, num_res_blocks, channel_mult):
+    for b in topology(in_channels, model_channels, out_channels, num_res_blocks, channel_mult, resblock_updown):
         p, ci, co = b["prefix"], b["cin"], b["cout"]
-        if b["kind"] == "conv_in":
+        if b["kind"] in ("conv_in", "down", "up"):
             out += [(p + ".weight", (co, ci, 3, 3, 3)), (p + ".bias", (co,))]
         elif b["kind"] == "res":
             out += [(p + ".in_layers.0.weight", (ci,)), (p + ".in_layers.0.bias", (ci,)),
@@ -134,7 +144,7 @@ def _resblock(P, p, x, emb, groups, updown):
 
 
 def unet_forward(P, x, t, model_channels=64, num_groups=32, in_channels=32, out_channels=8,
-                 num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4), trace=None):
+                 num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4), trace=None, resblock_updown=True):
     """UNetModel.forward (unet.py:754-800).  ``trace`` (optional list)
     collects every block output for layer-level parity tests."""
     emb = timestep_embedding(t, model_channels)
@@ -142,11 +152,17 @@ def unet_forward(P, x, t, model_channels=64, num_groups=32, in_channels=32, out_
     emb = F.linear(F.silu(emb), P["time_embed.2.weight"], P["time_embed.2.bias"])
     hs = []
     h = x
-    for b in topology(in_channels, model_channels, out_channels, num_res_blocks, channel_mult):
+    for b in topology(in_channels, model_channels, out_channels, num_res_blocks, channel_mult, resblock_updown):
         p = b["prefix"]
         if b["kind"] == "conv_in":
             h = F.conv3d(h, P[p + ".weight"], P[p + ".bias"], padding=1)
             hs.append(h)
+        elif b["kind"] == "down":     # Downsample(use_conv=True): conv_nd(3, C, C, 3, stride=2, padding=1)
+            h = F.conv3d(h, P[p + ".weight"], P[p + ".bias"], stride=2, padding=1)
+            hs.append(h)
+        elif b["kind"] == "up":       # Upsample(use_conv=True): nearest x2, then conv_nd(3, C, C, 3, padding=1)
+            h = F.conv3d(F.interpolate(h, scale_factor=2, mode="nearest"), P[p + ".weight"], P[p + ".bias"],
+                         padding=1)
         elif b["kind"] == "res":
             if "pop" in b:
                 h = torch.cat([h, hs.pop()], dim=1)

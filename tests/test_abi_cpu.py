@@ -82,3 +82,36 @@ def test_conv_pack_sizes():
     assert L.cwdm_conv3d_packed_bytes(64, 64, 3, _lib.CWDM_BF16) == 27 * 64 * 64 * 2
     assert L.cwdm_conv3d_packed_bytes(8, 64, 3, _lib.CWDM_F32) == 27 * 32 * 64 * 4   # cout padded to 32
     assert L.cwdm_conv3d_packed_bytes(64, 24, 3, _lib.CWDM_BF16) == -1              # 24 % 16 != 0
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_plan_param_contract_resblock_updown_false(dtype):
+    """resblock_updown=False (Downsample stride-2 conv / Upsample nearest+conv,
+    reference unet.py:40-100): names and shapes of the plan == the oracle's."""
+    from cwdm_hip.unet_runtime import UNetPlan
+    cfg = dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4))
+    plan = UNetPlan(32, 64, 8, 2, (1, 2, 2, 4, 4), 32, dtype, resblock_updown=False)
+    want = ou.param_shapes(resblock_updown=False, **cfg)
+    assert [(n, tuple(s)) for n, s in plan.param_specs] == [(n, tuple(s)) for n, s in want]
+    names = [n for n, _ in want]
+    assert "input_blocks.3.0.op.weight" in names and "output_blocks.2.1.conv.weight" in names
+    # algorithmic FLOPs: the stride-2 convs count their 27 C taps, not the expanded kernel
+    f_true = plan.flops(1, 32, 32, 32)
+    import torch.nn.functional as F  # noqa: F401
+    down = sum(2 * (32 >> (k + 1)) ** 3 * c * 27 * c for k, c in enumerate((64, 128, 128, 256)))
+    up_ref = UNetPlan(32, 64, 8, 2, (1, 2, 2, 4, 4), 32, dtype).flops(1, 32, 32, 32)
+    assert f_true < up_ref and f_true > 0 and down > 0
+
+
+def test_unet_model_accepts_resblock_updown_false():
+    from guided_diffusion.unet import UNetModel
+    m = UNetModel(image_size=64, in_channels=32, model_channels=32, out_channels=8, num_res_blocks=1,
+                  attention_resolutions=(), channel_mult=(1, 2), dims=3, resblock_updown=False,
+                  bottleneck_attention=False, resample_2d=False, num_groups=8)
+    sd = m.state_dict()
+    assert sd["input_blocks.2.0.op.weight"].shape == (32, 32, 3, 3, 3)
+    assert sd["output_blocks.1.1.conv.weight"].shape == (64, 64, 3, 3, 3)
+    with pytest.raises(NotImplementedError):
+        UNetModel(image_size=64, in_channels=32, model_channels=32, out_channels=8, num_res_blocks=1,
+                  attention_resolutions=(), channel_mult=(1, 2), dims=3, resblock_updown=False, conv_resample=False,
+                  bottleneck_attention=False, resample_2d=False, num_groups=8)

@@ -516,3 +516,39 @@ def test_production_unet_backward_bf16_close_to_fp32():
     print("bf16 out rel", rel_err(out, ref_out), "worst grads", top)
     assert rel_err(out, ref_out) < 5e-2
     assert top[0][1] < 8e-2, top
+
+
+@pytest.mark.parametrize("k", [0, 1], ids=["tiny", "runsh"])
+def test_unet_resblock_updown_false_backward_vs_oracle_autograd(k):
+    """Backward of the stride-2 Downsample conv (expanded-weight wgrad folded
+    back onto the 27 taps, dgrad + depth-to-space) and of the Upsample conv
+    (wgrad on the nearest-x2 input, dgrad + the nearest adjoint), whole U-Net,
+    fp32: every gradient within 1e-3 rel-L2 of the oracle's autograd."""
+    from guided_diffusion.unet import UNetModel
+    cfgs = [(dict(in_channels=32, model_channels=32, out_channels=8, num_res_blocks=1, channel_mult=(1, 2)), 8,
+             (16, 16, 16)),
+            (dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4)),
+             32, (16, 32, 32))]
+    cfg, G, grid = cfgs[k]
+    P = ou.random_params(seed=27, resblock_updown=False, **cfg)
+    m = UNetModel(image_size=2 * grid[0], in_channels=cfg["in_channels"], model_channels=cfg["model_channels"],
+                  out_channels=cfg["out_channels"], num_res_blocks=cfg["num_res_blocks"], attention_resolutions=(),
+                  channel_mult=cfg["channel_mult"], dims=3, resblock_updown=False, bottleneck_attention=False,
+                  resample_2d=False, num_groups=G, compute_dtype="fp32")
+    m.load_state_dict(P)
+    m.to(DEV)
+    g = torch.Generator().manual_seed(28)
+    x = torch.randn(2, 32, *grid, generator=g)
+    t = torch.tensor([9, 444])
+    R = torch.randn(2, 8, *grid, generator=g)
+    out = m(x.to(DEV), t.to(DEV))
+    (out * R.to(DEV)).sum().backward()
+    Pr = {kk: v.clone().requires_grad_(True) for kk, v in P.items()}
+    ref = ou.unet_forward(Pr, x, t, num_groups=G, resblock_updown=False, **cfg)
+    (ref * R).sum().backward()
+    assert rel_err(out.detach(), ref.detach()) < 1e-3
+    worst = {n: float((p.grad.double().cpu() - Pr[n].grad.double()).norm() / Pr[n].grad.double().norm().clamp_min(1e-30))
+             for n, p in m.named_parameters()}
+    bad = {n: v for n, v in worst.items() if v > 1e-3}
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:8]
+    assert any(".op." in n for n in worst) and any(".conv." in n for n in worst)

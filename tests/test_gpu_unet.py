@@ -296,3 +296,40 @@ def test_training_losses_forward_vs_oracle():
     assert rel_err(out, rout) < 1e-3
     assert rel_err(out_idwt, ridwt) < 1e-3
     assert rel_err(terms["mse_wav"], rterms["mse_wav"]) < 1e-3
+
+
+S2_CFGS = [(dict(in_channels=32, model_channels=32, out_channels=8, num_res_blocks=1, channel_mult=(1, 2)), 8,
+            (16, 16, 16)),
+           (dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4)),
+            32, (16, 32, 32))]
+
+
+@pytest.mark.parametrize("k", [0, 1], ids=["tiny", "runsh"])
+@pytest.mark.parametrize("dtype,tol", [("fp32", 1e-3), ("bf16", 6e-2)])
+def test_unet_resblock_updown_false_forward_vs_oracle(k, dtype, tol):
+    """resblock_updown=False: Downsample(use_conv=True) = stride-2 Conv3d (run as
+    a stride-1 conv over the space-to-depth input) and Upsample(use_conv=True) =
+    nearest x2 + Conv3d (unet.py:40-100), whole U-Net vs the oracle."""
+    from guided_diffusion.unet import UNetModel
+    cfg, G, grid = S2_CFGS[k]
+    P = ou.random_params(seed=17, resblock_updown=False, **cfg)
+    m = UNetModel(image_size=2 * grid[0], in_channels=cfg["in_channels"], model_channels=cfg["model_channels"],
+                  out_channels=cfg["out_channels"], num_res_blocks=cfg["num_res_blocks"], attention_resolutions=(),
+                  channel_mult=cfg["channel_mult"], dims=3, resblock_updown=False, bottleneck_attention=False,
+                  resample_2d=False, num_groups=G, compute_dtype=dtype)
+    m.load_state_dict(P)
+    m.to(DEV)
+    g = torch.Generator().manual_seed(18)
+    x = torch.randn(1, 32, *grid, generator=g)
+    t = torch.tensor([321])
+    trace = []
+    ref = ou.unet_forward(P, x, t, num_groups=G, trace=trace, resblock_updown=False, **cfg)
+    with torch.no_grad():
+        out = m(x.to(DEV), t.to(DEV))
+    assert rel_err(out, ref) < tol
+    ws = m.plan.workspace(1, *grid, DEV)
+    got = m.plan.trace_tensors(ws, 1, *grid)
+    assert len(got) == len(trace)
+    for i, (gt, rf) in enumerate(zip(got, trace)):
+        if gt is not None:
+            assert rel_err(gt.float().permute(0, 4, 1, 2, 3), rf) < tol, i
