@@ -35,6 +35,7 @@ class SamplerArgs(ctypes.Structure):
         ("clip_denoised", ctypes.c_int),
         ("mean_type", ctypes.c_int),
         ("update", ctypes.c_int),
+        ("per_band", ctypes.c_int),
     ]
 
 
@@ -97,7 +98,8 @@ _PROTOS = {
                                         ctypes.c_int, ctypes.c_int, vp]),
     "cwdm_haar_idwt3d_planes": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(i64), i64, i64, i64,
                                                i64, i64, vp, vp]),
-    "cwdm_prepare_batch": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, vp, i64, vp, vp, vp]),
+    "cwdm_prepare_batch": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, ctypes.c_int, vp, i64, vp, vp,
+                                          vp]),
     "cwdm_sampler_step": (ctypes.c_int, [ctypes.POINTER(SamplerArgs), vp]),
     "cwdm_quantile_workspace_bytes": (i64, []),
     "cwdm_quantiles": (ctypes.c_int, [vp, ctypes.c_int, i64, ctypes.POINTER(i64), ctypes.c_int,

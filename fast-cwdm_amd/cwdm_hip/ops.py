@@ -85,9 +85,10 @@ def idwt3d_planes(bands, lll_mul3=False):
     return out
 
 
-def prepare_batch(target, c1, c2, c3, eps_img, coef, t, T):
+def prepare_batch(target, c1, c2, c3, eps_img, coef, t, T, per_band=False):
     """training_losses front end in one kernel (cwdm_prepare_batch): returns
-    (x_in (B, 32, d, h, w) = [q_sample | 3 condition DWTs], x0 (B, 8, d, h, w))."""
+    (x_in (B, 32, d, h, w) = [q_sample | 3 condition DWTs], x0 (B, 8, d, h, w)).
+    per_band: coef is [T][8][2] (FATS per-band schedules)."""
     vols = [v.contiguous().float() for v in (target, c1, c2, c3, eps_img)]
     _need_cuda(*vols, coef, t)
     for v in vols:
@@ -97,8 +98,8 @@ def prepare_batch(target, c1, c2, c3, eps_img, coef, t, T):
     x_in = torch.empty((B, 32, D // 2, H // 2, W // 2), device=vols[0].device, dtype=torch.float32)
     x0 = torch.empty((B, 8, D // 2, H // 2, W // 2), device=vols[0].device, dtype=torch.float32)
     t = t.to(dtype=torch.int64).contiguous()
-    check(lib().cwdm_prepare_batch(*[_p(v) for v in vols], B, D, H, W, _p(coef), _p(t), T, _p(x_in), _p(x0),
-                                   _stream()), "training_losses")
+    check(lib().cwdm_prepare_batch(*[_p(v) for v in vols], B, D, H, W, _p(coef), 1 if per_band else 0, _p(t), T,
+                                   _p(x_in), _p(x0), _stream()), "training_losses")
     return x_in, x0
 
 
@@ -123,7 +124,7 @@ def ndhwc_strides(B, C, V, c_total=None):
 
 def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t, T, B, d, h, w,
                  clip_denoised=True, pred_xstart=None, px_s=(0, 0, 0), mirror=None, mr_s=(0, 0, 0),
-                 mean_type=0, update=0):
+                 mean_type=0, update=0, per_band=False):
     """Fused process_xstart + posterior mean + noise (cwdm_sampler_step);
     update=1: the DDIM step instead of the posterior mean + noise."""
     _need_cuda(model_out, x_t, x_prev, noise, coef, t, pred_xstart, mirror)
@@ -143,6 +144,7 @@ def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t,
     a.clip_denoised = 1 if clip_denoised else 0
     a.mean_type = int(mean_type)
     a.update = int(update)
+    a.per_band = 1 if per_band else 0
     check(lib().cwdm_sampler_step(ctypes.byref(a), _stream()), "sampler_step")
 
 

@@ -47,7 +47,9 @@ class SpacedDiffusion(GaussianDiffusion):
         base = GaussianDiffusion(**kwargs)
         last_alpha_cumprod = 1.0
         new_betas = []
-        for i, alpha_cumprod in enumerate(base.alphas_cumprod):
+        # the base (shared) schedule; FATS per-band tables are rebuilt from it by
+        # GaussianDiffusion (each band's acp_k is a function of acp at the same step)
+        for i, alpha_cumprod in enumerate(base.base_alphas_cumprod):
             if i in self.use_timesteps:
                 new_betas.append(1 - alpha_cumprod / last_alpha_cumprod)
                 last_alpha_cumprod = alpha_cumprod

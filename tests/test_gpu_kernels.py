@@ -406,3 +406,53 @@ def test_gn_silu_pool(dtype_name):
     tol = 1e-5 if dtype_name == "fp32" else 1e-2
     assert rel_err(_nc(oh.float().cpu()), h) < tol
     assert rel_err(_nc(ox.float().cpu()), F.avg_pool3d(x, 2)) < tol
+
+
+FATS_SHIFT = [-1.2, 0.4, 0.5, 0.9, 0.3, 0.8, 1.0, 1.6]
+
+
+@pytest.mark.parametrize("update,eta", [(0, 0.0), (1, 0.0), (1, 0.4)], ids=["ddpm", "ddim", "ddim_eta"])
+def test_fats_per_band_sampler_step_vs_oracle(update, eta):
+    """FATS: the fused step reads one coefficient row per subband (per_band):
+    vs the oracle's p_sample / ddim_sample on per-band tables."""
+    from oracle import diffusion as od
+    from guided_diffusion import script_util
+    d = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
+                                              timestep_respacing="ddim10", band_log_snr_shift=FATS_SHIFT)
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"), use_timesteps=od.space_timesteps(1000, "ddim10"),
+                    band_shift=FATS_SHIFT)
+    g = torch.Generator().manual_seed(9)
+    B, n = 3, 6
+    mo = torch.randn(B, 8, n, n, n, generator=g) * 0.5 + 0.2
+    x = torch.randn(B, 8, n, n, n, generator=g)
+    noise = torch.randn(B, 8, n, n, n, generator=g)
+    cond = torch.zeros(B, 24, n, n, n)
+    t = torch.tensor([0, 4, 9])
+    sample, pred = d._epilogue(mo.to(DEV), x.to(DEV), t.to(DEV), True, None,
+                               None if update else noise.to(DEV), update=update, eta=eta)
+    if update:
+        ref = od.ddim_sample(tab, lambda xc, tt: mo, x, t, cond, clip_denoised=True, eta=eta)
+    else:
+        ref = od.p_sample(tab, lambda xc, tt: mo, x, t, cond, noise)
+    assert rel_err(pred, ref["pred_xstart"]) < 1e-6
+    assert rel_err(sample, ref["sample"]) < 1e-6
+
+
+def test_fats_per_band_prepare_batch_bitexact():
+    from cwdm_hip import ops
+    from oracle import diffusion as od
+    from guided_diffusion import script_util
+    d = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
+                                              band_log_snr_shift=FATS_SHIFT)
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"), band_shift=FATS_SHIFT)
+    g = torch.Generator().manual_seed(10)
+    shape = (2, 1, 8, 12, 10)
+    vols = [torch.rand(shape, generator=g) for _ in range(4)]
+    eps = torch.randn(shape, generator=g)
+    t = torch.tensor([3, 871])
+    x_in, x0 = ops.prepare_batch(*[v.to(DEV) for v in vols], eps.to(DEV), d.q_coef_table(DEV), t.to(DEV), 1000,
+                                 per_band=True)
+    rx0 = haar.dwt_cat(vols[0])
+    reps = torch.cat(list(haar.dwt3d(eps)), 1)
+    assert torch.equal(x0.cpu(), rx0)
+    assert torch.equal(x_in[:, :8].cpu(), od.q_sample(tab, rx0, t, reps))
