@@ -36,7 +36,11 @@ inline int64_t align_up(int64_t v) { return (v + kAlign - 1) / kAlign * kAlign; 
 
 struct Param { std::string name; std::vector<int64_t> shape; int64_t numel() const { int64_t n = 1; for (auto s : shape) n *= s; return n; } };
 
-struct Tensor { int level; int channels; };
+struct Tensor {
+  int level, channels;
+  int stats_kind = 0;  // producer of its (sum, sum^2) parts: 0 conv epilogue, 1 / 2 cwdm_haar_nd over its own /
+                       // the half grid (analysis / synthesis output), -1 none (never GroupNorm'd)
+};
 
 struct GnStep {
   int src0, src1;       // tensor ids (src1 = -1 if none)
@@ -76,14 +80,24 @@ struct PoolStep {  // down-ResBlock pre-pass (cwdm_gn_silu_pool)
   int src, ss_id, out_h, out_x, level_out, channels;
 };
 
-struct Step { int kind; int idx; };  // kind 0 = gn, 1 = conv, 2 = pool pre-pass, 3 = space-to-depth
+struct HaarStep {  // WavUNetModel resampling / input pyramid (cwdm_haar_nd, wavelet_nd.hip)
+  int src, high_in, out, high_out;  // tensor ids (-1 none)
+  int inverse, all8;
+  float lll_scale, high_scale;
+  int emb_row;                      // emb projection row offset added after the resampling, -1 none
+  bool stats;
+  int level;                        // the coarse grid's level
+};
+
+struct Step { int kind; int idx; };  // kind 0 = gn, 1 = conv, 2 = pool pre-pass, 3 = space-to-depth, 4 = haar
 
 // one ResBlock, for the backward (reverse order) and the gradient segments
 struct Block {
   int g1, pool, c1, g2, c2;   // step indices (pool = -1 unless down)
   int x0, x1;                 // input tensors (x1 = -1 unless decoder concat)
   int updown;                 // 0 none, 1 up, 2 down; layers without a ResBlock (resblock_updown=False):
-                              // 3 Downsample stride-2 conv (c1, pool = its S2dStep), 4 Upsample nearest + conv (c1)
+                              // 3 Downsample stride-2 conv (c1, pool = its S2dStep), 4 Upsample nearest + conv (c1);
+                              // WavUNetModel ResBlocks: 5 down (DWT), 6 up (IDWT)
   int p_begin, p_end;         // parameter index range
   int emb_k;                  // index into emb_rows_*
 };
@@ -99,12 +113,17 @@ struct cwdm_unet {
   std::vector<ConvStep> convs;
   std::vector<PoolStep> pools;
   std::vector<S2dStep> s2ds;
+  std::vector<HaarStep> haars;
   std::vector<Step> steps;
+  struct Alias { std::string name; int owner, before; };
+  std::vector<Alias> aliases;     // WavUNetModel: second state_dict name of a reused parameter; before = the
+                                  // parameter index it precedes in state_dict order
   std::vector<int> trace;         // tensor id per topology block (-1 = final output)
   std::vector<int> trace_level;
   int input_tensor = -1;          // pseudo tensor for x
   int R = 0;                      // emb projection rows
   std::vector<int> emb_rows_w, emb_rows_b, emb_rows_cb;  // per res block: emb weight/bias param, conv1 bias param
+                                                         // (-1: the conv bias is not folded, WavUNet up/down)
   std::vector<int> emb_rows_off, emb_rows_n;
   int te_w1, te_b1, te_w2, te_b2;
   std::vector<Block> blocks;
@@ -148,9 +167,23 @@ void build(cwdm_unet* u) {
   };
   u->input_tensor = new_tensor(0, c.in_channels);
 
+  // WavUNetModel's decoder registers one ResBlock under two prefixes
+  // (wunet.py:648-687): while alias_from is set, names under it resolve to the
+  // parameter of the same suffix under alias_to instead of a new parameter
+  std::string alias_from, alias_to;
+  auto addp = [&](const std::string& n, std::vector<int64_t> shape) {
+    if (alias_from.empty() || n.compare(0, alias_from.size(), alias_from) != 0) return u->add_param(n, std::move(shape));
+    const std::string owner = alias_to + n.substr(alias_from.size());
+    for (size_t i = 0; i < u->params.size(); ++i)
+      if (u->params[i].name == owner) {
+        u->aliases.push_back({n, (int)i, (int)u->params.size()});
+        return (int)i;
+      }
+    return -1;  // unreachable: the owner block was built first
+  };
   auto conv_params = [&](const std::string& p, int co, int ci, int k, int* wp, int* bp) {
-    *wp = u->add_param(p + ".weight", {co, ci, k, k, k});
-    *bp = u->add_param(p + ".bias", {co});
+    *wp = addp(p + ".weight", {co, ci, k, k, k});
+    *bp = addp(p + ".bias", {co});
   };
 
   // conv_in
@@ -175,8 +208,8 @@ void build(cwdm_unet* u) {
     GnStep g{};
     g.src0 = s0; g.src1 = s1;
     g.channels = u->tensors[s0].channels + (s1 >= 0 ? u->tensors[s1].channels : 0);
-    g.gamma_p = u->add_param(p + ".weight", {g.channels});
-    g.beta_p = u->add_param(p + ".bias", {g.channels});
+    g.gamma_p = addp(p + ".weight", {g.channels});
+    g.beta_p = addp(p + ".bias", {g.channels});
     g.level = lvl;
     g.ss_id = (int)u->gns.size();
     u->gns.push_back(g);
@@ -184,16 +217,83 @@ void build(cwdm_unet* u) {
     return g.ss_id;
   };
 
-  // ResBlock (unet.py:185-311): returns output tensor
-  auto resblock = [&](const std::string& p, int x0, int x1, int cout, int updown /*0 none 1 up 2 down*/) {
+  auto haar_step = [&](const HaarStep& hs) {
+    u->haars.push_back(hs);
+    u->steps.push_back({4, (int)u->haars.size() - 1});
+  };
+  auto add_emb_row = [&](Block& blk, int wp, int bp, int cbp, int n) {
+    u->emb_rows_w.push_back(wp); u->emb_rows_b.push_back(bp); u->emb_rows_cb.push_back(cbp);
+    blk.emb_k = (int)u->emb_rows_off.size();
+    u->emb_rows_off.push_back(u->R); u->emb_rows_n.push_back(n);
+    const int row = u->R;
+    u->R += n;
+    return row;
+  };
+
+  // ResBlock (unet.py:185-311): returns output tensor.  updown 5 / 6: the
+  // WavUNetModel ResBlock (wunet.py:210-269) that down/upsamples by DWT / IDWT
+  // AFTER its first conv; skip_bands = the 7 high bands an up block inverts
+  // with, *skip_out = the 7 high bands a down block returns.
+  auto resblock = [&](const std::string& p, int x0, int x1, int cout, int updown, int skip_bands = -1,
+                      int* skip_out = nullptr) {
     Block blk{};
     blk.p_begin = (int)u->params.size();
     blk.x0 = x0; blk.x1 = x1; blk.updown = updown; blk.pool = -1;
     const int lin = u->tensors[x0].level;
     const int cin = u->tensors[x0].channels + (x1 >= 0 ? u->tensors[x1].channels : 0);
-    const int lout = updown == 2 ? lin + 1 : (updown == 1 ? lin - 1 : lin);
+    const int lout = (updown == 2 || updown == 5) ? lin + 1 : ((updown == 1 || updown == 6) ? lin - 1 : lin);
     int g1 = gn_step(p + ".in_layers.0", x0, x1, lin);
     blk.g1 = g1;
+    if (updown >= 5) {
+      const bool down = updown == 5;
+      ConvStep c1{};
+      conv_params(p + ".in_layers.2", cout, cin, 3, &c1.w_p, &c1.b_p);
+      c1.emb_w_p = addp(p + ".emb_layers.1.weight", {cout, E});
+      c1.emb_b_p = addp(p + ".emb_layers.1.bias", {cout});
+      c1.a0 = x0; c1.a1 = -1; c1.amode = 0; c1.gn = g1; c1.cin_a = cin;
+      c1.sb0 = c1.sb1 = -1; c1.ws_p = c1.wsb_p = -1; c1.cin_b = 0;
+      c1.bias_kind = 0; c1.res = -1; c1.rmode = -1; c1.cout = cout; c1.level = lin; c1.stats = false;
+      const int h1 = c1.out = new_tensor(lin, cout);
+      u->tensors[h1].stats_kind = -1;
+      u->convs.push_back(c1);
+      blk.c1 = (int)u->convs.size() - 1;
+      u->steps.push_back({1, blk.c1});
+      const int row = add_emb_row(blk, c1.emb_w_p, c1.emb_b_p, -1, cout);
+      // h: DWT -> LLL / 3 (+ the 7 high bands as the skip) or IDWT(3 h, skip); then + emb
+      HaarStep hh{};
+      hh.src = h1; hh.high_in = down ? -1 : skip_bands; hh.inverse = down ? 0 : 1; hh.all8 = 0;
+      hh.lll_scale = down ? 1.f / 3.f : 3.f; hh.high_scale = 1.f;
+      hh.out = new_tensor(lout, cout);
+      u->tensors[hh.out].stats_kind = down ? 1 : 2;
+      hh.high_out = -1;
+      if (down) {
+        hh.high_out = new_tensor(lout, 7 * cout);
+        u->tensors[hh.high_out].stats_kind = -1;
+      }
+      hh.emb_row = row; hh.stats = true; hh.level = down ? lout : lin;
+      haar_step(hh);
+      if (skip_out) *skip_out = hh.high_out;
+      // x: the same resampling, LLL only / with the same skip bands (x_upd)
+      HaarStep hx = hh;
+      hx.src = x0; hx.out = new_tensor(lout, cin); hx.high_out = -1; hx.emb_row = -1; hx.stats = false;
+      u->tensors[hx.out].stats_kind = -1;
+      haar_step(hx);
+      const int g2 = gn_step(p + ".out_layers.0", hh.out, -1, lout);
+      blk.g2 = g2;
+      ConvStep c2{};
+      conv_params(p + ".out_layers.3", cout, cout, 3, &c2.w_p, &c2.b_p);
+      c2.a0 = hh.out; c2.a1 = -1; c2.amode = 0; c2.gn = g2; c2.cin_a = cout;
+      c2.sb0 = c2.sb1 = -1; c2.ws_p = c2.wsb_p = -1; c2.cin_b = 0;
+      c2.res = hx.out; c2.rmode = 0;  // up/down blocks keep the channel count (checked at create)
+      c2.bias_kind = 0; c2.cout = cout; c2.level = lout; c2.stats = true;
+      const int o = c2.out = new_tensor(lout, cout);
+      u->convs.push_back(c2);
+      blk.c2 = (int)u->convs.size() - 1;
+      u->steps.push_back({1, blk.c2});
+      blk.p_end = (int)u->params.size();
+      u->blocks.push_back(blk);
+      return o;
+    }
     int xres = x0, xrmode = updown == 2 ? 2 : (updown == 1 ? 1 : 0);
     int a_src = x0, a_mode = updown, a_gn = g1;
     if (updown == 2) {
@@ -210,15 +310,11 @@ void build(cwdm_unet* u) {
     }
     ConvStep c1{};
     conv_params(p + ".in_layers.2", cout, cin, 3, &c1.w_p, &c1.b_p);
-    c1.emb_w_p = u->add_param(p + ".emb_layers.1.weight", {cout, E});
-    c1.emb_b_p = u->add_param(p + ".emb_layers.1.bias", {cout});
+    c1.emb_w_p = addp(p + ".emb_layers.1.weight", {cout, E});
+    c1.emb_b_p = addp(p + ".emb_layers.1.bias", {cout});
     c1.a0 = a_src; c1.a1 = x1; c1.amode = a_mode; c1.gn = a_gn; c1.cin_a = cin;
     c1.sb0 = c1.sb1 = -1; c1.ws_p = c1.wsb_p = -1; c1.cin_b = 0;
-    c1.bias_kind = 1; c1.bias_off = u->R;
-    u->emb_rows_w.push_back(c1.emb_w_p); u->emb_rows_b.push_back(c1.emb_b_p); u->emb_rows_cb.push_back(c1.b_p);
-    blk.emb_k = (int)u->emb_rows_off.size();
-    u->emb_rows_off.push_back(u->R); u->emb_rows_n.push_back(cout);
-    u->R += cout;
+    c1.bias_kind = 1; c1.bias_off = add_emb_row(blk, c1.emb_w_p, c1.emb_b_p, c1.b_p, cout);
     c1.res = -1; c1.rmode = -1; c1.cout = cout; c1.level = lout; c1.stats = true;
     int h1 = c1.out = new_tensor(lout, cout);
     u->convs.push_back(c1);
@@ -283,7 +379,79 @@ void build(cwdm_unet* u) {
 
   int ch = mc, idx = 1;
   const int nl = c.num_levels;
-  for (int l = 0; l < nl; ++l) {
+  if (c.use_freq) {
+    // WavUNetModel (wunet.py:470-700, forward :754-795): every level ends in a
+    // DWT ResBlock and a WaveletDownsample of the input pyramid; the decoder
+    // has no concatenation, only the high-band skips into its IDWT ResBlocks
+    std::vector<int> skips;
+    int pyr = u->input_tensor;
+    for (int l = 0; l < nl; ++l) {
+      const int mult = c.channel_mult[l];
+      for (int r = 0; r < c.num_res_blocks; ++r) {
+        h = resblock("input_blocks." + std::to_string(idx) + ".0", h, -1, mult * mc, 0);
+        ch = mult * mc;
+        u->trace.push_back(h); u->trace_level.push_back(level);
+        ++idx;
+      }
+      int sk = -1;
+      h = resblock("input_blocks." + std::to_string(idx) + ".0", h, -1, ch, 5, -1, &sk);
+      skips.push_back(sk);
+      ++level;
+      u->trace.push_back(h); u->trace_level.push_back(level);
+      // WaveletDownsample (:131-145): conv(cat(8 bands) / 3) + h
+      const int cp = u->tensors[pyr].channels;
+      HaarStep hp{};
+      hp.src = pyr; hp.high_in = -1; hp.high_out = -1; hp.inverse = 0; hp.all8 = 1;
+      hp.lll_scale = hp.high_scale = 1.f / 3.f; hp.emb_row = -1; hp.stats = false; hp.level = level;
+      hp.out = new_tensor(level, 8 * cp);
+      u->tensors[hp.out].stats_kind = -1;
+      haar_step(hp);
+      ConvStep cs{};
+      conv_params("input_blocks." + std::to_string(idx + 1) + ".0.conv", ch, 8 * cp, 3, &cs.w_p, &cs.b_p);
+      cs.a0 = hp.out; cs.a1 = -1; cs.amode = 0; cs.gn = -1; cs.cin_a = 8 * cp;
+      cs.sb0 = cs.sb1 = -1; cs.ws_p = cs.wsb_p = -1; cs.cin_b = 0;
+      cs.bias_kind = 0; cs.res = h; cs.rmode = 0; cs.cout = ch; cs.level = level; cs.stats = true;
+      h = pyr = cs.out = new_tensor(level, ch);
+      u->convs.push_back(cs);
+      u->steps.push_back({1, (int)u->convs.size() - 1});
+      u->trace.push_back(h); u->trace_level.push_back(level);
+      idx += 2;
+    }
+    h = resblock("middle_block.0", h, -1, ch, 0);
+    u->trace.push_back(h); u->trace_level.push_back(level);
+    h = resblock("middle_block.1", h, -1, ch, 0);
+    u->trace.push_back(h); u->trace_level.push_back(level);
+    idx = 0;
+    for (int l = nl - 1; l >= 0; --l) {
+      const int mult = c.channel_mult[l];
+      const int sk = skips.back();  // popped by the level's first output block (hs.pop() skips the Nones)
+      skips.pop_back();
+      std::string owner;
+      for (int i = 0; i <= c.num_res_blocks; ++i) {
+        const std::string p = "output_blocks." + std::to_string(idx);
+        if (i != c.num_res_blocks) {
+          h = resblock(p + ".0", h, -1, mc * mult, 0);
+          ch = mc * mult;
+          owner = p + ".0";
+        } else {
+          // Sequential(<the level's last ResBlock again>, IDWT ResBlock)
+          alias_from = p + ".0.";
+          alias_to = owner + ".";
+          h = resblock(p + ".0", h, -1, ch, 0);
+          alias_from.clear();
+          h = resblock(p + ".1", h, -1, ch, 6, sk);
+          --level;
+        }
+        u->trace.push_back(h); u->trace_level.push_back(level);
+        ++idx;
+      }
+    }
+    for (int i = 0; i < c.num_res_blocks; ++i) {
+      h = resblock("out_res." + std::to_string(i) + ".0", h, -1, ch, 0);
+      u->trace.push_back(h); u->trace_level.push_back(level);
+    }
+  }
+  for (int l = 0; l < nl && !c.use_freq; ++l) {
     const int mult = c.channel_mult[l];
     for (int r = 0; r < c.num_res_blocks; ++r) {
       h = resblock("input_blocks." + std::to_string(idx) + ".0", h, -1, mult * mc, 0);
@@ -301,12 +469,14 @@ void build(cwdm_unet* u) {
       ++idx;
     }
   }
-  h = resblock("middle_block.0", h, -1, ch, 0);
-  u->trace.push_back(h); u->trace_level.push_back(level);
-  h = resblock("middle_block.1", h, -1, ch, 0);
-  u->trace.push_back(h); u->trace_level.push_back(level);
-  idx = 0;
-  for (int l = nl - 1; l >= 0; --l) {
+  if (!c.use_freq) {
+    h = resblock("middle_block.0", h, -1, ch, 0);
+    u->trace.push_back(h); u->trace_level.push_back(level);
+    h = resblock("middle_block.1", h, -1, ch, 0);
+    u->trace.push_back(h); u->trace_level.push_back(level);
+    idx = 0;
+  }
+  for (int l = nl - 1; l >= 0 && !c.use_freq; --l) {
     const int mult = c.channel_mult[l];
     for (int i = 0; i <= c.num_res_blocks; ++i) {
       int skip = stack.back();
@@ -433,7 +603,10 @@ Layout layout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
       continue;
     }
     L.t_off.push_back(take(B * d * h * w * t.channels * es));
-    const int64_t parts = cwdm_conv3d_parts(u->cfg.dtype, d, h, w, t.channels);
+    const int64_t parts = t.stats_kind < 0    ? 0
+                          : t.stats_kind == 1 ? cwdm_haar_nd_parts(d, h, w)
+                          : t.stats_kind == 2 ? cwdm_haar_nd_parts(d / 2, h / 2, w / 2)
+                                              : cwdm_conv3d_parts(u->cfg.dtype, d, h, w, t.channels);
     L.s_parts.push_back(parts);
     L.s_off.push_back(take(B * parts * t.channels * 2 * 4));
   }
@@ -502,6 +675,23 @@ extern "C" int cwdm_unet_create(const cwdm_unet_config* cfg, cwdm_unet** plan) {
                  "cwdm_unet_create: level channels must be multiples of 32 (and of the chunk)");
     CWDM_REQUIRE(ch % cfg->num_groups == 0, CWDM_E_INVALID, "cwdm_unet_create: channels not divisible by groups");
   }
+  if (cfg->use_freq) {
+    // WavUNetModel as script_util.create_model builds it (:268-292)
+    CWDM_REQUIRE(cfg->resblock_updown, CWDM_E_UNSUPPORTED,
+                 "cwdm_unet_create: use_freq needs resblock_updown=1 (wunet.Downsample with use_freq ignores its conv)");
+    CWDM_REQUIRE(cfg->channel_mult[0] == 1, CWDM_E_UNSUPPORTED,
+                 "cwdm_unet_create: use_freq: the output head takes model_channels (wunet.py:713), channel_mult[0] = 1");
+    CWDM_REQUIRE(cfg->in_channels % 8 == 0 && cfg->in_channels <= 2048, CWDM_E_UNSUPPORTED,
+                 "cwdm_unet_create: use_freq: the wavelet pyramid needs in_channels a multiple of 8");
+    // the decoder re-runs each level's last ResBlock on its own output (wunet.py:648-687): that block must keep
+    // its channel count, i.e. num_res_blocks >= 2 or no channel change into the level
+    for (int l = 0; l < cfg->num_levels && cfg->num_res_blocks == 1; ++l) {
+      const int prev = l == cfg->num_levels - 1 ? cfg->channel_mult[l] : cfg->channel_mult[l + 1];
+      CWDM_REQUIRE(prev == cfg->channel_mult[l], CWDM_E_UNSUPPORTED,
+                   "cwdm_unet_create: use_freq with num_res_blocks=1 needs equal channel_mult across levels "
+                   "(the reused decoder ResBlock would see the wrong channel count, as in the reference)");
+    }
+  }
   auto* u = new cwdm_unet();
   u->cfg = *cfg;
   build(u);
@@ -530,6 +720,19 @@ extern "C" int cwdm_unet_param_info(const cwdm_unet* u, int i, char* name, int c
   return CWDM_OK;
 }
 
+extern "C" int cwdm_unet_num_aliases(const cwdm_unet* u) { return u ? (int)u->aliases.size() : -1; }
+
+extern "C" int cwdm_unet_alias_info(const cwdm_unet* u, int i, char* name, int cap, int* owner, int* before) {
+  CWDM_REQUIRE(u && i >= 0 && i < (int)u->aliases.size(), CWDM_E_INVALID, "cwdm_unet_alias_info: bad index");
+  if (name && cap > 0) {
+    std::strncpy(name, u->aliases[i].name.c_str(), cap - 1);
+    name[cap - 1] = 0;
+  }
+  if (owner) *owner = u->aliases[i].owner;
+  if (before) *before = u->aliases[i].before;
+  return CWDM_OK;
+}
+
 extern "C" int64_t cwdm_unet_packed_bytes(const cwdm_unet* u) { return u ? u->packed_bytes : -1; }
 
 extern "C" int cwdm_unet_pack(const cwdm_unet* u, const float* const* P, void* packed, cwdm_stream_t stream) {
@@ -549,7 +752,11 @@ extern "C" int cwdm_unet_pack(const cwdm_unet* u, const float* const* P, void* p
   for (size_t k = 0; k < u->emb_rows_w.size(); ++k) {
     const int64_t o = u->emb_rows_off[k], n = u->emb_rows_n[k];
     CWDM_HIP(hipMemcpyAsync(ew + o * u->E, P[u->emb_rows_w[k]], n * u->E * 4, hipMemcpyDeviceToDevice, s));
-    if ((rc = launch_vec_add(P[u->emb_rows_b[k]], P[u->emb_rows_cb[k]], eb + o, n, s))) return rc;
+    if (u->emb_rows_cb[k] < 0) {
+      CWDM_HIP(hipMemcpyAsync(eb + o, P[u->emb_rows_b[k]], n * 4, hipMemcpyDeviceToDevice, s));
+    } else if ((rc = launch_vec_add(P[u->emb_rows_b[k]], P[u->emb_rows_cb[k]], eb + o, n, s))) {
+      return rc;
+    }
   }
   for (const auto& cs : u->convs) {
     if (cs.s2) {
@@ -596,7 +803,7 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
                                  cwdm_stream_t stream) {
   CWDM_REQUIRE(u && packed && x && t && out && ws, CWDM_E_INVALID, "cwdm_unet_forward: null pointer");
   CWDM_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0, CWDM_E_SHAPE, "cwdm_unet_forward: empty grid");
-  const int64_t div = int64_t(1) << (u->cfg.num_levels - 1);
+  const int64_t div = int64_t(1) << (u->cfg.num_levels - (u->cfg.use_freq ? 0 : 1));
   CWDM_REQUIRE(D % div == 0 && H % div == 0 && W % div == 0, CWDM_E_SHAPE,
                "cwdm_unet_forward: every subband edge must be divisible by " + std::to_string(div));
   Layout L = layout(u, B, D, H, W);
@@ -655,6 +862,24 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
       if ((rc = cwdm_space_to_depth(tptr(sd.src), sd.channels, B, D >> lv, H >> lv, W >> lv, u->cfg.dtype,
                                     wb + L.t_off[sd.out], 1, 0, stream)))
         return rc;
+      continue;
+    }
+    if (st.kind == 4) {
+      const auto& hs = u->haars[st.idx];
+      const int lv = hs.level;
+      cwdm_haar_nd_desc a{};
+      a.dtype = u->cfg.dtype;
+      a.B = B; a.d = D >> lv; a.h = H >> lv; a.w = W >> lv;
+      a.C = u->tensors[hs.src].channels;
+      a.inverse = hs.inverse; a.all8 = hs.all8;
+      a.src = tptr(hs.src); a.high_in = tptr(hs.high_in);
+      a.lll_scale = hs.lll_scale; a.high_scale = hs.high_scale;
+      a.out = wb + L.t_off[hs.out];
+      a.high_out = hs.high_out >= 0 ? wb + L.t_off[hs.high_out] : nullptr;
+      a.bias = hs.emb_row >= 0 ? ebias + hs.emb_row : nullptr;
+      a.bias_bstride = u->R;
+      a.stats = hs.stats ? reinterpret_cast<float*>(wb + L.s_off[hs.out]) : nullptr;
+      if ((rc = cwdm_haar_nd(&a, stream))) return rc;
       continue;
     }
     if (st.kind == 0) {
@@ -845,6 +1070,7 @@ extern "C" int64_t cwdm_unet_packed_bwd_bytes(const cwdm_unet* u) { return u ? u
 
 extern "C" int cwdm_unet_pack_bwd(const cwdm_unet* u, const float* const* P, void* packed_bwd, cwdm_stream_t stream) {
   CWDM_REQUIRE(u && P && packed_bwd, CWDM_E_INVALID, "cwdm_unet_pack_bwd: null pointer");
+  CWDM_REQUIRE(!u->cfg.use_freq, CWDM_E_UNSUPPORTED, "cwdm_unet_pack_bwd: the WavUNetModel plan is forward-only");
   auto* base = reinterpret_cast<unsigned char*>(packed_bwd);
   int rc;
   for (size_t i = 0; i < u->convs.size(); ++i) {
@@ -863,7 +1089,7 @@ extern "C" int cwdm_unet_pack_bwd(const cwdm_unet* u, const float* const* P, voi
 }
 
 extern "C" int64_t cwdm_unet_grad_workspace_bytes(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
-  if (!u || B <= 0 || D <= 0 || H <= 0 || W <= 0) return -1;
+  if (!u || u->cfg.use_freq || B <= 0 || D <= 0 || H <= 0 || W <= 0) return -1;
   return glayout(u, B, D, H, W).total;
 }
 
@@ -901,6 +1127,8 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
                                   int seg_begin, int seg_end, cwdm_stream_t stream) {
   CWDM_REQUIRE(u && packed && packed_bwd && x && t && dout && grads && ws && gws, CWDM_E_INVALID,
                "cwdm_unet_backward: null pointer");
+  CWDM_REQUIRE(!u->cfg.use_freq, CWDM_E_UNSUPPORTED,
+               "cwdm_unet_backward: the WavUNetModel plan is forward-only (sampling); train with UNetModel");
   const int nseg = (int)u->blocks.size() + 2;
   CWDM_REQUIRE(0 <= seg_begin && seg_begin <= seg_end && seg_end <= nseg, CWDM_E_INVALID,
                "cwdm_unet_backward: bad segment range");

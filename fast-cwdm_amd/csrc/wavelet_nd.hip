@@ -1,0 +1,177 @@
+// Channels-last, multi-channel Haar analysis / synthesis for the frequency-aware
+// U-Net (WavUNetModel, guided_diffusion/wunet.py): Downsample(use_freq) =
+// DWT of a feature map, LLL / 3 kept, 7 high bands returned as the skip
+// (:120-128); Upsample(use_freq) = IDWT(3 LLL, skip bands) (:62-80);
+// WaveletDownsample = cat(8 bands) / 3 as a conv input (:131-145).  Each
+// output may get a per-(b, c) bias (the ResBlock's emb projection, added right
+// after the resampling, :252) and per-part (sum, sum^2) statistics for the
+// GroupNorm that consumes it (same [B][parts][C][2] contract as the conv
+// epilogue).  One thread = one coarse voxel x 8 channels; a workgroup covers
+// 64 coarse voxels of one batch index (one statistics part).
+#include "common.hpp"
+#include "haar8.hpp"
+
+namespace cwdm {
+namespace {
+
+constexpr int kVox = 64;  // coarse voxels per workgroup (= per statistics part)
+
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float* f) {
+  if constexpr (sizeof(T) == 2) {
+    const uint4 q = *reinterpret_cast<const uint4*>(p);
+    const unsigned u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(u[i] << 16);
+      f[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store8(T* p, const float* f) {
+  if constexpr (sizeof(T) == 2) {
+    uint4 q;
+    q.x = (unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16);
+    q.y = (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16);
+    q.z = (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16);
+    q.w = (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = q;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+  }
+}
+
+template <typename T, bool INV>
+__global__ void __launch_bounds__(256) haar_nd_kernel(cwdm_haar_nd_desc a, int parts) {
+  __shared__ float red[256 * 16];
+  const int C = a.C, G = C / 8;
+  const int tid = threadIdx.x, g = tid % G, vl = tid / G, VB = 256 / G;
+  const int64_t b = blockIdx.x / parts, part = blockIdx.x % parts;
+  const int64_t nv = a.d * a.h * a.w;
+  const int64_t W2 = 2 * a.w, H2 = 2 * a.h;
+  float bias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bias[e] = a.bias ? a.bias[b * a.bias_bstride + g * 8 + e] : 0.f;
+  float ssum[8], ssq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { ssum[e] = 0.f; ssq[e] = 0.f; }
+  const T* src = reinterpret_cast<const T*>(a.src);
+  T* out = reinterpret_cast<T*>(a.out);
+  for (int vv = vl; vl < VB && vv < kVox; vv += VB) {  // threads past G x VB idle (C / 8 not a power of two)
+    const int64_t v = part * kVox + vv;
+    if (v >= nv) break;
+    const int64_t x = v % a.w, y = (v / a.w) % a.h, z = v / (a.w * a.h);
+    // fine voxel (a, bb, c) of this coarse voxel, channel group g
+    auto fine = [&](int i) {
+      const int pa = i >> 2, pb = (i >> 1) & 1, pc = i & 1;
+      return (((b * 2 * a.d + 2 * z + pa) * H2 + 2 * y + pb) * W2 + 2 * x + pc) * C + g * 8;
+    };
+    if constexpr (!INV) {
+      float blk[8][8];  // [fine voxel][channel]
+#pragma unroll
+      for (int i = 0; i < 8; ++i) load8(src + fine(i), blk[i]);
+      float band[8][8];  // [band][channel]
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float vin[8], o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vin[i] = blk[i][e];
+        haar_fwd8(vin, o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) band[k][e] = k == 0 ? __fmul_rn(o[0], a.lll_scale) : __fmul_rn(o[k], a.high_scale);
+      }
+      const int64_t cv = b * nv + v;
+      if (a.all8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) store8(out + (cv * 8 + k) * C + g * 8, band[k]);
+      } else {
+        float l[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          l[e] = band[0][e] + bias[e];
+          ssum[e] += l[e];
+          ssq[e] += l[e] * l[e];
+        }
+        store8(out + cv * C + g * 8, l);
+      }
+      if (a.high_out) {
+        T* ho = reinterpret_cast<T*>(a.high_out);
+#pragma unroll
+        for (int k = 1; k < 8; ++k) store8(ho + (cv * 7 + (k - 1)) * C + g * 8, band[k]);
+      }
+    } else {
+      const int64_t cv = b * nv + v;
+      float band[8][8];
+      load8(src + cv * C + g * 8, band[0]);
+      const T* hi = reinterpret_cast<const T*>(a.high_in);
+#pragma unroll
+      for (int k = 1; k < 8; ++k) load8(hi + (cv * 7 + (k - 1)) * C + g * 8, band[k]);
+      float blk[8][8];  // [fine voxel][channel]
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float o[8], r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = band[k][e];
+        o[0] = __fmul_rn(o[0], a.lll_scale);
+        haar_inv8(o, r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float val = r[i] + bias[e];
+          blk[i][e] = val;
+          ssum[e] += val;
+          ssq[e] += val * val;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) store8(out + fine(i), blk[i]);
+    }
+  }
+  if (!a.stats) return;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = ssum[e]; red[tid * 16 + 8 + e] = ssq[e]; }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    const int gg = c / 8, e = c % 8;
+    float sm = 0.f, sq = 0.f;
+    for (int k = 0; k < VB; ++k) { sm += red[(k * G + gg) * 16 + e]; sq += red[(k * G + gg) * 16 + 8 + e]; }
+    const int64_t pidx = (b * parts + part) * C + c;
+    a.stats[pidx * 2 + 0] = sm;
+    a.stats[pidx * 2 + 1] = sq;
+  }
+}
+
+}  // namespace
+}  // namespace cwdm
+
+using namespace cwdm;
+
+extern "C" int64_t cwdm_haar_nd_parts(int64_t d, int64_t h, int64_t w) { return ceil_div(d * h * w, kVox); }
+
+extern "C" int cwdm_haar_nd(const cwdm_haar_nd_desc* a, cwdm_stream_t stream) {
+  CWDM_REQUIRE(a && a->src && a->out, CWDM_E_INVALID, "cwdm_haar_nd: null pointer");
+  CWDM_REQUIRE(a->dtype == CWDM_F32 || a->dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_haar_nd: bad dtype");
+  CWDM_REQUIRE(a->B > 0 && a->d > 0 && a->h > 0 && a->w > 0, CWDM_E_SHAPE, "cwdm_haar_nd: empty grid");
+  CWDM_REQUIRE(a->C > 0 && a->C % 8 == 0 && a->C <= 2048, CWDM_E_UNSUPPORTED,
+               "cwdm_haar_nd: channels must be a multiple of 8, at most 2048");
+  CWDM_REQUIRE(!a->inverse || a->high_in, CWDM_E_INVALID, "cwdm_haar_nd: synthesis needs the 7 high bands");
+  CWDM_REQUIRE(!(a->all8 && (a->stats || a->bias)), CWDM_E_UNSUPPORTED,
+               "cwdm_haar_nd: all-band output takes no bias / statistics");
+  const int parts = (int)cwdm_haar_nd_parts(a->d, a->h, a->w);
+  const dim3 grid((unsigned)(a->B * parts));
+  hipStream_t s = (hipStream_t)stream;
+  if (a->dtype == CWDM_BF16) {
+    if (a->inverse) hipLaunchKernelGGL((haar_nd_kernel<bf16_t, true>), grid, dim3(256), 0, s, *a, parts);
+    else hipLaunchKernelGGL((haar_nd_kernel<bf16_t, false>), grid, dim3(256), 0, s, *a, parts);
+  } else {
+    if (a->inverse) hipLaunchKernelGGL((haar_nd_kernel<float, true>), grid, dim3(256), 0, s, *a, parts);
+    else hipLaunchKernelGGL((haar_nd_kernel<float, false>), grid, dim3(256), 0, s, *a, parts);
+  }
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}

@@ -83,7 +83,21 @@ class UNetConfig(ctypes.Structure):
         ("out_channels", ctypes.c_int), ("num_res_blocks", ctypes.c_int),
         ("num_levels", ctypes.c_int), ("channel_mult", ctypes.c_int * 8),
         ("num_groups", ctypes.c_int), ("dtype", ctypes.c_int),
-        ("resblock_updown", ctypes.c_int),
+        ("resblock_updown", ctypes.c_int), ("use_freq", ctypes.c_int),
+    ]
+
+
+class HaarNdDesc(ctypes.Structure):
+    _fields_ = [
+        ("dtype", ctypes.c_int),
+        ("B", i64), ("d", i64), ("h", i64), ("w", i64),
+        ("C", ctypes.c_int),
+        ("inverse", ctypes.c_int),
+        ("src", vp), ("high_in", vp),
+        ("lll_scale", ctypes.c_float), ("high_scale", ctypes.c_float),
+        ("out", vp), ("all8", ctypes.c_int), ("high_out", vp),
+        ("bias", vp), ("bias_bstride", i64),
+        ("stats", vp),
     ]
 
 
@@ -139,6 +153,11 @@ _PROTOS = {
     "cwdm_unet_create": (ctypes.c_int, [ctypes.POINTER(UNetConfig), ctypes.POINTER(vp)]),
     "cwdm_unet_destroy": (None, [vp]),
     "cwdm_unet_num_params": (ctypes.c_int, [vp]),
+    "cwdm_unet_num_aliases": (ctypes.c_int, [vp]),
+    "cwdm_unet_alias_info": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "cwdm_haar_nd_parts": (i64, [i64, i64, i64]),
+    "cwdm_haar_nd": (ctypes.c_int, [ctypes.POINTER(HaarNdDesc), vp]),
     "cwdm_unet_param_info": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(i64),
                                             ctypes.POINTER(ctypes.c_int)]),
     "cwdm_unet_packed_bytes": (i64, [vp]),

@@ -26,7 +26,7 @@ def parse_dtype(d):
 
 class UNetPlan:
     def __init__(self, in_channels, model_channels, out_channels, num_res_blocks, channel_mult, num_groups,
-                 dtype="fp32", resblock_updown=True):
+                 dtype="fp32", resblock_updown=True, use_freq=False):
         cfg = _lib.UNetConfig()
         cfg.in_channels, cfg.model_channels, cfg.out_channels = in_channels, model_channels, out_channels
         cfg.num_res_blocks, cfg.num_levels = num_res_blocks, len(channel_mult)
@@ -37,6 +37,8 @@ class UNetPlan:
         cfg.num_groups = num_groups
         cfg.dtype = parse_dtype(dtype)
         cfg.resblock_updown = 1 if resblock_updown else 0
+        cfg.use_freq = 1 if use_freq else 0
+        self.use_freq = bool(use_freq)
         self.dtype = cfg.dtype
         self.torch_dtype = TORCH_DT[cfg.dtype]
         self.num_levels = len(channel_mult)
@@ -52,6 +54,12 @@ class UNetPlan:
         for i in range(lib().cwdm_unet_num_params(h)):
             check(lib().cwdm_unet_param_info(h, i, name, 256, shape, ctypes.byref(nd)))
             self.param_specs.append((name.value.decode(), tuple(shape[k] for k in range(nd.value))))
+        # (alias name, owner index, index of the parameter it precedes in state_dict order)
+        self.aliases = []
+        owner, before = ctypes.c_int(), ctypes.c_int()
+        for i in range(lib().cwdm_unet_num_aliases(h)):
+            check(lib().cwdm_unet_alias_info(h, i, name, 256, ctypes.byref(owner), ctypes.byref(before)))
+            self.aliases.append((name.value.decode(), owner.value, before.value))
         self._ws = None
         self._ws_key = None
 
@@ -92,7 +100,7 @@ class UNetPlan:
         return self._ws
 
     def check_grid(self, D, H, W):
-        div = 2 ** (self.num_levels - 1)
+        div = 2 ** (self.num_levels - (0 if self.use_freq else 1))
         if D % div or H % div or W % div:
             raise AssertionError(f"every subband edge must be divisible by {div} (got {D}x{H}x{W})")
 

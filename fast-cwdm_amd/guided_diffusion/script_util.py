@@ -2,8 +2,9 @@
 
 Same defaults dicts, kwarg names and argparse helpers, so the reference's
 scripts and run.sh flag bundles work unchanged.  ``create_model`` builds the
-native ``UNetModel``; ``use_freq=True`` (WavUNetModel) and the classifier /
-super-resolution factories are outside the hot path and raise.
+native ``UNetModel``, or with ``use_freq=True`` the native (forward-only)
+``WavUNetModel``; the classifier / super-resolution factories are outside the
+hot path and raise.
 """
 import argparse
 
@@ -137,8 +138,17 @@ def create_model(image_size, num_channels, num_res_blocks, channel_mult="", lear
     if out_channels == 0:
         out_channels = 2 * in_channels if learn_sigma else in_channels
     if use_freq:
-        raise NotImplementedError("WavUNetModel (use_freq=True) is outside the fast-cwdm hot path (run.sh uses "
-                                  "use_freq=False); see DESIGN.md 'next'")
+        from .wunet import WavUNetModel
+        return WavUNetModel(
+            image_size=image_size, in_channels=in_channels, model_channels=num_channels,
+            out_channels=out_channels * (1 if not learn_sigma else 2), num_res_blocks=num_res_blocks,
+            attention_resolutions=tuple(attention_ds), dropout=dropout, channel_mult=channel_mult,
+            num_classes=(NUM_CLASSES if class_cond else None), use_checkpoint=use_checkpoint, use_fp16=use_fp16,
+            num_heads=num_heads, num_head_channels=num_head_channels, num_heads_upsample=num_heads_upsample,
+            use_scale_shift_norm=use_scale_shift_norm, resblock_updown=resblock_updown,
+            use_new_attention_order=use_new_attention_order, dims=dims, num_groups=num_groups,
+            bottleneck_attention=bottleneck_attention, additive_skips=additive_skips, use_freq=use_freq,
+            compute_dtype=compute_dtype)
     return UNetModel(
         image_size=image_size, in_channels=in_channels, model_channels=num_channels,
         out_channels=out_channels * (1 if not learn_sigma else 2), num_res_blocks=num_res_blocks,

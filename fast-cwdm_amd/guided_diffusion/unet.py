@@ -87,6 +87,17 @@ class UNetModel(nn.Module):
         if unsupported:
             raise NotImplementedError("fast-cwdm_amd UNetModel covers the run.sh configuration only; unsupported: "
                                       + ", ".join(unsupported))
+        self._setup_native(image_size, in_channels, model_channels, out_channels, num_res_blocks,
+                           attention_resolutions, dropout, channel_mult, conv_resample, num_classes, use_checkpoint,
+                           num_heads, num_groups, resblock_updown, bottleneck_attention, additive_skips,
+                           decoder_device_thresh, compute_dtype)
+
+    use_freq = False
+
+    def _setup_native(self, image_size, in_channels, model_channels, out_channels, num_res_blocks,
+                      attention_resolutions, dropout, channel_mult, conv_resample, num_classes, use_checkpoint,
+                      num_heads, num_groups, resblock_updown, bottleneck_attention, additive_skips,
+                      decoder_device_thresh, compute_dtype):
         self.image_size = image_size
         self.in_channels = in_channels
         self.model_channels = model_channels
@@ -110,8 +121,18 @@ class UNetModel(nn.Module):
         self.compute_dtype = compute_dtype
         self._plans = {}
         spec_plan = self._plan(compute_dtype)
-        for name, shape in spec_plan.param_specs:
-            _register(self, name, nn.Parameter(th.empty(shape, dtype=th.float32)))
+        # state_dict order; a reused block's second names (WavUNetModel) alias the owner's Parameter
+        by_pos = {}
+        for name, owner, before in spec_plan.aliases:
+            by_pos.setdefault(before, []).append((name, owner))
+        registered = []
+        specs = spec_plan.param_specs
+        for i in range(len(specs) + 1):
+            for aname, owner in by_pos.get(i, []):
+                _register(self, aname, registered[owner])
+            if i < len(specs):
+                registered.append(nn.Parameter(th.empty(specs[i][1], dtype=th.float32)))
+                _register(self, specs[i][0], registered[-1])
         self._reset_parameters()
         self._param_gen = 0
         self._packed = None
@@ -187,7 +208,7 @@ class UNetModel(nn.Module):
         if key not in self._plans:
             self._plans[key] = UNetPlan(self.in_channels, self.model_channels, self.out_channels,
                                         self.num_res_blocks, self.channel_mult, self.num_groups, dtype,
-                                        resblock_updown=self.resblock_updown)
+                                        resblock_updown=self.resblock_updown, use_freq=self.use_freq)
         return self._plans[key]
 
     @property

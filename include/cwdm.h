@@ -82,6 +82,35 @@ int cwdm_haar_idwt3d_planes(const void* const* bands /* [8] host */, int in_dtyp
                             int64_t B, int64_t C, int64_t d, int64_t h, int64_t w, float* x,
                             cwdm_stream_t stream);
 
+/* cwdm_haar_nd: channels-last multi-channel Haar for the frequency-aware U-Net
+ * (WavUNetModel, guided_diffusion/wunet.py).  Grid (d, h, w) is the COARSE grid.
+ *   inverse 0 (Downsample(use_freq) :120-128 / WaveletDownsample :131-145):
+ *     src fine (B, 2d, 2h, 2w, C) -> out coarse: LLL x lll_scale (+ bias[b][c])
+ *     as (B, d, h, w, C), or with all8 all 8 bands band-major (B, d, h, w, 8C)
+ *     (LLL x lll_scale, the rest x high_scale); high_out (optional): the 7 high
+ *     bands x high_scale, (B, d, h, w, 7C) band-major.
+ *   inverse 1 (Upsample(use_freq) :62-80): IDWT(src x lll_scale, high_in) ->
+ *     out fine (B, 2d, 2h, 2w, C) (+ bias[b][c]).
+ * bias: NULL or fp32 [b * bias_bstride + c]; stats: NULL or fp32
+ * [B][cwdm_haar_nd_parts(d, h, w)][C][2] (sum, sum^2) of out (not with all8).
+ * C: a multiple of 8, <= 2048.  dtype CWDM_F32 / CWDM_BF16. */
+typedef struct {
+  int dtype;
+  int64_t B, d, h, w;
+  int C;
+  int inverse;
+  const void* src;
+  const void* high_in;
+  float lll_scale, high_scale;
+  void* out;
+  int all8;
+  void* high_out;
+  const float* bias; int64_t bias_bstride;
+  float* stats;
+} cwdm_haar_nd_desc;
+int64_t cwdm_haar_nd_parts(int64_t d, int64_t h, int64_t w);
+int cwdm_haar_nd(const cwdm_haar_nd_desc* desc, cwdm_stream_t stream);
+
 /* cwdm_prepare_batch: the i2i front end of training_losses
  * (guided_diffusion/gaussian_diffusion.py:1131-1149) in one pass -- Haar DWT of
  * the target and the three condition volumes (LLL / 3), of the noise image (no
@@ -366,6 +395,8 @@ typedef struct {
   int dtype;          /* storage/compute dtype of activations and weights */
   int resblock_updown; /* 1: ResBlock(down/up=True) resampling (run.sh); 0: Downsample(use_conv=True) stride-2
                           conv / Upsample(use_conv=True) nearest + conv (unet.py:40-100, conv_resample) */
+  int use_freq;        /* 1: WavUNetModel (guided_diffusion/wunet.py, script_util.py:268-292): DWT/IDWT
+                          resampling with high-band skips, wavelet input pyramid; forward only */
 } cwdm_unet_config;
 
 int cwdm_unet_create(const cwdm_unet_config* cfg, cwdm_unet** plan);
@@ -373,6 +404,12 @@ void cwdm_unet_destroy(cwdm_unet* plan);
 int cwdm_unet_num_params(const cwdm_unet* plan);
 int cwdm_unet_param_info(const cwdm_unet* plan, int i, char* name, int name_cap,
                          int64_t* shape /* [5] */, int* ndim);
+/* state_dict keys that alias another parameter (WavUNetModel registers one
+ * decoder ResBlock per level under two prefixes, wunet.py:648-687): alias i
+ * names parameter owner (an index of cwdm_unet_param_info) and sits right
+ * before parameter `before` in state_dict order (num_params: at the end). */
+int cwdm_unet_num_aliases(const cwdm_unet* plan);
+int cwdm_unet_alias_info(const cwdm_unet* plan, int i, char* name, int name_cap, int* owner, int* before);
 int64_t cwdm_unet_packed_bytes(const cwdm_unet* plan);
 /* params: host array of device pointers to fp32 contiguous tensors, state_dict order */
 int cwdm_unet_pack(const cwdm_unet* plan, const float* const* params, void* packed,

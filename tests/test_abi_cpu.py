@@ -6,6 +6,7 @@ import os
 import re
 
 import pytest
+import torch
 
 from conftest import ROOT
 from oracle import unet as ou
@@ -115,3 +116,47 @@ def test_unet_model_accepts_resblock_updown_false():
         UNetModel(image_size=64, in_channels=32, model_channels=32, out_channels=8, num_res_blocks=1,
                   attention_resolutions=(), channel_mult=(1, 2), dims=3, resblock_updown=False, conv_resample=False,
                   bottleneck_attention=False, resample_2d=False, num_groups=8)
+
+
+@pytest.mark.parametrize("cfg", [dict(in_channels=32, model_channels=32, out_channels=8, num_res_blocks=2,
+                                      channel_mult=(1, 2)),
+                                 dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2,
+                                      channel_mult=(1, 2, 2, 4, 4))])
+def test_wavunet_state_dict_matches_oracle(cfg):
+    """script_util.create_model(use_freq=True) -> WavUNetModel: the state_dict
+    (names, shapes, order) equals the reference's, including the second prefix
+    of each reused decoder ResBlock (wunet.py:648-687), and both names share one
+    Parameter (parameters() lists it once)."""
+    from guided_diffusion import script_util
+    from oracle import wunet as ow
+    m = script_util.create_model(image_size=128, num_channels=cfg["model_channels"],
+                                 num_res_blocks=cfg["num_res_blocks"],
+                                 channel_mult=",".join(str(v) for v in cfg["channel_mult"]), attention_resolutions="",
+                                 dims=3, num_groups=8, in_channels=32, out_channels=8, bottleneck_attention=False,
+                                 resblock_updown=True, use_freq=True)
+    sd = m.state_dict(keep_vars=True)
+    want = ow.param_shapes(with_aliases=True, **cfg)
+    assert [(n, tuple(v.shape)) for n, v in sd.items()] == [(n, tuple(s)) for n, s in want]
+    assert len(list(m.parameters())) == len(ow.param_shapes(**cfg))
+    for alias, owner in ow.aliases(**cfg).items():
+        assert sd[alias + ".in_layers.2.weight"] is sd[owner + ".in_layers.2.weight"]
+    if cfg["model_channels"] == 64:
+        assert sum(p.numel() for p in m.parameters()) == 90079304
+    with pytest.raises(NotImplementedError):   # forward-only: no silent detach under autograd
+        m(torch.zeros(1, 32, 32, 32, 32), torch.zeros(1))
+
+
+def test_wavunet_plan_refusals():
+    from cwdm_hip.unet_runtime import UNetPlan
+    from cwdm_hip._lib import CwdmError
+    with pytest.raises(CwdmError, match="resblock_updown"):
+        UNetPlan(32, 32, 8, 2, (1, 2), 8, "fp32", resblock_updown=False, use_freq=True)
+    with pytest.raises(CwdmError, match="num_res_blocks=1"):
+        UNetPlan(32, 32, 8, 1, (1, 2), 8, "fp32", use_freq=True)
+    UNetPlan(32, 32, 8, 1, (1, 1), 8, "fp32", use_freq=True)   # equal channels: the reuse is well-formed
+    plan = UNetPlan(32, 32, 8, 2, (1, 2), 8, "fp32", use_freq=True)
+    with pytest.raises(AssertionError):
+        plan.check_grid(16, 16, 6)    # every level downsamples: edges divisible by 2^levels
+    plan.check_grid(16, 16, 4)
+    with pytest.raises(AssertionError):  # forward-only plan: no gradient workspace
+        plan.grad_workspace_bytes(1, 8, 8, 8)

@@ -456,3 +456,95 @@ def test_fats_per_band_prepare_batch_bitexact():
     reps = torch.cat(list(haar.dwt3d(eps)), 1)
     assert torch.equal(x0.cpu(), rx0)
     assert torch.equal(x_in[:, :8].cpu(), od.q_sample(tab, rx0, t, reps))
+
+
+# --------------------------------------------------------------------------- channels-last Haar (WavUNetModel)
+def _haar_nd(src, C, d, h, w, inverse=0, high_in=None, lll=1.0, high=1.0, all8=0, want_high=False, bias=None,
+             stats=False):
+    """cwdm_haar_nd through the C ABI; src/high_in channels-last device tensors."""
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import check
+    from cwdm_hip.ops import _stream
+    L = _lib.lib()
+    B = src.shape[0]
+    dt = _lib.CWDM_BF16 if src.dtype == torch.bfloat16 else _lib.CWDM_F32
+    shape = (B, 2 * d, 2 * h, 2 * w, C) if inverse else ((B, d, h, w, 8, C) if all8 else (B, d, h, w, C))
+    out = torch.empty(shape, dtype=src.dtype, device=DEV)
+    ho = torch.empty((B, d, h, w, 7, C), dtype=src.dtype, device=DEV) if want_high else None
+    parts = int(L.cwdm_haar_nd_parts(d, h, w))
+    st = torch.empty((B, parts, C, 2), dtype=torch.float32, device=DEV) if stats else None
+    ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    desc = _lib.HaarNdDesc(dtype=dt, B=B, d=d, h=h, w=w, C=C, inverse=inverse, src=ptr(src), high_in=ptr(high_in),
+                           lll_scale=lll, high_scale=high, out=ptr(out), all8=all8, high_out=ptr(ho),
+                           bias=ptr(bias), bias_bstride=C, stats=ptr(st))
+    check(L.cwdm_haar_nd(ctypes.byref(desc), _stream()), "haar_nd")
+    torch.cuda.synchronize()
+    return out, ho, st
+
+
+def _same(a, b, what=""):
+    a, b = a.cpu(), b.cpu()
+    if not torch.equal(a, b):
+        d = (a.double() - b.double()).abs()
+        raise AssertionError(f"{what}: not bit-exact, max |diff| {float(d.max()):.3e} at {int(d.argmax())}")
+
+
+def _cl(x):  # NCDHW -> NDHWC
+    return x.permute(0, 2, 3, 4, 1).contiguous()
+
+
+@pytest.mark.parametrize("C", [32, 96])
+@pytest.mark.parametrize("grid", [(3, 5, 4), (8, 8, 6)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_haar_nd_analysis_vs_oracle(C, grid, dtype):
+    """Downsample(use_freq) of a ResBlock (wunet.py:120-128, :239-252): LLL x 1/3
+    + emb bias and the 7 high bands, bit-exact vs the oracle DWT on the same
+    (dtype-rounded) input; the GroupNorm statistics of the output vs float64."""
+    d, h, w = grid
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(2, C, 2 * d, 2 * h, 2 * w, generator=g).to(dtype)
+    bias = torch.randn(2, C, generator=g)
+    third = torch.tensor(1.0 / 3.0, dtype=torch.float32)
+    out, ho, st = _haar_nd(_cl(x).to(DEV), C, d, h, w, lll=float(third), want_high=True, bias=bias.to(DEV),
+                           stats=True)
+    bands = haar.dwt3d(x.float())
+    ref = (bands[0] * third + bias[:, :, None, None, None]).to(dtype)
+    _same(out, _cl(ref), "LLL")
+    for k in range(7):
+        _same(ho[:, :, :, :, k], _cl(bands[k + 1].to(dtype)), f"band {k + 1}")
+    r64 = (bands[0] * third + bias[:, :, None, None, None]).double()
+    s = st.double().sum(1).cpu()
+    assert torch.allclose(s[..., 0], r64.sum((2, 3, 4)), rtol=1e-5, atol=1e-4)
+    assert torch.allclose(s[..., 1], (r64 * r64).sum((2, 3, 4)), rtol=1e-5, atol=1e-4)
+
+
+def test_haar_nd_all_bands_pyramid_vs_oracle():
+    """WaveletDownsample input (wunet.py:141-144): cat(8 bands) / 3, band-major
+    channels, bit-exact vs the oracle."""
+    g = torch.Generator().manual_seed(32)
+    x = torch.randn(1, 32, 8, 12, 6, generator=g)
+    third = torch.tensor(1.0 / 3.0, dtype=torch.float32)
+    out, _, _ = _haar_nd(_cl(x).to(DEV), 32, 4, 6, 3, lll=float(third), high=float(third), all8=1)
+    ref = torch.cat([b * third for b in haar.dwt3d(x)], dim=1)
+    _same(out.reshape(1, 4, 6, 3, 256), _cl(ref), "all bands")
+
+
+@pytest.mark.parametrize("C", [64, 40])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_haar_nd_synthesis_vs_oracle(C, dtype):
+    """Upsample(use_freq) of a ResBlock (wunet.py:62-80, :236-252): IDWT(3 h,
+    skip bands) + emb bias, bit-exact vs the oracle IDWT; statistics vs float64."""
+    d, h, w = 4, 3, 5
+    g = torch.Generator().manual_seed(33)
+    low = torch.randn(2, C, d, h, w, generator=g).to(dtype)
+    highs = [torch.randn(2, C, d, h, w, generator=g).to(dtype) for _ in range(7)]
+    bias = torch.randn(2, C, generator=g)
+    hi = torch.stack([_cl(b) for b in highs], dim=4).contiguous()
+    out, _, st = _haar_nd(_cl(low).to(DEV), C, d, h, w, inverse=1, high_in=hi.to(DEV), lll=3.0, bias=bias.to(DEV),
+                          stats=True)
+    rf = haar.idwt3d(low.float() * 3.0, *[b.float() for b in highs]) + bias[:, :, None, None, None]
+    _same(out, _cl(rf.to(dtype)), "synthesis")
+    s = st.double().sum(1).cpu()
+    r64 = rf.double()
+    assert torch.allclose(s[..., 0], r64.sum((2, 3, 4)), rtol=1e-5, atol=1e-4)
+    assert torch.allclose(s[..., 1], (r64 * r64).sum((2, 3, 4)), rtol=1e-5, atol=1e-4)

@@ -364,3 +364,66 @@ def test_fats_sampling_loop_vs_oracle(sampler):
                                       noise_fn=lambda x: next(it))
         ref = od.p_sample_loop(tab, om, x_T, cond, noises)
     assert rel_err(out, ref) < 1e-3
+
+
+WU_CFGS = {
+    "tiny": (dict(in_channels=32, model_channels=32, out_channels=8, num_res_blocks=2, channel_mult=(1, 2)), 8,
+             (16, 16, 16)),
+    "three": (dict(in_channels=32, model_channels=32, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2)), 8,
+              (32, 16, 24)),
+    # script_util's use_freq model at the production topology (mc 64, (1, 2, 2, 4, 4), 90.1M parameters);
+    # 32^3 puts the deepest level at 1^3
+    "prod": (dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2,
+                  channel_mult=(1, 2, 2, 4, 4)), 32, (32, 32, 32)),
+}
+
+
+def _wavunet(k, dtype, seed=21):
+    from guided_diffusion import script_util
+    from oracle import wunet as ow
+    cfg, G, grid = WU_CFGS[k]
+    m = script_util.create_model(image_size=128, num_channels=cfg["model_channels"],
+                                 num_res_blocks=cfg["num_res_blocks"],
+                                 channel_mult=",".join(str(v) for v in cfg["channel_mult"]), attention_resolutions="",
+                                 dims=3, num_groups=G, in_channels=cfg["in_channels"],
+                                 out_channels=cfg["out_channels"], bottleneck_attention=False, resample_2d=False,
+                                 resblock_updown=True, use_freq=True, compute_dtype=dtype)
+    P = ow.random_params(seed=seed, **cfg)
+    full = dict(P)
+    for alias, owner in ow.aliases(**cfg).items():
+        for n, v in P.items():
+            if n.startswith(owner + "."):
+                full[alias + n[len(owner):]] = v
+    m.load_state_dict(full)
+    return m.to(DEV), P, cfg, G, grid
+
+
+@pytest.mark.parametrize("k,dtype,tol", [("tiny", "fp32", 1e-3), ("three", "fp32", 1e-3), ("prod", "fp32", 1e-3),
+                                         ("tiny", "bf16", 6e-2)])
+def test_wavunet_forward_vs_oracle(k, dtype, tol):
+    """WavUNetModel (use_freq=True, wunet.py:754-795) forward on the native plan:
+    DWT/IDWT ResBlocks, wavelet input pyramid, the reused decoder ResBlock
+    (two state_dict names, run twice) -- output and every block's activation
+    vs the oracle restatement."""
+    from oracle import wunet as ow
+    m, P, cfg, G, grid = _wavunet(k, dtype)
+    g = torch.Generator().manual_seed(22)
+    x = torch.randn(2, 32, *grid, generator=g)
+    t = torch.tensor([37, 801])
+    trace = []
+    ref = ow.wunet_forward(P, x, t, num_groups=G, trace=trace, **cfg)
+    with torch.no_grad():
+        out = m(x.to(DEV), t.to(DEV))
+    assert rel_err(out, ref) < tol
+    got = m.plan.trace_tensors(m.plan.workspace(2, *grid, DEV), 2, *grid)
+    assert len(got) == len(trace)
+    for i, (gt, rf) in enumerate(zip(got, trace)):
+        if gt is not None:
+            assert rel_err(gt.float().permute(0, 4, 1, 2, 3), rf) < tol, i
+
+
+def test_wavunet_refuses_training():
+    m, _, _, _, grid = _wavunet("tiny", "fp32")
+    x = torch.randn(1, 32, *grid, device=DEV)
+    with pytest.raises(NotImplementedError):
+        m(x, torch.tensor([3], device=DEV))
