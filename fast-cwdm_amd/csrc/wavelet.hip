@@ -407,11 +407,17 @@ extern "C" int cwdm_sample_finish(const float* sample, int64_t B, int64_t d, int
   return CWDM_OK;
 }
 
+namespace cwdm {
+int sampler2_launch(const cwdm_sampler_args* a, hipStream_t s);  // wavelet2.hip
+}
+
 extern "C" int cwdm_sampler_step(const cwdm_sampler_args* a, cwdm_stream_t stream) {
   CWDM_REQUIRE(a && a->model_out && a->x_t && a->x_prev && a->coef && a->t, CWDM_E_INVALID,
                "cwdm_sampler_step: null pointer");
   CWDM_REQUIRE(a->B > 0 && a->d > 0 && a->h > 0 && a->w > 0 && a->T > 0, CWDM_E_SHAPE,
                "cwdm_sampler_step: empty shape");
+  CWDM_REQUIRE(a->levels >= 0 && a->levels <= 2, CWDM_E_UNSUPPORTED, "cwdm_sampler_step: levels must be 1 or 2");
+  if (a->levels == 2) return cwdm::sampler2_launch(a, (hipStream_t)stream);
   int64_t n = a->B * a->d * a->h * a->w;
   dim3 grid((unsigned)ceil_div(n, 256));
   S3 mo = s3(a->mo_s), xt = s3(a->xt_s), xp = s3(a->xp_s), nz = s3(a->nz_s), px = s3(a->px_s),

@@ -36,6 +36,7 @@ class SamplerArgs(ctypes.Structure):
         ("mean_type", ctypes.c_int),
         ("update", ctypes.c_int),
         ("per_band", ctypes.c_int),
+        ("levels", ctypes.c_int),
     ]
 
 
@@ -158,6 +159,8 @@ _PROTOS = {
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "cwdm_haar_nd_parts": (i64, [i64, i64, i64]),
     "cwdm_haar_nd": (ctypes.c_int, [ctypes.POINTER(HaarNdDesc), vp]),
+    "cwdm_wavelet2_analysis": (ctypes.c_int, [vp, i64, i64, i64, i64, vp, ctypes.c_int, i64, i64, ctypes.c_int, vp]),
+    "cwdm_wavelet2_synthesis": (ctypes.c_int, [vp, i64, i64, i64, i64, i64, i64, ctypes.c_int, vp, vp]),
     "cwdm_unet_param_info": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(i64),
                                             ctypes.POINTER(ctypes.c_int)]),
     "cwdm_unet_packed_bytes": (i64, [vp]),

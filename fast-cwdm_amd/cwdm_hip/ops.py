@@ -124,9 +124,10 @@ def ndhwc_strides(B, C, V, c_total=None):
 
 def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t, T, B, d, h, w,
                  clip_denoised=True, pred_xstart=None, px_s=(0, 0, 0), mirror=None, mr_s=(0, 0, 0),
-                 mean_type=0, update=0, per_band=False):
+                 mean_type=0, update=0, per_band=False, levels=1):
     """Fused process_xstart + posterior mean + noise (cwdm_sampler_step);
-    update=1: the DDIM step instead of the posterior mean + noise."""
+    update=1: the DDIM step instead of the posterior mean + noise; levels=2:
+    the 64-channel two-level block representation (config 5, wavelet2_*)."""
     _need_cuda(model_out, x_t, x_prev, noise, coef, t, pred_xstart, mirror)
     a = _lib.SamplerArgs()
     a.model_out, a.mo_s = model_out.data_ptr(), _lib.I64x3(*mo_s)
@@ -145,7 +146,46 @@ def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t,
     a.mean_type = int(mean_type)
     a.update = int(update)
     a.per_band = 1 if per_band else 0
+    a.levels = int(levels)
     check(lib().cwdm_sampler_step(ctypes.byref(a), _stream()), "sampler_step")
+
+
+# ---- two-level block representation (config 5; specification oracle/wavelet2.py) ----
+def wavelet2_analysis(x, out=None, c0=0, dtype=None):
+    """(B, 1, D, H, W) fp32 image (edges multiples of 4) -> 64 coefficient
+    channels per voxel of the (D/4, H/4, W/4) grid, channels-last.  ``out``:
+    an existing channels-last (B, d, h, w, C) buffer (fp32 or bf16) written at
+    channels [c0, c0 + 64), e.g. a slice of the U-Net input; else a new fp32
+    (B, d, h, w, 64) tensor."""
+    _need_cuda(x, out)
+    if x.dim() != 5 or x.shape[1] != 1:
+        raise AssertionError("wavelet2_analysis expects a (B, 1, D, H, W) image")
+    B, _, D, H, W = x.shape
+    if D % 4 or H % 4 or W % 4:
+        raise AssertionError(f"wavelet2_analysis: edges must be multiples of 4 (got {D}x{H}x{W})")
+    x = x.contiguous().float()
+    d, h, w = D // 4, H // 4, W // 4
+    if out is None:
+        out = torch.empty((B, d, h, w, 64), dtype=dtype or torch.float32, device=x.device)
+    if tuple(out.shape[:4]) != (B, d, h, w) or out.shape[4] < c0 + 64 or not out.is_contiguous():
+        raise AssertionError("wavelet2_analysis: out must be a contiguous (B, d, h, w, >= c0 + 64) tensor")
+    C = out.shape[4]
+    check(lib().cwdm_wavelet2_analysis(x.data_ptr(), B, D, H, W, out.data_ptr(), DT[out.dtype], d * h * w * C, C,
+                                       c0, _stream()), "wavelet2_analysis")
+    return out
+
+
+def wavelet2_synthesis(coef, c0=0):
+    """Inverse of wavelet2_analysis: channels-last fp32 (B, d, h, w, C >= c0 + 64)
+    -> (B, 1, 4d, 4h, 4w) fp32 image."""
+    _need_cuda(coef)
+    if coef.dim() != 5 or coef.shape[4] < c0 + 64 or coef.dtype != torch.float32 or not coef.is_contiguous():
+        raise AssertionError("wavelet2_synthesis expects contiguous fp32 (B, d, h, w, >= c0 + 64) coefficients")
+    B, d, h, w, C = coef.shape
+    out = torch.empty((B, 1, 4 * d, 4 * h, 4 * w), dtype=torch.float32, device=coef.device)
+    check(lib().cwdm_wavelet2_synthesis(coef.data_ptr(), B, d, h, w, d * h * w * C, C, c0, out.data_ptr(), _stream()),
+          "wavelet2_synthesis")
+    return out
 
 
 # ---- multi-level Haar (BASELINE config 5, SURVEY.md §8(f) f4) ---------------

@@ -162,9 +162,25 @@ typedef struct {
   int clip_denoised;
   int mean_type;        /* 0 START_X (model predicts x0), 1 EPSILON */
   int update;           /* 0 ancestral p_sample, 1 DDIM */
-  int per_band;         /* coef is [T][8 bands][8]: one schedule per subband (FATS, guided_diffusion/fats.py) */
+  int per_band;         /* coef is [T][C][8]: one schedule per subband channel (FATS, guided_diffusion/fats.py) */
+  int levels;           /* 0 / 1: 8 single-level subbands; 2: the 64-channel 2-level block representation of
+                           config 5 (cwdm_wavelet2_*), process_xstart = 2-level inverse -> clamp -> forward */
 } cwdm_sampler_args;
 int cwdm_sampler_step(const cwdm_sampler_args* args, cwdm_stream_t stream);
+
+/* Config 5 (BASELINE.json: 2-level DWT + FATS, 224^3; no reference code --
+ * the specification is oracle/wavelet2.py).  Per modality 64 channels on the
+ * level-2 grid: the 8 level-2 bands (LLL2 / 3 after LLL1 / 3, then the 7
+ * details), then the 7 level-1 detail bands folded 2x2x2 -> 8 channels each
+ * (phase 4 pz + 2 py + px).  analysis: x (B, 1, D, H, W) fp32 contiguous, D, H,
+ * W multiples of 4 -> out[b * out_bs + v * out_vs + out_c0 + j] (j < 64, v over
+ * the (D/4, H/4, W/4) grid), fp32 or bf16 -- e.g. straight into a channel
+ * slice of the channels-last U-Net input.  synthesis: the inverse, fp32
+ * coefficients -> (B, 1, 4d, 4h, 4w) fp32. */
+int cwdm_wavelet2_analysis(const float* x, int64_t B, int64_t D, int64_t H, int64_t W, void* out, int out_dtype,
+                           int64_t out_bs, int64_t out_vs, int out_c0, cwdm_stream_t stream);
+int cwdm_wavelet2_synthesis(const float* coef, int64_t B, int64_t d, int64_t h, int64_t w, int64_t c_bs,
+                            int64_t c_vs, int c_c0, float* out, cwdm_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Volume I/O either side of the wavelet path.

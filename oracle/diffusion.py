@@ -133,8 +133,10 @@ def process_xstart(x):
     return haar.dwt_cat(img)
 
 
-def p_mean_variance(tab, model, x, t, cond, clip_denoised=True):
-    """i2i branch with START_X and FIXED_LARGE (gaussian_diffusion.py:269-388)."""
+def p_mean_variance(tab, model, x, t, cond, clip_denoised=True, process=None):
+    """i2i branch with START_X and FIXED_LARGE (gaussian_diffusion.py:269-388).
+    ``process``: the process_xstart to use (default the single-level one;
+    oracle.wavelet2.process_xstart2 for the 2-level config-5 representation)."""
     B = x.shape[0]
     assert t.shape == (B,)
     x_cond = torch.cat([x, cond], dim=1)
@@ -142,21 +144,21 @@ def p_mean_variance(tab, model, x, t, cond, clip_denoised=True):
     out = model(x_cond, model_t)
     var = extract(tab.fixed_large_variance, t, x.shape)
     logvar = extract(tab.fixed_large_log_variance, t, x.shape)
-    pred = process_xstart(out) if clip_denoised else out
+    pred = (process or process_xstart)(out) if clip_denoised else out
     mean = extract(tab.posterior_mean_coef1, t, x.shape) * pred + \
-        extract(tab.posterior_mean_coef2, t, x.shape) * x[:, :8]
+        extract(tab.posterior_mean_coef2, t, x.shape) * x
     return {"mean": mean, "variance": var, "log_variance": logvar, "pred_xstart": pred, "model_output": out}
 
 
-def p_sample(tab, model, x, t, cond, noise, clip_denoised=True):
+def p_sample(tab, model, x, t, cond, noise, clip_denoised=True, process=None):
     """gaussian_diffusion.py:529-574 with the step noise passed in."""
-    out = p_mean_variance(tab, model, x, t, cond, clip_denoised)
+    out = p_mean_variance(tab, model, x, t, cond, clip_denoised, process)
     mask = (t != 0).float().view(-1, *([1] * (x.dim() - 1)))
     sample = out["mean"] + mask * torch.exp(0.5 * out["log_variance"]) * noise
     return {"sample": sample, "pred_xstart": out["pred_xstart"], "model_output": out["model_output"]}
 
 
-def p_sample_loop(tab, model, x_T, cond, step_noises, time=None, clip_denoised=True):
+def p_sample_loop(tab, model, x_T, cond, step_noises, time=None, clip_denoised=True, process=None):
     """p_sample_loop_progressive (gaussian_diffusion.py:668-719); ``time``
     defaults to num_timesteps (the reference's default of 1000 only works
     for T=1000)."""
@@ -164,7 +166,7 @@ def p_sample_loop(tab, model, x_T, cond, step_noises, time=None, clip_denoised=T
     img = x_T
     for k, i in enumerate(range(time - 1, -1, -1)):
         t = torch.full((x_T.shape[0],), i, dtype=torch.int64)
-        img = p_sample(tab, model, img, t, cond, step_noises[k], clip_denoised)["sample"]
+        img = p_sample(tab, model, img, t, cond, step_noises[k], clip_denoised, process)["sample"]
     return img
 
 
@@ -185,12 +187,12 @@ def training_losses(tab, model, x_start, t, noise_img, contr="t1n"):
     return {"mse_wav": mse}, out, out_idwt
 
 
-def ddim_sample(tab, model, x, t, cond, clip_denoised=True, eta=0.0):
+def ddim_sample(tab, model, x, t, cond, clip_denoised=True, eta=0.0, process=None):
     """Spec-defined i2i DDIM step (the reference raises for
     i2i).  Follows ddim_sample's formulas (gaussian_diffusion.py:721-784) with
     the i2i conditioning of p_mean_variance; returns mean_pred like the
     reference does (:784).  Parity unpinned against the reference."""
-    out = p_mean_variance(tab, model, x, t, cond, clip_denoised)
+    out = p_mean_variance(tab, model, x, t, cond, clip_denoised, process)
     shape = x.shape
     eps = (extract(tab.sqrt_recip_alphas_cumprod, t, shape) * x - out["pred_xstart"]) / \
         extract(tab.sqrt_recipm1_alphas_cumprod, t, shape)
@@ -201,12 +203,12 @@ def ddim_sample(tab, model, x, t, cond, clip_denoised=True, eta=0.0):
     return {"sample": mean_pred, "pred_xstart": out["pred_xstart"]}
 
 
-def ddim_sample_loop(tab, model, x_T, cond, clip_denoised=True, eta=0.0, time=None):
+def ddim_sample_loop(tab, model, x_T, cond, clip_denoised=True, eta=0.0, time=None, process=None):
     """ddim_sample_loop_progressive (gaussian_diffusion.py:974-1047) over the
     (respaced) tables, t = time-1 ... 0, each step feeding mean_pred back."""
     time = tab.num_timesteps if time is None else time
     img = x_T
     for i in range(time - 1, -1, -1):
         t = torch.full((x_T.shape[0],), i, dtype=torch.int64)
-        img = ddim_sample(tab, model, img, t, cond, clip_denoised, eta)["sample"]
+        img = ddim_sample(tab, model, img, t, cond, clip_denoised, eta, process)["sample"]
     return img

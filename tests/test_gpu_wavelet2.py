@@ -1,0 +1,155 @@
+"""Config 5 (BASELINE.json: 2-level DWT + FATS per-band schedule; spec-only,
+SURVEY.md §8(d) C5) on the GPU: the 64-channel two-level block
+representation (csrc/wavelet2.hip) bit-exact against its oracle
+(oracle/wavelet2.py, pinned to PyWavelets wavedecn in
+tests/test_wavelet2_cpu.py), the 2-level fused sampler step, and the whole
+native HIP-graph loop with FATS per-subband schedules vs the oracle loop."""
+import pytest
+import torch
+
+from oracle import cases, diffusion as od, unet as ou, wavelet2 as w2
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _same(a, b, what=""):
+    a, b = a.cpu(), b.cpu()
+    if not torch.equal(a, b):
+        d = (a.double() - b.double()).abs()
+        raise AssertionError(f"{what}: not bit-exact, max |diff| {float(d.max()):.3e}")
+
+
+def _cl(x):
+    return x.permute(0, 2, 3, 4, 1).contiguous()
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 4, 4, 4), (2, 1, 8, 12, 16), (1, 1, 32, 16, 24)])
+def test_wavelet2_analysis_synthesis_bitexact(shape):
+    from cwdm_hip import ops
+    x = torch.rand(shape, generator=torch.Generator().manual_seed(3))
+    ref = w2.analysis2(x)
+    got = ops.wavelet2_analysis(x.to(DEV))
+    _same(got, _cl(ref), "analysis")
+    _same(ops.wavelet2_synthesis(got), w2.synthesis2(ref), "synthesis")
+    assert (ops.wavelet2_synthesis(got).cpu() - x).abs().max() < 1e-5
+
+
+def test_wavelet2_analysis_into_channel_slice_bf16():
+    """Straight into channels [64, 128) of a bf16 channels-last U-Net input."""
+    from cwdm_hip import ops
+    x = torch.rand(2, 1, 8, 8, 12, generator=torch.Generator().manual_seed(4))
+    buf = torch.zeros(2, 2, 2, 3, 256, dtype=torch.bfloat16, device=DEV)
+    ops.wavelet2_analysis(x.to(DEV), out=buf, c0=64)
+    _same(buf[..., 64:128], _cl(w2.analysis2(x)).to(torch.bfloat16), "bf16 slice")
+    assert buf[..., :64].abs().max() == 0 and buf[..., 128:].abs().max() == 0
+
+
+@pytest.mark.parametrize("clip,mean_type,per_band", [(True, 0, False), (True, 1, True), (False, 0, True)])
+def test_sampler2_step_vs_oracle(clip, mean_type, per_band):
+    """cwdm_sampler_step(levels=2): 2-level process_xstart + posterior + noise
+    (per-channel FATS rows when per_band) vs the oracle, NCDHW strides."""
+    from guided_diffusion import script_util
+    shift = [-1.0 + 0.15 * k for k in range(15)] if per_band else None
+    d = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=(mean_type == 0), mode="i2i",
+                                              wavelet_levels=2, band_log_snr_shift=shift)
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"),
+                    band_shift=w2.channel_shift(shift) if per_band else None)
+    g = torch.Generator().manual_seed(5)
+    B, n = 3, 3
+    mo = torch.rand(B, 64, n, n, n, generator=g) * 0.4
+    x = torch.randn(B, 64, n, n, n, generator=g)
+    noise = torch.randn(B, 64, n, n, n, generator=g)
+    t = torch.tensor([0, 17, 999])
+    sample, pred = d._epilogue(mo.to(DEV), x.to(DEV), t.to(DEV), clip, None, noise.to(DEV))
+    if mean_type == 0:
+        x0 = mo
+    else:
+        x0 = od.extract(tab.sqrt_recip_alphas_cumprod, t, x.shape) * x - \
+            od.extract(tab.sqrt_recipm1_alphas_cumprod, t, x.shape) * mo
+    pref = w2.process_xstart2(x0) if clip else x0
+    mean = od.extract(tab.posterior_mean_coef1, t, x.shape) * pref + od.extract(tab.posterior_mean_coef2, t, x.shape) * x
+    mask = (t != 0).float().view(-1, 1, 1, 1, 1)
+    sref = mean + mask * torch.exp(0.5 * od.extract(tab.fixed_large_log_variance, t, x.shape)) * noise
+    assert rel_err(pred, pref) < 1e-6
+    assert rel_err(sample, sref) < 1e-6
+
+
+C5_CFG = dict(in_channels=256, model_channels=32, out_channels=64, num_res_blocks=1, channel_mult=(1, 2, 2))
+
+
+def _c5_model(dtype="fp32"):
+    from guided_diffusion import script_util
+    return script_util.create_model(image_size=32, num_channels=32, num_res_blocks=1, channel_mult="1,2,2",
+                                    attention_resolutions="", dims=3, num_groups=8, in_channels=256,
+                                    out_channels=64, bottleneck_attention=False, resample_2d=False,
+                                    resblock_updown=True, compute_dtype=dtype)
+
+
+@pytest.mark.parametrize("sampler", ["ddpm", "ddim"])
+def test_config5_fats_loop_vs_oracle(sampler):
+    """The config-5 pipeline at a reduced size: 32^3 images -> 2-level
+    analysis (cond straight into the channels-last model input) -> 3-level
+    U-Net on the 8^3 level-2 grid (256 -> 64 channels) -> 2-level fused
+    sampler step with FATS per-subband schedules, HIP-graph loop over ddim10
+    tables; vs the oracle loop (process_xstart2, per-channel tables), fp32 1e-3."""
+    from cwdm_hip import ops
+    from guided_diffusion import script_util
+    shift = [-1.5, 0.2, 0.3, 0.5, 0.2, 0.4, 0.6, 1.0] + [0.8, 1.0, 1.2, 1.0, 1.2, 1.4, 1.8]
+    diffusion = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
+                                                      timestep_respacing="ddim10", band_log_snr_shift=shift,
+                                                      wavelet_levels=2)
+    P = ou.random_params(seed=2, **C5_CFG)
+    model = _c5_model()
+    model.load_state_dict(P)
+    model.to(DEV)
+    vols = cases.data.brats_batch(32, seed=9, batch=1)
+    cond = torch.cat([w2.analysis2(vols[k]) for k in ("t1c", "t2w", "t2f")], dim=1)
+    cond_dev = torch.cat([ops.wavelet2_analysis(vols[k].to(DEV)).permute(0, 4, 1, 2, 3) for k in ("t1c", "t2w", "t2f")],
+                         dim=1)
+    _same(cond_dev, cond, "cond analysis")
+    g = torch.Generator().manual_seed(12)
+    x_T = torch.randn(1, 64, 8, 8, 8, generator=g)
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"), use_timesteps=od.space_timesteps(1000, "ddim10"),
+                    band_shift=w2.channel_shift(shift))
+    om = ou.OracleUNet(P, num_groups=8, **C5_CFG)
+    if sampler == "ddim":
+        out = diffusion.ddim_sample_loop(model, x_T.shape, noise=x_T.to(DEV), cond=cond_dev.contiguous())
+        ref = od.ddim_sample_loop(tab, om, x_T, cond, process=w2.process_xstart2)
+    else:
+        noises = [torch.randn(x_T.shape, generator=g) for _ in range(10)]
+        it = iter([z.to(DEV) for z in noises])
+        out = diffusion.p_sample_loop(model, x_T.shape, noise=x_T.to(DEV), cond=cond_dev.contiguous(), progress=False,
+                                      noise_fn=lambda x: next(it))
+        ref = od.p_sample_loop(tab, om, x_T, cond, noises, process=w2.process_xstart2)
+    assert rel_err(out, ref) < 1e-3
+    img = ops.wavelet2_synthesis(_cl(out).contiguous())
+    assert img.shape == (1, 1, 32, 32, 32)
+    assert torch.allclose(img.cpu(), w2.synthesis2(ref), atol=1e-3 * float(ref.abs().max()) * 8)
+
+
+def test_config5_graph_loop_bf16_runs_at_224():
+    """The config-5 sizes themselves: 224^3 -> 56^3 x 64 channels, bf16 graph
+    loop, 3 steps; finite, and the eager loop agrees with the graph replay."""
+    from guided_diffusion import script_util
+    model = script_util.create_model(image_size=224, num_channels=64, num_res_blocks=2, channel_mult="1,2,2",
+                                     attention_resolutions="", dims=3, num_groups=32, in_channels=256,
+                                     out_channels=64, bottleneck_attention=False, resample_2d=False,
+                                     resblock_updown=True, compute_dtype="bf16").to(DEV)
+    diffusion = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
+                                                      timestep_respacing="3", wavelet_levels=2)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    cond = torch.rand(1, 192, 56, 56, 56, device=DEV, generator=g)
+    x_T = torch.randn(1, 64, 56, 56, 56, device=DEV, generator=g)
+    outs = []
+    for graph in (True, False):
+        diffusion.use_hip_graph = graph
+        torch.manual_seed(0)
+        outs.append(diffusion.p_sample_loop(model, x_T.shape, noise=x_T, cond=cond, progress=False))
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
