@@ -199,6 +199,56 @@ def train_leg(model, diffusion, n, rank, world, device, steps, warmup, sync, max
             "scaling": "weak"}
 
 
+def config5_leg(args, device, rank, world, sync, max_over_ranks):
+    """Config 5 (spec-only): 224^3 phantoms -> 2-level block
+    wavelet analysis (56^3 x 64 channels per modality, straight from the GPU
+    kernel) -> 3-level U-Net (256 -> 64 channels, mc 64, mult 1,2,2) -> the
+    2-level fused sampler step with FATS per-subband schedules (shifts from
+    the conditioning's subband energies), HIP-graph-captured loop, bf16."""
+    from cwdm_hip import ops
+    from guided_diffusion import fats, script_util
+    n = 224
+    g = n // 4
+    model = script_util.create_model(image_size=n, num_channels=64, num_res_blocks=2, channel_mult="1,2,2",
+                                     attention_resolutions="", dims=3, num_groups=32, in_channels=256,
+                                     out_channels=64, bottleneck_attention=False, resample_2d=False,
+                                     resblock_updown=True, compute_dtype=args.dtype)
+    seeded_weights(model, 5)
+    model.to(device)
+    t0 = time.perf_counter()
+    cond_cl = torch.empty(1, g, g, g, 192, device=device)
+    for k in range(3):
+        ops.wavelet2_analysis(phantom_gpu(n, 500 + 10 * rank + k, device), out=cond_cl, c0=64 * k)
+    sync()
+    t_front = time.perf_counter() - t0
+    cond = cond_cl.permute(0, 4, 1, 2, 3)
+    shifts = fats.band_log_snr_shifts(
+        fats.subband_energy(cond[:, :64], levels=2) + fats.subband_energy(cond[:, 64:128], levels=2))
+    diffusion = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
+                                                      band_log_snr_shift=shifts, wavelet_levels=2)
+    torch.manual_seed(4321 + rank)
+    x_T = torch.randn(1, 64, g, g, g, device=device)
+    K = args.config5
+    loop = diffusion._native_loop(model, x_T, list(range(1000))[::-1][:K + 4], cond.contiguous(), True,
+                                  graph=bool(args.graph), fresh_outputs=False, need_pred=False)
+    dt = max_over_ranks(time_loop(loop, (3, K), world, sync))
+    loop.close()
+    per = dt / K
+    fl = model.plan.flops(1, g, g, g)
+    res = {"workload": "config5: 224^3 input, 2-level block wavelet (56^3 x 64 ch per modality, 15 subbands), "
+                       "FATS per-subband schedules, 3-level U-Net (256->64 ch, mc 64, mult 1,2,2, 2 res blocks), "
+                       f"{args.dtype}, {'HIP-graph' if args.graph else 'eager'} loop, one volume per GPU",
+           "denoising_steps_per_s": round(world * K / dt, 3), "ms_per_step": round(1000 * per, 3), "steps": K,
+           "s_per_volume": {"1000_steps": round(1000 * per, 2), "50_steps": round(50 * per, 3)},
+           "front_end_ms": round(1000 * t_front, 2), "unet_tflop_per_step": round(fl / 1e12, 3),
+           "mfma_frac": round(fl / per / 1e12 / BF16_PEAK_TFLOPS, 4),
+           "precision_note": "fp16 requested by the config is served by bf16 (same MFMA rate on gfx950; the "
+                             "reference's use_fp16 is a no-op, DESIGN.md)"}
+    del model, loop
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -215,6 +265,8 @@ def main():
                          "0 = skip); reported beside, never as, the B=1 metric")
     ap.add_argument("--fp32", type=int, default=3, help="also time K steps of the fp32 parity mode (0 = skip)")
     ap.add_argument("--train", type=int, default=5, help="config-3 train_ddp side figure: timed steps (0 = skip)")
+    ap.add_argument("--config5", type=int, default=10, help="config-5 side figure (224^3, 2-level wavelets + FATS): "
+                                                            "timed steps (0 = skip)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the rank launch / barrier / max-over-ranks plumbing only")
     args = ap.parse_args()
@@ -362,6 +414,10 @@ def main():
         cpu_state = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
         cpu_cond, cpu_x = cond.cpu(), x_T.cpu()
 
+    config5 = None
+    if args.config5:
+        config5 = config5_leg(args, device, rank, world, sync, max_over_ranks)
+
     train = None
     if args.train:
         train = train_leg(model, diffusion, n, rank, world, device, args.train, 2, sync, max_over_ranks)
@@ -404,6 +460,7 @@ def main():
         "batched_serving": batched,
         "fp32_parity_mode": fp32,
         "train_ddp": train,
+        "config5_224": config5,
         "mfma_util_whole_step": round(step_flops * (value / world) / 1e12 / peak, 4),
         "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,

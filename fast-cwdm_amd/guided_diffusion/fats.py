@@ -33,6 +33,19 @@ def band_energy(x0_bands):
     return e.cpu().numpy()
 
 
+def subband_energy(coef, levels=1):
+    """band_energy for either representation: (B, 8, ...) single-level bands
+    -> [8]; (B, 64, ...) two-level block coefficients (config 5,
+    oracle/wavelet2.py) -> [15] (LLL2, 7 level-2 details, 7 level-1 details,
+    each level-1 band's 8 folded phases pooled)."""
+    e = band_energy(coef)
+    if levels == 1:
+        return e
+    if e.shape[0] != 64:
+        raise AssertionError("two-level coefficients have 64 channels")
+    return np.concatenate([e[:8], e[8:].reshape(7, 8).mean(axis=1)])
+
+
 def band_log_snr_shifts(energy, strength=1.0, max_shift=4.0, floor=1e-12):
     """shift_k = strength * (mean_j log E_j - log E_k), clipped to +-max_shift."""
     le = np.log(np.maximum(np.asarray(energy, dtype=np.float64), floor))
@@ -51,4 +64,4 @@ def create_fats_diffusion(energy=None, shifts=None, strength=1.0, max_shift=4.0,
     return create_gaussian_diffusion(band_log_snr_shift=np.asarray(shifts, dtype=np.float64), **diffusion_kwargs)
 
 
-__all__ = ["band_energy", "band_log_snr_shifts", "create_fats_diffusion"]
+__all__ = ["band_energy", "subband_energy", "band_log_snr_shifts", "create_fats_diffusion"]
