@@ -1,6 +1,6 @@
 """Per-launch timeline of one denoising step from a rocprofv3 kernel trace of
 bench.py (the last complete step: between the last two sampler launches).
-usage: python tools/trace_step.py gpurun_out/TAG/trace [--agg]"""
+usage: python tools/trace_step.py gpurun_out/TAG/trace [--agg] [--last]"""
 import csv
 import glob
 import os
@@ -23,7 +23,10 @@ def short(n):
 def main():
     rows = load(sys.argv[1])
     samp = [i for i, r in enumerate(rows) if "sampler_kernel" in r["Kernel_Name"]]
-    a, b = samp[-2] + 1, samp[-1] + 1
+    # the last step of the timed (graph-replayed) loop: bench.py ends with one
+    # eager profiling step whose setup copies would otherwise land in it
+    k = -2 if "--last" not in sys.argv else -1
+    a, b = samp[k - 1] + 1, samp[k] + 1
     step = rows[a:b]
     tot = 0.0
     agg = defaultdict(lambda: [0, 0.0])
