@@ -100,7 +100,7 @@ std::atomic<int> g_conv_path{[] {
 std::atomic<unsigned long long*> g_stamps{nullptr};
 
 int64_t v4_items(const cwdm_conv3d_desc* d) {
-  return d->B * (d->W / 32) * (d->H / 4) * (d->D / 4) * (d->cout / 64);
+  return d->B * ((d->W + 31) / 32) * (d->H / 4) * (d->D / 4) * (d->cout / 64);
 }
 
 // work items a launch aims for before it splits K (env CWDM_V4_KSPLIT_TARGET)
@@ -130,7 +130,8 @@ bool v4_eligible(const cwdm_conv3d_desc* d) {
   const int path = g_conv_path.load(std::memory_order_relaxed);
   if (path == 1) return false;
   if (d->dtype != CWDM_BF16 && d->dtype != CWDM_F32) return false;
-  if (!d->a_w || d->W % 32 || d->H % 4 || d->D % 4 || d->cout % 64) return false;
+  // W >= 32: the statistics partials follow cwdm_conv3d_parts' 32-wide x tiles (pick_brick)
+  if (!d->a_w || d->W < 32 || d->H % 4 || d->D % 4 || d->cout % 64) return false;
   if (d->a_mode != 0 && d->a_mode != 1) return false;
   if (d->res_mode < -1 || d->res_mode > 1) return false;
   if (d->out1 && d->out_c0 % 8) return false;
@@ -184,7 +185,7 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   const int64_t SV = src_voxels(d);
   V4Params p{};
   p.B = (int)d->B; p.D = (int)d->D; p.H = (int)d->H; p.W = (int)d->W;
-  p.tx = p.W / 32; p.ty = p.H / 4; p.tz = p.D / 4;
+  p.tx = (p.W + 31) / 32; p.ty = p.H / 4; p.tz = p.D / 4;
   p.cout = d->cout; p.nct = d->cout / 64;
   p.nch0 = c0 / ck; p.nch = (c0 + c1) / ck;
   p.a0 = a0; p.ac0 = c0; p.a1 = a1; p.ac1 = c1;

@@ -1,5 +1,6 @@
 // Conv3d 3x3x3 (stride 1, pad 1) implicit GEMM, DMA-staged variant for the
-// wide U-Net levels (W % 32 == 0, H % 4 == 0, D % 4 == 0, cout % 64 == 0).
+// wide U-Net levels (W >= 32, H % 4 == 0, D % 4 == 0, cout % 64 == 0; a last
+// x tile past W computes zero-padded voxels and masks them at the epilogue).
 //
 // Design (MI355X / gfx950):
 //   * The input is already activated (GroupNorm+SiLU applied by
@@ -142,6 +143,8 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
 #pragma unroll
   for (int i = 0; i < 16; ++i) { ssum[i] = 0.f; ssq[i] = 0.f; }
   const int ox = x0 + lr;
+  const bool xin = ox < p.W;          // lanes of a partial last x tile store nothing
+  const float xm = xin ? 1.f : 0.f;   // and add nothing to the statistics
   const long long HW = (long long)p.H * p.W;
   // voxel of (plane pl, line m) = vox0 + pl * HW + m * W
   const long long vox0 = (((long long)b * p.D + z0 + 2 * vg) * p.H + y0) * p.W + ox;
@@ -173,7 +176,7 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
             r = reinterpret_cast<const bf16_t*>(p.res) + rvox * p.cout + ct * 64 + f * 32 + 8 * hh;
           }
 #pragma unroll
-          for (int jj = 0; jj < 2; ++jj) rq[m][jj] = *reinterpret_cast<const u32x4*>(r + 16 * jj);
+          for (int jj = 0; jj < 2; ++jj) rq[m][jj] = xin ? *reinterpret_cast<const u32x4*>(r + 16 * jj) : u32x4{0, 0, 0, 0};
         }
       }
 #pragma unroll
@@ -196,8 +199,9 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
           }
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            ssum[8 * jj + k] += v[k];
-            ssq[8 * jj + k] += v[k] * v[k];
+            const float vv = v[k] * xm;
+            ssum[8 * jj + k] += vv;
+            ssq[8 * jj + k] += vv * vv;
           }
           const unsigned p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
           const unsigned p2 = pack_bf16x2(v[4], v[5]), p3 = pack_bf16x2(v[6], v[7]);
@@ -205,7 +209,7 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
           const auto t1 = __builtin_amdgcn_permlane32_swap(p1, p3, false, false);
           u32x4 w;
           w[0] = t0[0]; w[1] = t1[0]; w[2] = t0[1]; w[3] = t1[1];
-          *reinterpret_cast<u32x4*>(o + 16 * jj) = w;
+          if (xin) *reinterpret_cast<u32x4*>(o + 16 * jj) = w;
         }
       }
     }
@@ -214,6 +218,7 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
     for (int pl = 0; pl < 2; ++pl) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
+        if (!xin) continue;
         const int oy = y0 + m, oz = z0 + 2 * vg + pl;
         const long long vox = vox0 + pl * HW + (long long)m * p.W;
         long long rvox = vox;

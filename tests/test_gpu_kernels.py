@@ -283,7 +283,7 @@ def test_conv3d_fused_vs_torch(case, dtype_name, split):
 
 
 V4_CASES = [
-    # name, B, grid(out), c0, c1, cout, amode, gn, skip1x1, rmode  (W % 32 == 0, H, D % 4 == 0, cout % 64 == 0)
+    # name, B, grid(out), c0, c1, cout, amode, gn, skip1x1, rmode  (W >= 32, H, D % 4 == 0, cout % 64 == 0)
     ("v4_plain", 1, (8, 8, 64), 32, 0, 64, 0, False, False, -1),
     ("v4_gn_concat_skip_res", 2, (4, 8, 32), 32, 16, 64, 0, True, True, 0),
     ("v4_up_res", 1, (8, 4, 64), 32, 0, 128, 1, True, False, 1),
@@ -291,6 +291,10 @@ V4_CASES = [
     # K-split work items (fewer tiles than CU slots): partial slices + finish pass
     ("v4_ksplit_gn_skip", 1, (8, 4, 32), 96, 32, 128, 0, True, True, 0),
     ("v4_ksplit_up", 2, (8, 8, 32), 64, 0, 64, 1, True, False, 1),
+    # W not a multiple of 32: the last x tile is partial (masked stores / statistics)
+    ("v4_partial_x_gn_res", 1, (4, 8, 56), 64, 0, 64, 0, True, False, 0),
+    ("v4_partial_x_ksplit_up", 1, (8, 4, 40), 64, 0, 64, 1, True, False, 1),
+    ("v4_partial_x_concat_skip", 2, (4, 4, 48), 32, 16, 64, 0, True, True, -1),
 ]
 
 
