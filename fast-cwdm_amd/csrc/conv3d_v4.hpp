@@ -461,15 +461,22 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   // lane read base: halo voxel (z = 2 vg, line 0, x = lr) of quad plane hh
   const int hlane = hh * (C::HVP * 16) + ((2 * vg) * (C::HX * C::HY) + lr) * 16;
 
+  // a tile's first weight group: ordinary (compiler-tracked) loads, issued
+  // before the previous tile's epilogue so their latency hides under it
+  auto load_w0 = [&](u32x4 (&w)[3], int ct, int c) {
+    const unsigned char* src = wlane + ((long long)ct * p.nch + c) * 27 * 2048;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) w[dy] = *reinterpret_cast<const u32x4*>(src + dy * 3 * 2048);
+  };
   Tile cur = tile_of(0);
   u32x4 wr[3][3];
   issue_bias(cur);
   issue_halo(cur, cur.c0, 0);
+  load_w0(wr[0], cur.ct, cur.c0);
   int gch = 0;  // chunk counter of the stream (selects the halo buffer)
   for (int it = 0; it < ntile; ++it) {
     const bool more = it + 1 < ntile;
-    // the tile's halo and bias were issued under the previous tile (or above)
-    load_w(wr[0], cur.ct, cur.c0, 0);
+    // the tile's halo, bias and first weight group were issued under the previous tile (or above)
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2])::"memory");
     __builtin_amdgcn_s_barrier();
     if (it == 0) V4_STAMP(1);
@@ -532,10 +539,15 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
     for (int c = cur.c0; c + 1 < cur.c1; ++c) chunk(std::false_type{}, c);
     chunk(std::true_type{}, cur.c1 - 1);
     if (it == 0) V4_STAMP(12);
+    Tile nxt = cur;
+    if (more) {
+      nxt = tile_of(it + 1);
+      load_w0(wr[0], nxt.ct, nxt.c0);
+    }
     // (K split: out is this slice's fp32 partial, see V4Params)
     v4_epilogue<T, FAST>(p, acc, cur.b, cur.sl, cur.ct, cur.x0, cur.y0, cur.z0, cur.ks, tid, wv, smem);
     if (it == 0) V4_STAMP(13);
-    if (more) cur = tile_of(it + 1);
+    cur = nxt;
   }
   V4_STAMP(15);
 #ifdef CWDM_CONV_STAMPS
