@@ -249,6 +249,35 @@ def config5_leg(args, device, rank, world, sync, max_over_ranks):
     return res
 
 
+def wavunet_leg(args, diffusion, x_T, cond, device, world, sync, max_over_ranks):
+    """f4: the frequency-aware WavUNetModel (use_freq=True, script_util's
+    configuration at the run.sh sizes: mc 64, mult 1,2,2,4,4, 2 res blocks,
+    90.1 M parameters) in the same 128^3 sampling loop (HIP graph, bf16)."""
+    from guided_diffusion import script_util
+    n = x_T.shape[-1]
+    model = script_util.create_model(image_size=2 * n, num_channels=64, num_res_blocks=2, channel_mult="1,2,2,4,4",
+                                     attention_resolutions="", dims=3, num_groups=32, in_channels=32,
+                                     out_channels=8, bottleneck_attention=False, resblock_updown=True,
+                                     use_freq=True, compute_dtype=args.dtype)
+    seeded_weights(model, 9)
+    model.to(device)
+    K = args.wavunet
+    loop = diffusion._native_loop(model, x_T, list(range(diffusion.num_timesteps))[::-1][:K + 4], cond, True,
+                                  graph=bool(args.graph), fresh_outputs=False, need_pred=False)
+    dt = max_over_ranks(time_loop(loop, (3, K), world, sync))
+    loop.close()
+    per = dt / K
+    fl = model.plan.flops(1, n, n, n)
+    res = {"workload": f"f4: WavUNetModel (use_freq, mc 64, mult 1,2,2,4,4, 2 res blocks, "
+                       f"{sum(p.numel() for p in model.parameters()) / 1e6:.1f}M params), {n}^3 subbands, {args.dtype}, "
+                       f"{'HIP-graph' if args.graph else 'eager'} 1000-step DDPM loop, one volume per GPU",
+           "denoising_steps_per_s": round(world * K / dt, 3), "ms_per_step": round(1000 * per, 3), "steps": K,
+           "unet_tflop_per_step": round(fl / 1e12, 3), "mfma_frac": round(fl / per / 1e12 / BF16_PEAK_TFLOPS, 4)}
+    del model, loop
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,6 +294,8 @@ def main():
                          "0 = skip); reported beside, never as, the B=1 metric")
     ap.add_argument("--fp32", type=int, default=3, help="also time K steps of the fp32 parity mode (0 = skip)")
     ap.add_argument("--train", type=int, default=5, help="config-3 train_ddp side figure: timed steps (0 = skip)")
+    ap.add_argument("--wavunet", type=int, default=10, help="f4 side figure: WavUNetModel at 128^3, timed steps "
+                                                            "(0 = skip)")
     ap.add_argument("--config5", type=int, default=10, help="config-5 side figure (224^3, 2-level wavelets + FATS): "
                                                             "timed steps (0 = skip)")
     ap.add_argument("--dry-run", action="store_true",
@@ -414,6 +445,10 @@ def main():
         cpu_state = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
         cpu_cond, cpu_x = cond.cpu(), x_T.cpu()
 
+    wavunet = None
+    if args.wavunet:
+        wavunet = wavunet_leg(args, diffusion, x_T, cond, device, world, sync, max_over_ranks)
+
     config5 = None
     if args.config5:
         config5 = config5_leg(args, device, rank, world, sync, max_over_ranks)
@@ -461,6 +496,7 @@ def main():
         "fp32_parity_mode": fp32,
         "train_ddp": train,
         "config5_224": config5,
+        "wavunet_128": wavunet,
         "mfma_util_whole_step": round(step_flops * (value / world) / 1e12 / peak, 4),
         "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
