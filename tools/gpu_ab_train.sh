@@ -1,10 +1,14 @@
 #!/bin/bash
-# A/B of the training step over env settings (alternating, twice): tools/gpu_ab_train.sh "VAR=a" "VAR=b" ...
-set -o pipefail
-R=$GRAFT_REPO_ROOT; mkdir -p $R/gpurun_out/abt; cd $R
-for rep in 1 2; do
-  for cfg in "$@"; do
-    env $cfg timeout -k 10 200 python tools/train_bench.py --steps 5 > gpurun_out/abt/t.json 2>gpurun_out/abt/t.err || exit 1
-    echo "$cfg => $(python -c "import json;d=json.loads(open('gpurun_out/abt/t.json').read().strip().splitlines()[-1]);print(d['ms_per_step'])") ms"
-  done
+# train_bench under several env settings, same box.  usage: tools/gpu_ab_train.sh TAG "ENV1" "ENV2" ... ("-" = none)
+set -e -o pipefail
+T=$1; shift
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/$T; mkdir -p $O; cd $R
+i=0
+for e in "$@"; do
+  i=$((i+1))
+  [ "$e" = "-" ] && e=""
+  echo "== $e" >> $O/ab.txt
+  env $e timeout -k 10 300 python -u tools/train_bench.py --steps 6 > $O/run$i.json 2> $O/run$i.err
+  tail -1 $O/run$i.json | cut -c1-200 >> $O/ab.txt
 done
+cat $O/ab.txt
