@@ -427,3 +427,28 @@ def test_wavunet_refuses_training():
     x = torch.randn(1, 32, *grid, device=DEV)
     with pytest.raises(NotImplementedError):
         m(x, torch.tensor([3], device=DEV))
+
+
+def test_fast_ddpm_sampled10_production_loop_vs_oracle():
+    """The production inference path (infer_pod.yml: brats_*_BEST_sampled_10.pt,
+    diffusion_steps=10, sample_schedule='sampled'; gaussian_diffusion.py:45-58):
+    the native HIP-graph loop over the 10-step Fast-DDPM schedule vs the
+    oracle loop on the same tables and noise, fp32, 1e-3."""
+    from guided_diffusion import script_util
+    args = script_util.run_sh_model_args(num_channels=32, channel_mult="1,2", num_res_blocks=1, num_groups=8,
+                                         diffusion_steps=10, sample_schedule="sampled")
+    keys = script_util.model_and_diffusion_defaults().keys()
+    model, diffusion = script_util.create_model_and_diffusion(**{k: args[k] for k in keys}, compute_dtype="fp32")
+    diffusion.mode = "i2i"
+    P = ou.random_params(seed=1, **cases.C1_CFG)
+    model.load_state_dict(P)
+    model.to(DEV)
+    assert diffusion.use_hip_graph
+    cond, x_T, g = _c1_loop_inputs(seed=14)
+    noises = [torch.randn(x_T.shape, generator=g) for _ in range(10)]
+    it = iter([z.to(DEV) for z in noises])
+    out = diffusion.p_sample_loop(model, x_T.shape, noise=x_T.to(DEV), cond=cond.to(DEV), progress=False,
+                                  noise_fn=lambda x: next(it))
+    tab = od.Tables(od.beta_schedule("linear", 10, "sampled"))
+    ref = od.p_sample_loop(tab, ou.OracleUNet(P, num_groups=8, **cases.C1_CFG), x_T, cond, noises)
+    assert rel_err(out, ref) < 1e-3
