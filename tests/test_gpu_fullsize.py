@@ -177,3 +177,32 @@ def test_fullsize_bf16_error_by_layer():
     o = float((outs["bf16"].double() - outs["fp32"].double()).norm() / outs["fp32"].double().norm())
     print(f"model output rel L2 {o:.3e}")
     assert o < 5e-2
+
+
+def test_fullsize_wavunet_forward_fp32_vs_oracle():
+    """f4 at the config-2 size: the 90.1 M-parameter WavUNetModel
+    (use_freq=True, mc 64, mult 1,2,2,4,4) forward at 128^3 subbands, fp32,
+    vs the oracle restatement (oracle/wunet.py), 1e-3."""
+    from guided_diffusion import script_util
+    from oracle import wunet as ow
+    cfg = dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4))
+    P = ow.random_params(seed=23, **cfg)
+    full = dict(P)
+    for alias, owner in ow.aliases(**cfg).items():
+        for n, v in P.items():
+            if n.startswith(owner + "."):
+                full[alias + n[len(owner):]] = v
+    m = script_util.create_model(image_size=256, num_channels=64, num_res_blocks=2, channel_mult="1,2,2,4,4",
+                                 attention_resolutions="", dims=3, num_groups=32, in_channels=32, out_channels=8,
+                                 bottleneck_attention=False, resblock_updown=True, use_freq=True, compute_dtype="fp32")
+    m.load_state_dict(full)
+    m.to(DEV)
+    g = torch.Generator().manual_seed(24)
+    x = torch.randn(1, 32, 128, 128, 128, generator=g)
+    t = torch.tensor([512])
+    with torch.no_grad():
+        out = m(x.to(DEV), t.to(DEV)).cpu()
+    torch.set_num_threads(16)
+    with torch.no_grad():
+        ref = ow.wunet_forward(P, x, t, num_groups=32, **cfg)
+    assert rel_err(out, ref) < 1e-3
