@@ -224,6 +224,43 @@ CASES = [
 @pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 def test_conv3d_fused_vs_torch(case, dtype_name, split):
+    _run_conv_case(case, dtype_name, split)
+
+
+def _random_conv_cases(n, seed):
+    """Seeded shapes drawn inside the ABI's limits (channels multiples of 16; even grids for resampling):
+    odd extents, partial bricks and partial x tiles, every input/residual mode, GN, concat, 1x1 skip."""
+    import random
+    r = random.Random(seed)
+    out = []
+    for i in range(n):
+        amode = r.choice([0, 0, 1, 2])
+        rmode = r.choice([-1, 0, 1, 2])
+        even = amode == 1 or rmode == 1
+        ext = [r.randint(1, 10) * (2 if even else 1) for _ in range(2)] + [r.choice([r.randint(2, 24), r.randint(32, 72)])]
+        if even:
+            ext[2] += ext[2] % 2
+        cout = r.choice([8, 16, 24, 32, 64, 96, 128, 192])
+        if r.random() < 0.4:  # shapes the DMA kernel takes (W >= 32, D, H % 4 == 0, cout % 64 == 0)
+            ext[0], ext[1], ext[2] = 4 * r.randint(1, 3), 4 * r.randint(1, 3), 2 * r.randint(16, 36)
+            cout = r.choice([64, 128, 192])
+        c0 = 16 * r.randint(1, 6)
+        c1 = r.choice([0, 0, 16, 32])
+        out.append((f"rand{i}", r.randint(1, 2), tuple(ext), c0, c1, cout, amode, r.random() < 0.7,
+                    amode == 0 and r.random() < 0.4, rmode))   # the 1x1 skip reads the output grid
+    return out
+
+
+RANDOM_CASES = _random_conv_cases(24, 20261016)
+
+
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", RANDOM_CASES, ids=[c[0] for c in RANDOM_CASES])
+def test_conv3d_random_shapes_vs_torch(case, dtype_name):
+    _run_conv_case(case, dtype_name, True)
+
+
+def _run_conv_case(case, dtype_name, split):
     from cwdm_hip import _lib
     name, B, grid, c0, c1, cout, amode, use_gn, skip, rmode = case
     dtype = _lib.CWDM_F32 if dtype_name == "fp32" else _lib.CWDM_BF16

@@ -49,6 +49,36 @@ WG_CASES = [
 @pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
 @pytest.mark.parametrize("case", WG_CASES, ids=[c[0] for c in WG_CASES])
 def test_conv3d_wgrad_vs_torch(case, dtype_name):
+    _run_wgrad_case(case, dtype_name)
+
+
+def _random_wgrad_cases(n, seed):
+    """Seeded wgrad shapes: odd extents, concat inputs, upsampled inputs, 1x1 and 3x3, padded dy rows."""
+    import random
+    r = random.Random(seed)
+    out = []
+    for i in range(n):
+        umode = r.choice([0, 0, 1])
+        k = 3 if umode else r.choice([3, 3, 1])     # upsampled / GN prologues exist for 3x3 only
+        ext = tuple(r.randint(1, 9) * (2 if umode else 1) for _ in range(2)) + (r.randint(2, 40) * (2 if umode else 1),)
+        cout = r.choice([8, 16, 32, 64, 96, 128])
+        dy_cs = (cout + 15) // 16 * 16 + r.choice([0, 16])
+        c0 = 16 * r.randint(1, 6)
+        c1 = r.choice([0, 32]) + (16 if c0 % 32 else 0)   # cin a multiple of 32
+        out.append((f"rand{i}", r.randint(1, 2), ext, c0, c1, cout, umode, k == 3 and r.random() < 0.7, k, dy_cs))
+    return out
+
+
+RANDOM_WG_CASES = _random_wgrad_cases(12, 20261016)
+
+
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", RANDOM_WG_CASES, ids=[c[0] for c in RANDOM_WG_CASES])
+def test_conv3d_wgrad_random_shapes_vs_torch(case, dtype_name):
+    _run_wgrad_case(case, dtype_name)
+
+
+def _run_wgrad_case(case, dtype_name):
     from cwdm_hip import _lib
     from cwdm_hip._lib import check, lib
     name, B, grid, c0, c1, cout, umode, use_gn, k, dy_cs = case
