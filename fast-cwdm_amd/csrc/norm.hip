@@ -8,50 +8,69 @@
 namespace cwdm {
 namespace {
 
-__global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restrict__ s0, long long p0, int c0,
-                                                         const float* __restrict__ s1, long long p1, int c1,
-                                                         const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, int groups,
-                                                         long long voxels, float eps, float* __restrict__ out,
-                                                         float* __restrict__ mean_rstd) {
+// One workgroup per (group, batch).  The group's (part, channel) items are
+// flattened so consecutive threads read consecutive channels of one part row
+// and every thread has up to 4 independent loads in flight: a small tensor
+// finishes in one load latency, a 128^3 one (4096 parts) in a few.
+constexpr int FIN_THREADS = 512;
+
+__device__ __forceinline__ void fin_segment(const float2* __restrict__ base, long long parts, int cs, int lo, int w,
+                                            double& s, double& q) {
+  // items i = pi * w + ci, channel lo + ci of part pi at base[pi * cs + lo + ci]
+  // (32-bit item indices: parts * w is far below 2^32 for any grid the plan admits)
+  const unsigned n = (unsigned)(parts * w), uw = (unsigned)w;
+  unsigned i = threadIdx.x;
+  for (; i + 3 * FIN_THREADS < n; i += 4 * FIN_THREADS) {
+    float2 u[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned j = i + k * FIN_THREADS;
+      u[k] = base[(long long)(j / uw) * cs + lo + (int)(j % uw)];
+    }
+    s += ((double)u[0].x + (double)u[1].x) + ((double)u[2].x + (double)u[3].x);
+    q += ((double)u[0].y + (double)u[1].y) + ((double)u[2].y + (double)u[3].y);
+  }
+  for (; i < n; i += FIN_THREADS) {
+    const float2 u = base[(long long)(i / uw) * cs + lo + (int)(i % uw)];
+    s += (double)u.x;
+    q += (double)u.y;
+  }
+}
+
+__global__ void __launch_bounds__(FIN_THREADS) gn_finalize_kernel(const float* __restrict__ s0, long long p0, int c0,
+                                                                 const float* __restrict__ s1, long long p1, int c1,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta, int groups,
+                                                                 long long voxels, float eps, float* __restrict__ out,
+                                                                 float* __restrict__ mean_rstd) {
   const int g = blockIdx.x, b = blockIdx.y;
   const int C = c0 + c1, cpg = C / groups;
-  __shared__ double rs[256], rq[256];
+  const int glo = g * cpg, ghi = glo + cpg;
   double s = 0.0, q = 0.0;
-  // items: (channel-in-group, part)
-  for (int ci = 0; ci < cpg; ++ci) {
-    const int c = g * cpg + ci;
-    const float* src;
-    long long parts;
-    int cc, cs;
-    if (c < c0) { src = s0; parts = p0; cc = c; cs = c0; }
-    else { src = s1; parts = p1; cc = c - c0; cs = c1; }
-    // (sum, sum^2) pairs of part pi at base[pi * cs]; four parts per thread in
-    // flight per iteration (the loads are independent, the adds are fp64)
-    const float2* base = reinterpret_cast<const float2*>(src) + (long long)b * parts * cs + cc;
-    long long pi = threadIdx.x;
-    for (; pi + 768 < parts; pi += 1024) {
-      const float2 u0 = base[pi * cs], u1 = base[(pi + 256) * cs], u2 = base[(pi + 512) * cs],
-                   u3 = base[(pi + 768) * cs];
-      s += ((double)u0.x + (double)u1.x) + ((double)u2.x + (double)u3.x);
-      q += ((double)u0.y + (double)u1.y) + ((double)u2.y + (double)u3.y);
-    }
-    for (; pi < parts; pi += 256) {
-      const float2 u = base[pi * cs];
-      s += (double)u.x;
-      q += (double)u.y;
-    }
+  if (glo < c0)  // the group's channels in the first source
+    fin_segment(reinterpret_cast<const float2*>(s0) + (long long)b * p0 * c0, p0, c0, glo, min(ghi, c0) - glo, s, q);
+  if (ghi > c0)  // ... and in the second (a concatenated input)
+    fin_segment(reinterpret_cast<const float2*>(s1) + (long long)b * p1 * c1, p1, c1, max(glo, c0) - c0,
+                ghi - max(glo, c0), s, q);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    q += __shfl_xor(q, o, 64);
   }
-  rs[threadIdx.x] = s;
-  rq[threadIdx.x] = q;
+  __shared__ double rs[FIN_THREADS / 64], rq[FIN_THREADS / 64];
+  if ((threadIdx.x & 63) == 0) {
+    rs[threadIdx.x >> 6] = s;
+    rq[threadIdx.x >> 6] = q;
+  }
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      rs[threadIdx.x] += rs[threadIdx.x + o];
-      rq[threadIdx.x] += rq[threadIdx.x + o];
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 1; k < FIN_THREADS / 64; ++k) {
+      rs[0] += rs[k];
+      rq[0] += rq[k];
     }
-    __syncthreads();
   }
+  __syncthreads();
   const double n = (double)cpg * (double)voxels;
   const double mean = rs[0] / n;
   double var = rq[0] / n - mean * mean;
@@ -62,7 +81,7 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restric
     mean_rstd[((long long)b * groups + g) * 2 + 0] = meanf;
     mean_rstd[((long long)b * groups + g) * 2 + 1] = rstd;
   }
-  for (int ci = threadIdx.x; ci < cpg; ci += 256) {
+  for (int ci = threadIdx.x; ci < cpg; ci += FIN_THREADS) {
     const int c = g * cpg + ci;
     const float sc = gamma[c] * rstd;
     out[((long long)b * C + c) * 2 + 0] = sc;
@@ -83,7 +102,9 @@ extern "C" int cwdm_gn_finalize(const float* s0, int64_t p0, int c0, const float
   CWDM_REQUIRE(groups > 0 && (c0 + c1) % groups == 0, CWDM_E_SHAPE,
                "cwdm_gn_finalize: channels must be divisible by num_groups");
   CWDM_REQUIRE(B > 0 && B < 65536 && voxels > 0, CWDM_E_SHAPE, "cwdm_gn_finalize: bad batch/voxels");
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, (unsigned)B), dim3(256), 0, (hipStream_t)stream, s0,
+  CWDM_REQUIRE(p0 > 0 && p0 * c0 < (1LL << 31) && (c1 == 0 || (p1 > 0 && p1 * c1 < (1LL << 31))), CWDM_E_SHAPE,
+               "cwdm_gn_finalize: bad part count");
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, (unsigned)B), dim3(FIN_THREADS), 0, (hipStream_t)stream, s0,
                      (long long)p0, c0, s1, (long long)p1, c1, gamma, beta, groups, (long long)voxels, eps, out,
                      mean_rstd);
   CWDM_LAUNCHED();
