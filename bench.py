@@ -249,6 +249,56 @@ def config5_leg(args, device, rank, world, sync, max_over_ranks):
     return res
 
 
+def train5_leg(args, device, rank, world, sync, max_over_ranks):
+    """Config 5 training: TrainLoop.run_step on the 2-level representation
+    (224^3 phantoms x 4 modalities -> cwdm_prepare_batch2 -> the config-5
+    3-level U-Net, FATS per-channel q_sample rows -> segmented native backward
+    (+ RCCL bucketed all-reduce when N > 1) -> fused AdamW), batch 1 per GPU."""
+    import numpy as np
+    from cwdm_hip import ops
+    from guided_diffusion import fats, script_util, train_util
+    os.environ.setdefault("CWDM_LOGDIR", os.path.join(ROOT, "gpurun_out", "bench_train5"))
+    n, g = 224, 56
+    model = script_util.create_model(image_size=n, num_channels=64, num_res_blocks=2, channel_mult="1,2,2",
+                                     attention_resolutions="", dims=3, num_groups=32, in_channels=256,
+                                     out_channels=64, bottleneck_attention=False, resample_2d=False,
+                                     resblock_updown=True, compute_dtype=args.dtype)
+    seeded_weights(model, 5)
+    model.to(device)
+    batch = {k: phantom_gpu(n, 700 + 100 * rank + j, device) for j, k in enumerate(("t1n", "t1c", "t2w", "t2f"))}
+    e = sum(fats.subband_energy(ops.wavelet2_analysis(batch[k]).permute(0, 4, 1, 2, 3), levels=2)
+            for k in ("t1c", "t2w"))
+    diffusion = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
+                                                      band_log_snr_shift=fats.band_log_snr_shifts(e),
+                                                      wavelet_levels=2)
+    np.random.seed(5)
+    loop = train_util.TrainLoop(model=model, diffusion=diffusion, data=[batch], batch_size=1, in_channels=256,
+                                image_size=n, microbatch=-1, lr=1e-5, ema_rate="0.9999", log_interval=10 ** 9,
+                                contr="t1n", save_interval=10 ** 9, resume_checkpoint="", resume_step=0,
+                                mode="i2i", diffusion_steps=1000)
+    for _ in range(2):
+        loop.run_step(batch, {})
+    sync()
+    K = args.train5
+    t0 = time.perf_counter()
+    for _ in range(K):
+        loss, _, _ = loop.run_step(batch, {})
+    sync()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    fl = model.plan.flops(1, g, g, g) + model.plan.backward_flops(1, g, g, g)
+    per = dt / K
+    res = {"workload": "config5 training: TrainLoop.run_step, 224^3 phantoms x 4 modalities -> 2-level block "
+                       "wavelets (56^3 x 64 ch per modality), FATS per-channel q_sample, 3-level U-Net (256->64 ch), "
+                       f"{args.dtype}, batch 1 per GPU, gradient all-reduce "
+                       f"({'RCCL' if world > 1 and dist.get_backend() == 'nccl' else dist.get_backend() if world > 1 else 'none'})",
+           "volumes_per_s": round(world * K / dt, 4), "ms_per_step": round(1000 * per, 2), "steps": K,
+           "conv_tflop_per_step": round(fl / 1e12, 3), "mfma_frac": round(fl / per / 1e12 / BF16_PEAK_TFLOPS, 4),
+           "loss": round(float(loss), 6), "scaling": "weak"}
+    del model, loop
+    torch.cuda.empty_cache()
+    return res
+
+
 def wavunet_leg(args, diffusion, x_T, cond, device, world, sync, max_over_ranks):
     """f4: the frequency-aware WavUNetModel (use_freq=True, script_util's
     configuration at the run.sh sizes: mc 64, mult 1,2,2,4,4, 2 res blocks,
@@ -298,6 +348,8 @@ def main():
                                                             "(0 = skip)")
     ap.add_argument("--config5", type=int, default=10, help="config-5 side figure (224^3, 2-level wavelets + FATS): "
                                                             "timed steps (0 = skip)")
+    ap.add_argument("--train5", type=int, default=3, help="config-5 training side figure (224^3, 2-level "
+                                                          "wavelets + FATS): timed steps (0 = skip)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the rank launch / barrier / max-over-ranks plumbing only")
     args = ap.parse_args()
@@ -471,6 +523,10 @@ def main():
     if args.config5:
         config5 = config5_leg(args, device, rank, world, sync, max_over_ranks)
 
+    train5 = None
+    if args.train5:
+        train5 = train5_leg(args, device, rank, world, sync, max_over_ranks)
+
     train = None
     if args.train:
         train = train_leg(model, diffusion, n, rank, world, device, args.train, 2, sync, max_over_ranks)
@@ -515,6 +571,7 @@ def main():
         "fp32_parity_mode": fp32,
         "train_ddp": train,
         "config5_224": config5,
+        "train_config5_224": train5,
         "wavunet_128": wavunet,
         "mfma_util_whole_step": round(step_flops * (value / world) / 1e12 / peak, 4),
         "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",

@@ -514,6 +514,41 @@ __device__ __forceinline__ void write_partial(const ConvParams& p, const float* 
   }
 }
 
+// sum the S fp32 slices of one (spatial tile, channel tile) into the epilogue
+// staging E[row][LD] in slice order 0..S-1 (deterministic whoever finishes it)
+template <int BX, int BY, int BZ, int NF, int ROWS>
+__device__ __forceinline__ void sum_slices(const ConvParams& p, float* E, int S, int b, int ct, int x0, int y0, int z0,
+                                           int tid) {
+  constexpr int NT = 32 * NF, LD = NT + 4, CG = NT / 8;
+  const int cg = tid % CG;
+  const int cbase = ct * NT + cg * 8;
+  const int nvalid = min(8, p.cout - cbase);
+  const long long slice = (long long)p.B * p.D * p.H * p.W * p.cout;
+  for (int u = tid; u < ROWS * CG; u += 256) {
+    const int row = u / CG;
+    const int rx = row % BX, ry = (row / BX) % BY, rz = row / (BX * BY);
+    const int ox = x0 + rx, oy = y0 + ry, oz = z0 + rz;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    if (!(ox >= p.W || oy >= p.H || oz >= p.D || nvalid <= 0)) {
+      const long long vox = (((long long)b * p.D + oz) * p.H + oy) * p.W + ox;
+      for (int k = 0; k < S; ++k) {
+        const float* src = p.partial + k * slice + vox * p.cout + cbase;
+        if (nvalid == 8) {
+          const float4 a = *reinterpret_cast<const float4*>(src), c = *reinterpret_cast<const float4*>(src + 4);
+          v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+          v[4] += c.x; v[5] += c.y; v[6] += c.z; v[7] += c.w;
+        } else {
+          for (int e = 0; e < nvalid; ++e) v[e] += src[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) E[row * LD + cg * 8 + e] = v[e];
+  }
+}
+
 template <typename T, int BX, int BY, int BZ>
 __device__ __forceinline__ void tile_origin(const ConvParams& p, int st, int* b, int* x0, int* y0, int* z0) {
   const int ix = st % p.tx, iy = (st / p.tx) % p.ty, iz = (st / (p.tx * p.ty)) % p.tz;
@@ -676,7 +711,6 @@ __global__ void __launch_bounds__(256) conv3d_reduce_kernel(ConvParams p, int S)
   tile_origin<T, BX, BY, BZ>(p, st, &b, &x0, &y0, &z0);
   const int cg = tid % CG;
   const int cbase = ct * NT + cg * 8;
-  const int nvalid = min(8, p.cout - cbase);
   if (S == 1 && ct * NT + NT <= p.cout) {  // workgroup-uniform: the whole channel tile is valid
     // pre-summed slice: every row's loads in flight at once (fully unrolled)
     constexpr int IT = ROWS * CG / 256;
@@ -702,30 +736,7 @@ __global__ void __launch_bounds__(256) conv3d_reduce_kernel(ConvParams p, int S)
     epilogue_rows<T, BX, BY, BZ, NF, ROWS>(p, E, b, st, ct, x0, y0, z0, tid);
     return;
   }
-  for (int u = tid; u < ROWS * CG; u += 256) {
-    const int row = u / CG;
-    const int rx = row % BX, ry = (row / BX) % BY, rz = row / (BX * BY);
-    const int ox = x0 + rx, oy = y0 + ry, oz = z0 + rz;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = 0.f;
-    if (!(ox >= p.W || oy >= p.H || oz >= p.D || nvalid <= 0)) {
-      const long long vox = (((long long)b * p.D + oz) * p.H + oy) * p.W + ox;
-      const long long slice = (long long)p.B * p.D * p.H * p.W * p.cout;
-      for (int k = 0; k < S; ++k) {
-        const float* src = p.partial + k * slice + vox * p.cout + cbase;
-        if (nvalid == 8) {
-          const float4 a = *reinterpret_cast<const float4*>(src), c = *reinterpret_cast<const float4*>(src + 4);
-          v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
-          v[4] += c.x; v[5] += c.y; v[6] += c.z; v[7] += c.w;
-        } else {
-          for (int e = 0; e < nvalid; ++e) v[e] += src[e];
-        }
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) E[row * LD + cg * 8 + e] = v[e];
-  }
+  sum_slices<BX, BY, BZ, NF, ROWS>(p, E, S, b, ct, x0, y0, z0, tid);
   __syncthreads();
   epilogue_rows<T, BX, BY, BZ, NF, ROWS>(p, E, b, st, ct, x0, y0, z0, tid);
 }

@@ -15,7 +15,11 @@
 namespace cwdm {
 namespace {
 
-// img: 4x4x4 block [z][y][x] -> c: the 64 coefficients
+// img: 4x4x4 block [z][y][x] -> c: the 64 coefficients.  SCALE = false: the
+// plain orthonormal 2-level transform (no LLL / 3 at either level), the noise
+// image's transform in training_losses (the reference DWTs the noise without
+// the /3, gaussian_diffusion.py:1143-1145)
+template <bool SCALE = true>
 __device__ __forceinline__ void wav2_fwd(const float img[64], float c[64]) {
   float l1[8];
 #pragma unroll
@@ -25,13 +29,13 @@ __device__ __forceinline__ void wav2_fwd(const float img[64], float c[64]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = img[(2 * pz + (i >> 2)) * 16 + (2 * py + ((i >> 1) & 1)) * 4 + 2 * px + (i & 1)];
     haar_fwd8(v, o);
-    l1[ph] = __fdiv_rn(o[0], 3.0f);
+    l1[ph] = SCALE ? __fdiv_rn(o[0], 3.0f) : o[0];
 #pragma unroll
     for (int k = 1; k < 8; ++k) c[8 + (k - 1) * 8 + ph] = o[k];
   }
   float o2[8];
   haar_fwd8(l1, o2);
-  c[0] = __fdiv_rn(o2[0], 3.0f);
+  c[0] = SCALE ? __fdiv_rn(o2[0], 3.0f) : o2[0];
 #pragma unroll
   for (int k = 1; k < 8; ++k) c[k] = o2[k];
 }
@@ -96,6 +100,59 @@ __global__ void __launch_bounds__(256) wav2_analysis_kernel(const float* __restr
   TO* o = out + b * obs + v * ovs + oc0;
 #pragma unroll
   for (int j = 0; j < 64; ++j) stw<TO>(o, j, c[j]);
+}
+
+__device__ __forceinline__ void load_block4(const float* __restrict__ x, int64_t b, int64_t d, int64_t h, int64_t w,
+                                            int64_t v, float img[64]) {
+  const int64_t xx = v % w, yy = (v / w) % h, zz = v / (w * h);
+  const int64_t W4 = 4 * w, H4 = 4 * h;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float4 q = *reinterpret_cast<const float4*>(
+        x + ((b * 4 * d + 4 * zz + (r >> 2)) * H4 + 4 * yy + (r & 3)) * W4 + 4 * xx);
+    img[r * 4 + 0] = q.x; img[r * 4 + 1] = q.y; img[r * 4 + 2] = q.z; img[r * 4 + 3] = q.w;
+  }
+}
+
+// training_losses front end for the 2-level representation (config 5; the
+// levels-1 cwdm_prepare_batch restated, oracle.diffusion.training_losses with
+// levels = 2): x0 = analysis2(target), the three conditions' analysis2, the
+// noise image's unscaled transform, q_sample with per-channel rows when
+// per_band.  One coarse voxel (one 4x4x4 block of each of the 5 volumes) per
+// thread; NCDHW fp32 outputs x_in (B, 256, d, h, w), x0 (B, 64, d, h, w).
+struct Prep2Args {
+  const float* img[5];  // target, c1, c2, c3, eps
+  float* x_in; float* x0;
+  const float* coef; const int64_t* t; int64_t T;
+  int64_t B, d, h, w; int per_band;
+};
+
+__global__ void __launch_bounds__(256) prepare_batch2_kernel(Prep2Args a) {
+  const int64_t nv = a.d * a.h * a.w;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.B * nv) return;
+  const int64_t b = i / nv, v = i - b * nv;
+  int64_t t = a.t[b];
+  t = t < 0 ? 0 : (t >= a.T ? a.T - 1 : t);
+  const float* cq = a.coef + t * (a.per_band ? 128 : 2);
+  const int bs = a.per_band ? 2 : 0;
+  float img[64], x0[64], c[64];
+  load_block4(a.img[0], b, a.d, a.h, a.w, v, img);
+  wav2_fwd<true>(img, x0);
+  float* o0 = a.x0 + b * 64 * nv + v;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) o0[j * nv] = x0[j];
+  load_block4(a.img[4], b, a.d, a.h, a.w, v, img);
+  wav2_fwd<false>(img, c);
+  float* xin = a.x_in + b * 256 * nv + v;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) xin[j * nv] = ad(mr(cq[j * bs], x0[j]), mr(cq[j * bs + 1], c[j]));
+  for (int s = 1; s < 4; ++s) {
+    load_block4(a.img[s], b, a.d, a.h, a.w, v, img);
+    wav2_fwd<true>(img, c);
+#pragma unroll
+    for (int j = 0; j < 64; ++j) xin[(64 * s + j) * nv] = c[j];
+  }
 }
 
 // coefficients (fp32, coef[b * cbs + v * cvs + cc0 + j]) -> image (B, 1, 4d, 4h, 4w)
@@ -267,6 +324,24 @@ extern "C" int cwdm_wavelet2_synthesis(const float* coef, int64_t B, int64_t d, 
   const dim3 grid((unsigned)ceil_div(B * d * h * w, 256));
   hipLaunchKernelGGL(wav2_synthesis_kernel, grid, dim3(256), 0, (hipStream_t)stream, coef, B, d, h, w, c_bs, c_vs,
                      c_c0, out);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+extern "C" int cwdm_prepare_batch2(const float* target, const float* c1, const float* c2, const float* c3,
+                                   const float* eps_img, int64_t B, int64_t D, int64_t H, int64_t W,
+                                   const float* coef, int per_band, const int64_t* t, int64_t T, float* x_in,
+                                   float* x0, cwdm_stream_t stream) {
+  CWDM_REQUIRE(target && c1 && c2 && c3 && eps_img && coef && t && x_in && x0, CWDM_E_INVALID,
+               "cwdm_prepare_batch2: null pointer");
+  CWDM_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0 && T > 0, CWDM_E_SHAPE, "cwdm_prepare_batch2: empty shape");
+  CWDM_REQUIRE(D % 4 == 0 && H % 4 == 0 && W % 4 == 0, CWDM_E_SHAPE,
+               "cwdm_prepare_batch2: D, H, W must be multiples of 4");
+  Prep2Args a{{target, c1, c2, c3, eps_img}, x_in, x0, coef, t, T, B, D / 4, H / 4, W / 4, per_band ? 1 : 0};
+  for (int s = 0; s < 5; ++s)
+    CWDM_REQUIRE(((uintptr_t)a.img[s] & 15) == 0, CWDM_E_INVALID, "cwdm_prepare_batch2: volumes must be 16-byte aligned");
+  const int64_t n = B * a.d * a.h * a.w;
+  hipLaunchKernelGGL(prepare_batch2_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, a);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }

@@ -115,6 +115,8 @@ _PROTOS = {
                                                i64, i64, vp, vp]),
     "cwdm_prepare_batch": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, ctypes.c_int, vp, i64, vp, vp,
                                           vp]),
+    "cwdm_prepare_batch2": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, ctypes.c_int, vp, i64, vp, vp,
+                                           vp]),
     "cwdm_sampler_step": (ctypes.c_int, [ctypes.POINTER(SamplerArgs), vp]),
     "cwdm_quantile_workspace_bytes": (i64, []),
     "cwdm_quantiles": (ctypes.c_int, [vp, ctypes.c_int, i64, ctypes.POINTER(i64), ctypes.c_int,

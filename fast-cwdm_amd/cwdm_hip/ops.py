@@ -103,6 +103,27 @@ def prepare_batch(target, c1, c2, c3, eps_img, coef, t, T, per_band=False):
     return x_in, x0
 
 
+def prepare_batch2(target, c1, c2, c3, eps_img, coef, t, T, per_band=False):
+    """The 2-level (config 5) training front end in one kernel
+    (cwdm_prepare_batch2): returns (x_in (B, 256, d, h, w) = [q_sample |
+    3 condition analyses], x0 (B, 64, d, h, w)), d = D / 4.  per_band: coef
+    is [T][64][2] (per-channel FATS rows)."""
+    vols = [v.contiguous().float() for v in (target, c1, c2, c3, eps_img)]
+    _need_cuda(*vols, coef, t)
+    for v in vols:
+        if v.dim() != 5 or v.shape[1] != 1 or v.shape != vols[0].shape:
+            raise AssertionError("prepare_batch2: five (B, 1, D, H, W) volumes of one shape")
+    B, _, D, H, W = vols[0].shape
+    if D % 4 or H % 4 or W % 4:
+        raise AssertionError(f"prepare_batch2: edges must be multiples of 4 (got {D}x{H}x{W})")
+    x_in = torch.empty((B, 256, D // 4, H // 4, W // 4), device=vols[0].device, dtype=torch.float32)
+    x0 = torch.empty((B, 64, D // 4, H // 4, W // 4), device=vols[0].device, dtype=torch.float32)
+    t = t.to(dtype=torch.int64).contiguous()
+    check(lib().cwdm_prepare_batch2(*[_p(v) for v in vols], B, D, H, W, _p(coef), 1 if per_band else 0, _p(t), T,
+                                    _p(x_in), _p(x0), _stream()), "training_losses")
+    return x_in, x0
+
+
 def copy3(src, src_strides, dst, dst_strides, B, C, V):
     _need_cuda(src, dst)
     check(lib().cwdm_copy3(_p(src), DT[src.dtype], strides(*src_strides), _p(dst), DT[dst.dtype],

@@ -536,13 +536,13 @@ class GaussianDiffusion:
     def training_losses(self, model, x_start, t, classifier=None, model_kwargs=None, noise=None, labels=None,
                         mode="default", contr="t1n"):
         """i2i training loss (reference :1084-1166): returns
-        (terms{"mse_wav": [8]}, model_output, model_output_idwt)."""
+        (terms{"mse_wav": [8]}, model_output, model_output_idwt); with
+        wavelet_levels = 2 the same on the 64-channel representation
+        (terms{"mse_wav": [64]}, config 5)."""
         if model_kwargs is None:
             model_kwargs = {}
         if mode != "i2i":
             raise NotImplementedError("training_losses: only mode='i2i' is on the fast-cwdm path")
-        if self.wavelet_levels != 1:
-            raise NotImplementedError("training_losses: the two-level representation (config 5) is sampling-only")
         order = {"t1n": ("t1n", "t1c", "t2w", "t2f"), "t1c": ("t1c", "t1n", "t2w", "t2f"),
                  "t2w": ("t2w", "t1n", "t1c", "t2f"), "t2f": ("t2f", "t1n", "t1c", "t2w")}
         if contr not in order:
@@ -556,6 +556,17 @@ class GaussianDiffusion:
         dev = target.device
         self._check_t(t)
         noise_img = th.randn_like(target) if noise is None else noise
+        if self.wavelet_levels == 2:
+            # config 5 (no reference code; the levels-1 loss below restated on
+            # the 64-channel block representation, oracle.diffusion.training_losses)
+            x_in, x_start_dwt = ops.prepare_batch2(target, x_start[keys[1]], x_start[keys[2]], x_start[keys[3]],
+                                                   noise_img, self.q_coef_table(dev), t, self.num_timesteps,
+                                                   per_band=self.per_band)
+            model_output = model(x_in, self._scale_timesteps(t), **model_kwargs)
+            mo = model_output.detach().float().permute(0, 2, 3, 4, 1).contiguous()
+            model_output_idwt = ops.wavelet2_synthesis(mo)
+            terms = {"mse_wav": th.mean(mean_flat((x_start_dwt - model_output) ** 2), dim=0)}
+            return terms, model_output, model_output_idwt
         # one kernel: 4 DWTs (LLL/3), the noise DWT (no /3, :1143-1145),
         # q_sample, straight into the 32-channel model input (cwdm_prepare_batch)
         x_in, x_start_dwt = ops.prepare_batch(target, x_start[keys[1]], x_start[keys[2]], x_start[keys[3]],

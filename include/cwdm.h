@@ -125,6 +125,20 @@ int cwdm_prepare_batch(const float* target, const float* c1, const float* c2, co
                        const float* coef, int per_band, const int64_t* t, int64_t T, float* x_in, float* x0,
                        cwdm_stream_t stream);
 
+/* cwdm_prepare_batch2: the same front end for the 2-level block wavelet
+ * representation (BASELINE config 5; no reference code -- the levels-1 front
+ * end above with cwdm_wavelet2_analysis's transform, oracle/wavelet2.py):
+ * x0 (B, 64, d, h, w) = analysis2(target), x_in (B, 256, d, h, w) =
+ * [q_sample(x0, eps) | analysis2(c1) | analysis2(c2) | analysis2(c3)] with eps
+ * the noise image's 2-level transform WITHOUT the LLL / 3 (as the reference's
+ * noise DWT, :1143-1145); d = D / 4 etc.  coef [T][2] or, per_band, [T][64][2]
+ * (one row per channel, guided_diffusion/fats.py).  Volumes fp32 contiguous,
+ * 16-byte aligned. */
+int cwdm_prepare_batch2(const float* target, const float* c1, const float* c2, const float* c3,
+                        const float* eps_img, int64_t B, int64_t D, int64_t H, int64_t W,
+                        const float* coef, int per_band, const int64_t* t, int64_t T, float* x_in, float* x0,
+                        cwdm_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Fused sampler step: replaces the tail of GaussianDiffusion.p_sample after
  * the model call (and EPSILON's _predict_xstart_from_eps, :390-397) -- process_xstart (IDWT(LLL*3) -> clamp(0,1) -> DWT ->

@@ -170,19 +170,25 @@ def p_sample_loop(tab, model, x_T, cond, step_noises, time=None, clip_denoised=T
     return img
 
 
-def training_losses(tab, model, x_start, t, noise_img, contr="t1n"):
+def training_losses(tab, model, x_start, t, noise_img, contr="t1n", levels=1):
     """i2i training_losses (gaussian_diffusion.py:1084-1166); returns
-    (terms, model_output, model_output_idwt)."""
+    (terms, model_output, model_output_idwt).  levels=2: the same on the
+    config-5 2-level block representation (oracle.wavelet2; spec only)."""
+    from . import wavelet2
     order = {"t1n": ("t1n", "t1c", "t2w", "t2f"), "t1c": ("t1c", "t1n", "t2w", "t2f"),
              "t2w": ("t2w", "t1n", "t1c", "t2f"), "t2f": ("t2f", "t1n", "t1c", "t2w")}[contr]
     target = x_start[order[0]]
-    cond = torch.cat([haar.dwt_cat(x_start[k]) for k in order[1:]], dim=1)
-    x0 = haar.dwt_cat(target)
-    eps = torch.cat(list(haar.dwt3d(noise_img)), dim=1)
+    fwd = haar.dwt_cat if levels == 1 else wavelet2.analysis2
+    cond = torch.cat([fwd(x_start[k]) for k in order[1:]], dim=1)
+    x0 = fwd(target)
+    if levels == 1:
+        eps = torch.cat(list(haar.dwt3d(noise_img)), dim=1)
+    else:
+        eps = wavelet2.analysis2(noise_img, scale=False)
     x_t = q_sample(tab, x0, t, eps)
     model_t = torch.tensor(tab.timestep_map, dtype=t.dtype)[t]
     out = model(torch.cat([x_t, cond], dim=1), model_t)
-    out_idwt = haar.idwt_split(out)
+    out_idwt = haar.idwt_split(out) if levels == 1 else wavelet2.synthesis2(out)
     mse = ((x0 - out) ** 2).mean(dim=list(range(2, out.dim()))).mean(dim=0)
     return {"mse_wav": mse}, out, out_idwt
 

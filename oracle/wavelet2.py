@@ -42,12 +42,16 @@ def _d2s(x):   # inverse of _s2d
     return y.reshape(B, C8 // 8, 2 * d, 2 * h, 2 * w)
 
 
-def analysis2(x):
-    """(B, 1, 4d, 4h, 4w) image -> (B, 64, d, h, w) coefficients."""
+def analysis2(x, scale=True):
+    """(B, 1, 4d, 4h, 4w) image -> (B, 64, d, h, w) coefficients.  scale=False:
+    no LLL / 3 at either level -- the noise image's transform in
+    training_losses (the reference DWTs the noise without the /3,
+    gaussian_diffusion.py:1143-1145)."""
     assert x.dim() == 5 and x.shape[1] == 1
+    div = 3.0 if scale else 1.0
     b1 = haar.dwt3d(x)
-    b2 = haar.dwt3d(b1[0] / 3.0)
-    low = [b2[0] / 3.0] + list(b2[1:])
+    b2 = haar.dwt3d(b1[0] / div)
+    low = [b2[0] / div] + list(b2[1:])
     return torch.cat(low + [_s2d(b) for b in b1[1:]], dim=1)
 
 

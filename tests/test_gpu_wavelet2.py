@@ -153,3 +153,63 @@ def test_config5_graph_loop_bf16_runs_at_224():
         outs.append(diffusion.p_sample_loop(model, x_T.shape, noise=x_T, cond=cond, progress=False))
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("per_band", [False, True])
+def test_prepare_batch2_bitexact_vs_oracle(per_band):
+    """cwdm_prepare_batch2 (config-5 training front end): x0 = analysis2(target),
+    the three conditions' analyses and q_sample with the noise image's unscaled
+    2-level transform (per-channel FATS rows when per_band), bit for bit."""
+    from cwdm_hip import ops
+    from guided_diffusion import script_util
+    shift = [-1.0 + 0.15 * k for k in range(15)] if per_band else None
+    d = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i", wavelet_levels=2,
+                                              band_log_snr_shift=shift)
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"),
+                    band_shift=w2.channel_shift(shift) if per_band else None)
+    g = torch.Generator().manual_seed(14)
+    shape = (2, 1, 8, 12, 16)
+    vols = [torch.rand(shape, generator=g) for _ in range(4)]
+    eps = torch.randn(shape, generator=g)
+    t = torch.tensor([0, 613])
+    x_in, x0 = ops.prepare_batch2(*[v.to(DEV) for v in vols], eps.to(DEV), d.q_coef_table(DEV), t.to(DEV), 1000,
+                                  per_band=per_band)
+    rx0 = w2.analysis2(vols[0])
+    _same(x0, rx0, "x0")
+    _same(x_in[:, 64:], torch.cat([w2.analysis2(v) for v in vols[1:]], 1), "cond")
+    _same(x_in[:, :64], od.q_sample(tab, rx0, t, w2.analysis2(eps, scale=False)), "x_t")
+
+
+def test_config5_training_step_vs_oracle():
+    """Config-5 training (levels = 2): training_losses -> loss.backward() on the
+    native U-Net (256 -> 64 channels, 3 levels, 8^3 level-2 grid from 32^3
+    volumes, FATS per-channel rows) vs the oracle's loss and autograd, fp32."""
+    from guided_diffusion import script_util
+    shift = [-1.5, 0.2, 0.3, 0.5, 0.2, 0.4, 0.6, 1.0] + [0.8, 1.0, 1.2, 1.0, 1.2, 1.4, 1.8]
+    diffusion = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
+                                                      band_log_snr_shift=shift, wavelet_levels=2)
+    P = ou.random_params(seed=21, **C5_CFG)
+    model = _c5_model()
+    model.load_state_dict(P)
+    model.to(DEV)
+    vols = {k: v.to(DEV) for k, v in cases.data.brats_batch(32, seed=5, batch=2).items()}
+    t = torch.tensor([11, 802], device=DEV)
+    noise = torch.randn(2, 1, 32, 32, 32, generator=torch.Generator().manual_seed(8)).to(DEV)
+    terms, out, out_img = diffusion.training_losses(model, vols, t, mode="i2i", contr="t1n", noise=noise)
+    assert terms["mse_wav"].shape == (64,)
+    terms["mse_wav"].mean().backward()
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"), band_shift=w2.channel_shift(shift))
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+
+    def om(x, tt, **kw):
+        return ou.unet_forward(Pr, x, tt, num_groups=8, **C5_CFG)
+    rterms, rout, rimg = od.training_losses(tab, om, {k: v.cpu() for k, v in vols.items()}, t.cpu(), noise.cpu(),
+                                            contr="t1n", levels=2)
+    rloss = rterms["mse_wav"].mean()
+    rloss.backward()
+    assert rel_err(out.detach(), rout.detach()) < 1e-3
+    assert rel_err(out_img, rimg.detach()) < 1e-3
+    assert abs(float(terms["mse_wav"].mean()) - float(rloss)) / float(rloss) < 1e-4
+    for n, p in model.named_parameters():
+        err = float((p.grad.double().cpu() - Pr[n].grad.double()).norm() / Pr[n].grad.double().norm().clamp_min(1e-30))
+        assert err < 1e-3, (n, err)

@@ -58,3 +58,19 @@ def test_per_subband_tables_match_oracle():
     assert tuple(d.coef_table("cpu").shape) == (50, 64, 8)
     with pytest.raises(ValueError):
         script_util.create_gaussian_diffusion(steps=1000, mode="i2i", band_log_snr_shift=np.zeros(8), wavelet_levels=2)
+
+
+@pytest.mark.parametrize("n", [0, 1])
+def test_oracle_unscaled_analysis2_is_pywt_wavedecn(n):
+    """The noise image's transform in the config-5 training front end
+    (analysis2(scale=False): no LLL / 3, as the reference's noise DWT) is the
+    plain orthonormal wavedecn(level=2) in the same channel layout, so unit
+    Gaussian noise stays unit Gaussian."""
+    g = np.load(os.path.join(GOLDEN, "pywt_haar3d_wavedec2.npz"), allow_pickle=False)
+    x = torch.from_numpy(g[f"x{n}"]).view(1, 1, *g[f"x{n}"].shape)
+    c = w2.analysis2(x, scale=False)[0].numpy()
+    assert np.allclose(c[0], g[f"x{n}_L2_LLL"], atol=1e-12)
+    for k, b in enumerate(HIGH):
+        assert np.allclose(c[1 + k], g[f"x{n}_L2_{b}"], atol=1e-12)
+    assert np.isclose(float((c.astype(np.float64) ** 2).sum()), float((g[f"x{n}"].astype(np.float64) ** 2).sum()),
+                      rtol=1e-6)   # the oracle Haar runs in fp32 like the reference
