@@ -263,6 +263,8 @@ class GaussianDiffusion:
             _extract_into_tensor(self.sqrt_recipm1_alphas_cumprod, t, x_t.shape)
 
     def _check_t(self, t):
+        if getattr(t, "_cwdm_t_checked", None) == self.num_timesteps:
+            return    # drawn on the host in range by the schedule sampler (resample.py)
         tmin, tmax = int(t.min()), int(t.max())
         if tmin < 0 or tmax >= self.num_timesteps:
             raise IndexError(f"Timesteps out of bounds: min={tmin}, max={tmax}, arr len={self.num_timesteps}")

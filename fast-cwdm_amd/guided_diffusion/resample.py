@@ -15,6 +15,13 @@ def create_named_schedule_sampler(name, diffusion, maxt=None):
     raise NotImplementedError(f"unknown schedule sampler: {name}")
 
 
+def _upload(t, device):
+    """Host -> device through pinned memory, asynchronous on the current stream."""
+    if th.device(device).type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 class ScheduleSampler(ABC):
     @abstractmethod
     def weights(self):
@@ -24,9 +31,12 @@ class ScheduleSampler(ABC):
         w = self.weights()
         p = w / np.sum(w)
         indices_np = np.random.choice(len(p), size=(batch_size,), p=p)
-        indices = th.from_numpy(indices_np).long().to(device)
+        indices = _upload(th.from_numpy(indices_np).long(), device)
+        # drawn in [0, T) on the host: training_losses need not read them back
+        # from the device to range-check (no host/device sync per step)
+        indices._cwdm_t_checked = len(p)
         weights_np = 1 / (len(p) * p[indices_np])
-        weights = th.from_numpy(weights_np).float().to(device)
+        weights = _upload(th.from_numpy(weights_np).float(), device)
         return indices, weights
 
 

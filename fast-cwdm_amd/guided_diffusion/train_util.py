@@ -154,6 +154,7 @@ class TrainLoop:
                 if os.environ.get("DIFFUSION_TRAINING_TEST", "") and self.step > 0:
                     return
             self.step += 1
+        self.flush_finite_check()
         if lossmse is not None and (self.step - 1) % self.save_interval != 0:
             self.save_if_best(float(lossmse))
 
@@ -167,13 +168,41 @@ class TrainLoop:
             else:
                 info["norm/param_max"] = max(p.abs().max() for p in self.model.parameters())
                 info["norm/grad_max"] = max(p.grad.abs().max() for p in self.model.parameters() if p.grad is not None)
-        if not th.isfinite(lossmse):
-            logger.log(f"Model parameters are finite, but loss is not: {lossmse}", level=logger.WARN)
+        self._check_finite(lossmse)
         self.opt.step()
         self._anneal_lr()
         self.log_step()
         self.last_info = info
         return lossmse, sample, sample_idwt
+
+    def _check_finite(self, lossmse):
+        """The reference's per-step loss check (train_util.py run_step), read
+        back one step late through pinned memory and an event so the host never
+        waits for the device: the warning for step k is logged during step k+1
+        (and by flush_finite_check)."""
+        if not (lossmse.is_cuda and th.cuda.is_available()):
+            if not th.isfinite(lossmse):
+                logger.log(f"Model parameters are finite, but loss is not: {lossmse}", level=logger.WARN)
+            return
+        host = th.empty((), dtype=lossmse.dtype, pin_memory=True)
+        host.copy_(lossmse.detach(), non_blocking=True)
+        ev = th.cuda.Event()
+        ev.record()
+        pending = getattr(self, "_finite_pending", None)
+        self._finite_pending = (host, ev)
+        if pending is not None:
+            self._report_finite(*pending)
+
+    def _report_finite(self, host, ev):
+        ev.synchronize()    # the previous step's loss: long done by now
+        if not bool(th.isfinite(host)):
+            logger.log(f"Model parameters are finite, but loss is not: {host}", level=logger.WARN)
+
+    def flush_finite_check(self):
+        pending = getattr(self, "_finite_pending", None)
+        self._finite_pending = None
+        if pending is not None:
+            self._report_finite(*pending)
 
     def forward_backward(self, batch, cond, label=None):
         for p in self.model.parameters():
