@@ -229,7 +229,9 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   // bench.py A/B on one MI355X): no delay 57.15 vs half-tile 56.80 steps/s
   static const int stagger_env = [] { const char* e = std::getenv("CWDM_CONV_STAGGER"); return e ? std::atoi(e) : 0; }();
   p.stagger_cycles = nblk > 2LL * ncu ? (stagger_env >= 0 ? stagger_env : (p.nch * 17000 + 12000) / 2) : 0;
-  const bool fast = !p.out_f32 && !p.accumulate && !p.out1;
+  // the fast epilogue addresses output / residual through 32-bit buffer offsets per batch
+  const bool fast = !p.out_f32 && !p.accumulate && !p.out1 &&
+                    (long long)p.D * p.H * p.W * p.cout * 2 < 0xFFFFE000LL;
   prof_begin(s);
   if (d->dtype == CWDM_BF16) {
     if (fast) {

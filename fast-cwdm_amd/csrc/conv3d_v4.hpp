@@ -152,67 +152,84 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
     // bf16 fast path: 16-byte residual loads and stores.  A lane pair (l, l+32)
     // holds channels 8j..8j+7 of one voxel split 4 / 4; v_permlane32_swap turns
     // two such groups (j, j+1) into 8 consecutive channels per lane.
-    const bf16_t* res0 = nullptr;
-    long long rHW = 0, rW = 0;
-    if (p.rmode == 0) {
-      res0 = reinterpret_cast<const bf16_t*>(p.res) + vox0 * p.cout + ct * 64 + f * 32 + 8 * hh;
-      rHW = HW * p.cout; rW = (long long)p.W * p.cout;
-    }
-    bf16_t* out0 = reinterpret_cast<bf16_t*>(p.out) + vox0 * p.cout + ct * 64 + f * 32 + 8 * hh;
-    const long long oHW = HW * p.cout, oW = (long long)p.W * p.cout;
+    // Buffer loads / stores on per-batch resources: lanes past W get an
+    // out-of-range offset (loads return 0, stores are dropped), so no lane
+    // branches around a memory instruction, and the residual / no-residual
+    // variants are separate straight-line code: with branches inside, the
+    // waitcnt pass fell back to vmcnt(0) after every store (measured: the
+    // residual epilogue serialised its 16 stores).
+    const int cl = ct * 64 + f * 32 + 8 * hh;   // this lane's first channel (jj = 0)
+    const long long V = (long long)p.D * HW;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<bf16_t*>(p.out) + (long long)b * V * p.cout, (short)0, (int)(V * p.cout * 2), 0x00020000);
+    const unsigned vb0 = (unsigned)((((z0 + 2 * vg) * p.H) + y0) * p.W + ox);  // (plane 0, line 0) in the batch
+    const unsigned rowb = (unsigned)p.W * (unsigned)p.cout * 2u, planeb = (unsigned)HW * (unsigned)p.cout * 2u;
+    const unsigned obase = vb0 * (unsigned)p.cout * 2u + (unsigned)cl * 2u;
+    auto run = [&](auto res_c) {
+      constexpr bool RES = decltype(res_c)::value;
+      u32x4 rq[2][4][2];  // residual rows of both planes, all loads in flight at once
+      if constexpr (RES) {
+        const long long rV = p.rmode == 1 ? V / 8 : V;
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(reinterpret_cast<const bf16_t*>(p.res) + (long long)b * rV * p.cout), (short)0,
+            (int)(rV * p.cout * 2), 0x00020000);
 #pragma unroll
-    for (int pl = 0; pl < 2; ++pl) {
-      u32x4 rq[4][2];  // this plane's residual rows, all loads in flight at once
-      if (p.rmode >= 0) {
+        for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            unsigned r0 = obase + (unsigned)pl * planeb + (unsigned)m * rowb;
+            if (p.rmode == 1) {
+              const int oy = y0 + m, oz = z0 + 2 * vg + pl;
+              const unsigned rvb = (unsigned)(((oz >> 1) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1));
+              r0 = rvb * (unsigned)p.cout * 2u + (unsigned)cl * 2u;
+            }
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+              rq[pl][m][jj] = __builtin_amdgcn_raw_buffer_load_b128(rr, xin ? r0 + 32u * jj : 0xFFFFFFF0u, 0, 0);
+          }
+        // all 16 loads ahead of every store: a load issued after a store would
+        // make its wait drain that store too (vmcnt counts in issue order)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) {
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-          const bf16_t* r;
-          if (p.rmode == 0) {
-            r = res0 + pl * rHW + m * rW;
-          } else {
-            const int oy = y0 + m, oz = z0 + 2 * vg + pl;
-            const long long rvox =
-                (((long long)b * (p.D >> 1) + (oz >> 1)) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1);
-            r = reinterpret_cast<const bf16_t*>(p.res) + rvox * p.cout + ct * 64 + f * 32 + 8 * hh;
-          }
+          const unsigned oo = obase + (unsigned)pl * planeb + (unsigned)m * rowb;
 #pragma unroll
-          for (int jj = 0; jj < 2; ++jj) rq[m][jj] = xin ? *reinterpret_cast<const u32x4*>(r + 16 * jj) : u32x4{0, 0, 0, 0};
+          for (int jj = 0; jj < 2; ++jj) {
+            float v[8];  // groups j = 2 jj (v[0..3]) and 2 jj + 1 (v[4..7]) in accumulator layout
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = acc[pl][m][8 * jj + k];
+            if constexpr (RES) {
+              const u32x4 q = rq[pl][m][jj];
+              const auto s0 = __builtin_amdgcn_permlane32_swap(q[0], q[2], false, false);
+              const auto s1 = __builtin_amdgcn_permlane32_swap(q[1], q[3], false, false);
+              const unsigned g0 = s0[0], g1 = s1[0], h0 = s0[1], h1 = s1[1];
+              v[0] += __uint_as_float(g0 << 16); v[1] += __uint_as_float(g0 & 0xffff0000u);
+              v[2] += __uint_as_float(g1 << 16); v[3] += __uint_as_float(g1 & 0xffff0000u);
+              v[4] += __uint_as_float(h0 << 16); v[5] += __uint_as_float(h0 & 0xffff0000u);
+              v[6] += __uint_as_float(h1 << 16); v[7] += __uint_as_float(h1 & 0xffff0000u);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float vv = v[k] * xm;
+              ssum[8 * jj + k] += vv;
+              ssq[8 * jj + k] += vv * vv;
+            }
+            const unsigned p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
+            const unsigned p2 = pack_bf16x2(v[4], v[5]), p3 = pack_bf16x2(v[6], v[7]);
+            const auto t0 = __builtin_amdgcn_permlane32_swap(p0, p2, false, false);
+            const auto t1 = __builtin_amdgcn_permlane32_swap(p1, p3, false, false);
+            u32x4 w;
+            w[0] = t0[0]; w[1] = t1[0]; w[2] = t0[1]; w[3] = t1[1];
+            __builtin_amdgcn_raw_buffer_store_b128(w, ro, xin ? oo + 32u * jj : 0xFFFFFFF0u, 0, 0);
+          }
         }
       }
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        bf16_t* o = out0 + pl * oHW + m * oW;
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          float v[8];  // groups j = 2 jj (v[0..3]) and 2 jj + 1 (v[4..7]) in accumulator layout
-#pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] = acc[pl][m][8 * jj + k];
-          if (p.rmode >= 0) {
-            const u32x4 q = rq[m][jj];
-            const auto s0 = __builtin_amdgcn_permlane32_swap(q[0], q[2], false, false);
-            const auto s1 = __builtin_amdgcn_permlane32_swap(q[1], q[3], false, false);
-            const unsigned g0 = s0[0], g1 = s1[0], h0 = s0[1], h1 = s1[1];
-            v[0] += __uint_as_float(g0 << 16); v[1] += __uint_as_float(g0 & 0xffff0000u);
-            v[2] += __uint_as_float(g1 << 16); v[3] += __uint_as_float(g1 & 0xffff0000u);
-            v[4] += __uint_as_float(h0 << 16); v[5] += __uint_as_float(h0 & 0xffff0000u);
-            v[6] += __uint_as_float(h1 << 16); v[7] += __uint_as_float(h1 & 0xffff0000u);
-          }
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const float vv = v[k] * xm;
-            ssum[8 * jj + k] += vv;
-            ssq[8 * jj + k] += vv * vv;
-          }
-          const unsigned p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
-          const unsigned p2 = pack_bf16x2(v[4], v[5]), p3 = pack_bf16x2(v[6], v[7]);
-          const auto t0 = __builtin_amdgcn_permlane32_swap(p0, p2, false, false);
-          const auto t1 = __builtin_amdgcn_permlane32_swap(p1, p3, false, false);
-          u32x4 w;
-          w[0] = t0[0]; w[1] = t1[0]; w[2] = t0[1]; w[3] = t1[1];
-          if (xin) *reinterpret_cast<u32x4*>(o + 16 * jj) = w;
-        }
-      }
-    }
+    };
+    if (p.rmode >= 0) run(std::true_type{});
+    else run(std::false_type{});
   } else {
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl) {
@@ -294,7 +311,10 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
         R[hh * 32 + 16 + i] = ssq[i];
       }
     }
-    __syncthreads();
+    // LDS-only exchange: wait for the LDS writes, not for the output stores
+    // (__syncthreads' fence would drain them: vmcnt(0))
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     if (tid < 64) {
       const int ff = tid >> 5, c32 = tid & 31, j = c32 >> 3, h2 = (c32 >> 2) & 1, k = c32 & 3;
       const int i = 4 * j + k;
@@ -309,6 +329,87 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
   }
 }
 
+// Work item of a persistent workgroup: iteration it of workgroup blockIdx.x ->
+// (batch b, spatial tile sl, channel tile ct, origin, K slice ks = chunks
+// [c0, c1)) through the XCD-aware bijective map: the tiles an XCD runs are one
+// contiguous run (x fastest; K slice slowest, so the tiles an XCD runs share
+// their weight chunks).
+struct V4Tile { int b, sl, ct, x0, y0, z0, ks, c0, c1; };
+__device__ __forceinline__ V4Tile v4_tile_of(const V4Params& p, int it) {
+  const int tiles = p.tx * p.ty * p.tz;
+  const int nbase = p.nblk / p.ksplit;
+  const int t = blockIdx.x + it * gridDim.x;
+  const int xcd = t & 7, q8 = p.nblk >> 3, r8 = p.nblk & 7;
+  int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (t >> 3);
+  V4Tile r;
+  r.ks = wg / nbase;
+  wg -= r.ks * nbase;
+  r.c0 = r.ks * p.kper;
+  r.c1 = min(p.nch, r.c0 + p.kper);
+  r.ct = wg % p.nct;
+  const int st = wg / p.nct;
+  r.b = st / tiles;
+  r.sl = st - r.b * tiles;
+  r.x0 = (r.sl % p.tx) * 32; r.y0 = ((r.sl / p.tx) % p.ty) * 4; r.z0 = (r.sl / (p.tx * p.ty)) * 4;
+  // wave-uniform by construction; say so, or every buffer op gets a waterfall loop
+  r.ct = __builtin_amdgcn_readfirstlane(r.ct); r.b = __builtin_amdgcn_readfirstlane(r.b);
+  r.sl = __builtin_amdgcn_readfirstlane(r.sl); r.x0 = __builtin_amdgcn_readfirstlane(r.x0);
+  r.y0 = __builtin_amdgcn_readfirstlane(r.y0); r.z0 = __builtin_amdgcn_readfirstlane(r.z0);
+  r.ks = __builtin_amdgcn_readfirstlane(r.ks); r.c0 = __builtin_amdgcn_readfirstlane(r.c0);
+  r.c1 = __builtin_amdgcn_readfirstlane(r.c1);
+  return r;
+}
+
+// Halo pieces of chunk c of tile tt into the halo buffer at hb (LDS-DMA; wave wv
+// issues pieces wv + 4 j).  Pieces wv + 4 j and wv + 4 (j + 5) cover the same
+// voxel slots of the two quad planes, so 5 voxel indices serve all 10; -2 marks
+// the padding slots (never written: bias / statistics scratch).  Recomputed per
+// chunk (a few VALU per piece) rather than held in registers.
+template <typename T, int MODE>
+__device__ __forceinline__ void v4_issue_halo(const V4Params& p, const V4Tile& tt, int c, unsigned char* hb, int wv,
+                                              int lane) {
+  using C = V4Cfg;
+  constexpr int CK = ConvTr<T>::CK;
+  constexpr int ESZ = sizeof(T);
+  const int SH = MODE == 1 ? p.H >> 1 : p.H, SW = MODE == 1 ? p.W >> 1 : p.W;
+  int svox[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int hv = (wv + 4 * j) * 64 + lane;
+    int sv = -2;
+    if (hv < C::HV) {
+      sv = -1;
+      const int hx = hv % C::HX, hy = (hv / C::HX) % C::HY, hz = hv / (C::HX * C::HY);
+      int ox = tt.x0 + hx - 1, oy = tt.y0 + hy - 1, oz = tt.z0 + hz - 1;
+      if (ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) {
+        if (MODE == 1) { ox >>= 1; oy >>= 1; oz >>= 1; }
+        sv = (oz * SH + oy) * SW + ox;
+      }
+    }
+    svox[j] = sv;
+  }
+  const bool s0 = c < p.nch0;
+  const unsigned char* base = s0 ? reinterpret_cast<const unsigned char*>(p.a0) + (long long)tt.b * p.a0_bstride
+                                 : reinterpret_cast<const unsigned char*>(p.a1) + (long long)tt.b * p.a1_bstride;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(s0 ? p.a0_bytes : p.a1_bytes), 0x00020000);
+  const int cs = s0 ? p.ac0 : p.ac1;
+  const int cb = (s0 ? c : c - p.nch0) * CK;
+  // byte offset of (voxel sv, quad qd) = sv * rowb + cofs + 16 qd
+  const bool cm = s0 && p.a0_cm;
+  const unsigned rowb = cm ? 32u : (unsigned)cs * ESZ;
+  const unsigned cofs = cm ? (unsigned)c * (unsigned)p.a0_cvox * 32u : (unsigned)(cb * ESZ);
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const int pc = wv + 4 * j;
+    const int sv = svox[j % 5];
+    const unsigned voff = sv >= 0 ? (unsigned)sv * rowb + cofs + (unsigned)((j / 5) * 16) : 0xFFFFFFF0u;
+    if (sv != -2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(hb + pc * 1024), 16,
+                                               voff, 0, 0, 0);
+  }
+}
+
 // Persistent: gridDim.x <= the number of tiles; workgroup k runs tiles
 // k, k + gridDim.x, ... as one continuous chunk stream, so the next tile's halo,
 // weights and bias are prefetched under the current tile's last chunk.
@@ -316,8 +417,6 @@ template <typename T, int MODE, bool FAST>
 __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   static_assert(!FAST || sizeof(T) == 2, "the fast epilogue is bf16 only");
   using C = V4Cfg;
-  constexpr int CK = ConvTr<T>::CK;
-  constexpr int ESZ = sizeof(T);
   __shared__ __attribute__((aligned(1024))) unsigned char smem[C::SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, hh = lane >> 5;
@@ -352,80 +451,12 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
     __syncthreads();
   }
   const int nblk = p.nblk;
-  const int tiles = p.tx * p.ty * p.tz;
-  const int SH = MODE == 1 ? p.H >> 1 : p.H, SW = MODE == 1 ? p.W >> 1 : p.W;
-  // tile it of this workgroup -> (b, spatial tile sl, channel tile ct, origin) through the
-  // XCD-aware bijective map: the tiles an XCD runs are one contiguous run (x fastest)
-  // (K slice slowest: the tiles an XCD runs share their weight chunks)
-  struct Tile { int b, sl, ct, x0, y0, z0, ks, c0, c1; };
-  const int nbase = nblk / p.ksplit;
-  auto tile_of = [&](int it) {
-    const int t = blockIdx.x + it * gridDim.x;
-    const int xcd = t & 7, q8 = nblk >> 3, r8 = nblk & 7;
-    int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (t >> 3);
-    Tile r;
-    r.ks = wg / nbase;
-    wg -= r.ks * nbase;
-    r.c0 = r.ks * p.kper;
-    r.c1 = min(p.nch, r.c0 + p.kper);
-    r.ct = wg % p.nct;
-    const int st = wg / p.nct;
-    r.b = st / tiles;
-    r.sl = st - r.b * tiles;
-    r.x0 = (r.sl % p.tx) * 32; r.y0 = ((r.sl / p.tx) % p.ty) * 4; r.z0 = (r.sl / (p.tx * p.ty)) * 4;
-    // wave-uniform by construction; say so, or every buffer op gets a waterfall loop
-    r.ct = __builtin_amdgcn_readfirstlane(r.ct); r.b = __builtin_amdgcn_readfirstlane(r.b);
-    r.sl = __builtin_amdgcn_readfirstlane(r.sl); r.x0 = __builtin_amdgcn_readfirstlane(r.x0);
-    r.y0 = __builtin_amdgcn_readfirstlane(r.y0); r.z0 = __builtin_amdgcn_readfirstlane(r.z0);
-    r.ks = __builtin_amdgcn_readfirstlane(r.ks); r.c0 = __builtin_amdgcn_readfirstlane(r.c0);
-    r.c1 = __builtin_amdgcn_readfirstlane(r.c1);
-    return r;
-  };
+  using Tile = V4Tile;
+  auto tile_of = [&](int it) { return v4_tile_of(p, it); };
   const int ntile = (nblk - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
 
-  // halo pieces of chunk c of tile tt into halo buffer hbuf
-  // Per-lane source voxel of this wave's pieces: pieces wv + 4 j and wv + 4 (j + 5)
-  // cover the same voxel slots of the two quad planes, so 5 voxel indices serve
-  // all 10; -2 marks the padding slots (never written: bias / statistics scratch).
-  // Recomputed per chunk (a few VALU per piece) rather than held in registers.
   auto issue_halo = [&](const Tile& tt, int c, int hbuf) {
-    int svox[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int hv = (wv + 4 * j) * 64 + lane;
-      int sv = -2;
-      if (hv < C::HV) {
-        sv = -1;
-        const int hx = hv % C::HX, hy = (hv / C::HX) % C::HY, hz = hv / (C::HX * C::HY);
-        int ox = tt.x0 + hx - 1, oy = tt.y0 + hy - 1, oz = tt.z0 + hz - 1;
-        if (ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) {
-          if (MODE == 1) { ox >>= 1; oy >>= 1; oz >>= 1; }
-          sv = (oz * SH + oy) * SW + ox;
-        }
-      }
-      svox[j] = sv;
-    }
-    const bool s0 = c < p.nch0;
-    const unsigned char* base = s0 ? reinterpret_cast<const unsigned char*>(p.a0) + (long long)tt.b * p.a0_bstride
-                                   : reinterpret_cast<const unsigned char*>(p.a1) + (long long)tt.b * p.a1_bstride;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(s0 ? p.a0_bytes : p.a1_bytes), 0x00020000);
-    const int cs = s0 ? p.ac0 : p.ac1;
-    const int cb = (s0 ? c : c - p.nch0) * CK;
-    // byte offset of (voxel sv, quad qd) = sv * rowb + cofs + 16 qd
-    const bool cm = s0 && p.a0_cm;
-    const unsigned rowb = cm ? 32u : (unsigned)cs * ESZ;
-    const unsigned cofs = cm ? (unsigned)c * (unsigned)p.a0_cvox * 32u : (unsigned)(cb * ESZ);
-    unsigned char* hb = smem + hbuf * C::HALO_B;
-#pragma unroll
-    for (int j = 0; j < 10; ++j) {
-      const int pc = wv + 4 * j;
-      const int sv = svox[j % 5];
-      const unsigned voff = sv >= 0 ? (unsigned)sv * rowb + cofs + (unsigned)((j / 5) * 16) : 0xFFFFFFF0u;
-      if (sv != -2)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(hb + pc * 1024), 16,
-                                                 voff, 0, 0, 0);
-    }
+    v4_issue_halo<T, MODE>(p, tt, c, smem + hbuf * C::HALO_B, wv, lane);
   };
   // weight fragments of group g of chunk c, channel tile ct: the 3 dy taps, this
   // lane's row (output channel) lr of the wave's 32-channel slice, quad hh
