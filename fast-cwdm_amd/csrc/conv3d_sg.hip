@@ -1,0 +1,366 @@
+// Conv3d 3x3x3 (stride 1, pad 1) for the small-grid U-Net levels (16^3, 8^3:
+// W = 16 or 8), bf16, on v_mfma_f32_16x16x32_bf16.  Same contract as the
+// DMA-staged wide-grid kernel (V4Params: GroupNorm+SiLU and the 1x1 skip are
+// pre-passes in conv3d_v4_forward; this kernel stages raw copies), called from
+// v4_launch for shapes sg_eligible() accepts.
+//
+// Why a separate kernel: a 16^3 x 256-channel conv is only 4096 x 256 outputs.
+// The wide kernel's 512-voxel x 64-channel tiles give 32 work items there, so
+// the brick kernels split K (768 items) and pay two finishing passes over the
+// fp32 slices (splitk_sum + conv3d_reduce, ~17 us per conv at 16^3, more than
+// the conv's MFMA work).  Here a work item is one statistics brick of
+// pick_brick (16x4x4 or 8x8x4 = 256 voxels, the partial layout of
+// cwdm_conv3d_parts is unchanged) x 16 output channels with the whole K:
+// 256 workgroups at 16^3, no split, no finishing pass.
+//
+//   * 4 waves, wave w = z-plane w of the brick (64 voxels = 4 B operands of
+//     16 voxels: one x line of 16, or two lines of 8).
+//   * K chunks of 32 input channels (two 16-channel sub-chunks: chunk-major
+//     gn_apply output or channels-last sources, concat boundary per
+//     sub-chunk); MFMA K = the chunk's 32 channels of one tap.
+//   * Halo image in LDS, quad-major [4 quads][HVP slots][16 B], double
+//     buffered, filled by LDS-DMA (out-of-volume voxels read as zeros through
+//     the buffer range check).  A ds_read_b128 of 16 lanes reads 16
+//     consecutive halo slots of one quad plane.
+//   * The chunk's A fragments (16 output channels x 32 K per tap, 27 KB) are
+//     LDS-DMA'd beside its halo, double-buffered too: one workgroup per CU
+//     (144 KB of LDS) has no co-resident partner to hide global-load latency,
+//     so nothing in the inner loop waits on memory; one vmcnt(0) + barrier
+//     per chunk.
+//   * Per (dz, dx) group the operand lines are read once and feed the 3 dy
+//     taps (6 reads / 12 MFMAs at W = 16, 9 / 12 at W = 8), with the group's 3
+//     A fragments; the next group's reads are issued before this group's
+//     MFMAs.
+//   * Epilogue: + bias, + residual (same grid / nearest-upsampled), bf16
+//     store, per-(brick, channel) (sum, sum^2) partials for the next
+//     GroupNorm.
+#include <atomic>
+#include <type_traits>
+
+#include "conv3d_v4.hpp"
+
+namespace cwdm {
+
+typedef float sg_f32x4 __attribute__((ext_vector_type(4)));
+
+template <int BX, int BY, int PAD>
+struct SGCfg {
+  // PAD 1: the 3x3x3 halo (648 / 600 voxels); PAD 0: the brick itself (1x1 skip)
+  static constexpr int HX = BX + 2 * PAD, HY = BY + 2 * PAD, HZ = 4 + 2 * PAD, HV = HX * HY * HZ;
+  static constexpr int PCS = (HV + 63) / 64;                                   // 64-slot pieces per quad plane
+  static constexpr int HVP = PCS * 64;                                         // 704 slots
+  static constexpr int QB = HVP * 16;                                          // bytes per quad plane
+  static constexpr int BUF = 4 * QB;                                           // one halo buffer (32 channels)
+  static constexpr int WBUF = 27 * 1024;       // one chunk's A fragments: [tap][lane][16 B]
+  static constexpr int SMEM = 2 * BUF + 2 * WBUF;
+  static constexpr int LPO = 16 / BX;         // x lines per 16-voxel operand
+  static constexpr int NR = 3 * LPO + 3;      // distinct operand line starts per (dz, dx) group
+  static_assert(BX * BY == 64, "a brick plane is 64 voxels");
+};
+
+struct SGParams {
+  V4Params v;   // shape / sources / weights / epilogue as for the wide kernel (ct counts 64-row tiles)
+  int ntile16;  // output channel tiles of 16
+  int parts;    // statistics bricks per batch
+};
+
+__device__ __forceinline__ void sg_mfma(sg_f32x4& acc, const u32x4& a, const u32x4& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0,
+                                                0, 0);
+}
+
+// TAPS = 27: the 3x3x3 conv; TAPS = 1: the 1x1 skip conv of a ResBlock (the
+// centre tap of the same halo image and weight buffer, packed with k = 1)
+template <int BX, int BY, int MODE, int TAPS>
+__global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
+  static_assert(TAPS == 27 || TAPS == 1, "3x3x3 or 1x1");
+  constexpr int PAD = TAPS == 27 ? 1 : 0;
+  using C = SGCfg<BX, BY, PAD>;
+  const V4Params& p = q.v;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[C::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // work item -> (batch, brick, 16-channel tile); channel tile fastest (the 16
+  // workgroups of a brick share its halo in L2)
+  const int t16 = blockIdx.x % q.ntile16;
+  const int st = blockIdx.x / q.ntile16;
+  const int b = st / q.parts, brick = st - b * q.parts;
+  const int tx = p.W / BX, ty = p.H / BY;
+  const int x0 = (brick % tx) * BX, y0 = ((brick / tx) % ty) * BY, z0 = (brick / (tx * ty)) * 4;
+  const int SH = MODE == 1 ? p.H >> 1 : p.H, SW = MODE == 1 ? p.W >> 1 : p.W;
+  const int nch = p.nch / 2;  // 32-channel chunks
+
+  // halo DMA of 32-channel chunk c into buffer hbuf: pieces pc = wv + 4 j (44 in
+  // all: quad plane pc / PCS, slot block pc % PCS); quads 0-1 / 2-3 are the two
+  // 16-channel sub-chunks 2c / 2c + 1
+  auto issue_halo = [&](int c, int hbuf) {
+    unsigned char* hb = smem + hbuf * C::BUF;
+#pragma unroll
+    for (int j = 0; j < C::PCS; ++j) {
+      const int pc = wv + 4 * j;
+      const int qd = pc / C::PCS, blk = pc - qd * C::PCS;
+      const int hv = blk * 64 + lane;
+      if (hv >= C::HV) continue;  // padding slots: statistics scratch
+      int sv = -1;
+      {
+        const int hx = hv % C::HX, hy = (hv / C::HX) % C::HY, hz = hv / (C::HX * C::HY);
+        int ox = x0 + hx - PAD, oy = y0 + hy - PAD, oz = z0 + hz - PAD;
+        if (ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) {
+          if (MODE == 1) { ox >>= 1; oy >>= 1; oz >>= 1; }
+          sv = (oz * SH + oy) * SW + ox;
+        }
+      }
+      const int sc = 2 * c + (qd >> 1);  // 16-channel sub-chunk
+      const bool s0 = sc < p.nch0;
+      const unsigned char* base = s0 ? reinterpret_cast<const unsigned char*>(p.a0) + (long long)b * p.a0_bstride
+                                     : reinterpret_cast<const unsigned char*>(p.a1) + (long long)b * p.a1_bstride;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(s0 ? p.a0_bytes : p.a1_bytes), 0x00020000);
+      const bool cm = s0 && p.a0_cm;
+      const unsigned rowb = cm ? 32u : (unsigned)(s0 ? p.ac0 : p.ac1) * 2u;
+      const unsigned cofs = cm ? (unsigned)sc * (unsigned)p.a0_cvox * 32u : (unsigned)((s0 ? sc : sc - p.nch0) * 32);
+      const unsigned voff = sv >= 0 ? (unsigned)sv * rowb + cofs + (unsigned)((qd & 1) * 16) : 0xFFFFFFF0u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(hb + pc * 1024), 16, voff,
+                                               0, 0, 0);
+    }
+  };
+
+  // A fragments of chunk c into weight buffer wbuf by LDS-DMA: piece = tap t
+  // (wave wv issues taps wv + 4 j), lane (kq, l16) = row t16 * 16 + l16 of the
+  // packed 64-row tile, sub-chunk 2c + (kq >> 1), quad kq & 1: the A operand
+  // layout, so a lane's ds_read_b128 of [t][lane] is its fragment
+  const int ct64 = t16 >> 2, row = (t16 & 3) * 16 + l16;
+  const unsigned wlane = (unsigned)(row * 32 + (((kq & 1) ^ ((row >> 3) & 1)) << 4));
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.aw + (long long)ct64 * p.nch * TAPS * 2048), (short)0, p.nch * TAPS * 2048, 0x00020000);
+  auto issue_w = [&](int c, int wbuf) {
+    unsigned char* wb = smem + 2 * C::BUF + wbuf * C::WBUF;
+    const unsigned cb = (unsigned)((2 * c + (kq >> 1)) * TAPS) * 2048u + wlane;
+#pragma unroll
+    for (int j = 0; j < (TAPS + 3) / 4; ++j) {
+      const int t = wv + 4 * j;
+      if (t < TAPS)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(wb + t * 1024), 16,
+                                                 cb + (unsigned)t * 2048u, 0, 0, 0);
+    }
+  };
+
+  // lane read base: halo slot of (plane wv, operand line yl, x) in quad plane kq
+  const int xl = l16 % BX, yl = l16 / BX;
+  const int hlane = kq * C::QB + ((wv * C::HY + yl) * C::HX + xl) * 16;
+
+  sg_f32x4 acc[4];
+  {
+    float bi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      bi[i] = p.bias ? p.bias[(long long)b * p.bias_bs + t16 * 16 + 4 * kq + i] : 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[m] = sg_f32x4{bi[0], bi[1], bi[2], bi[3]};
+  }
+
+  issue_halo(0, 0);
+  issue_w(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int c = 0; c < nch; ++c) {
+    const bool has_next = c + 1 < nch;
+    const unsigned char* hb = smem + (c & 1) * C::BUF + hlane;
+    const unsigned char* wb = smem + 2 * C::BUF + (c & 1) * C::WBUF + lane * 16;
+    u32x4 av[2][C::NR], aw[2][3];
+    auto read_group = [&](u32x4 (&a)[C::NR], u32x4 (&w)[3], int g) {
+      const int dz = g / 3, dx = g % 3;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) w[dy] = *reinterpret_cast<const u32x4*>(wb + (dz * 9 + dy * 3 + dx) * 1024);
+#pragma unroll
+      for (int s = 0; s < C::NR; ++s)
+        a[s] = *reinterpret_cast<const u32x4*>(hb + ((dz * C::HY + s) * C::HX + dx) * 16);
+    };
+    if constexpr (TAPS == 27) {
+      read_group(av[0], aw[0], 0);
+    } else {
+      // the brick image (no halo): operand lines 0 .. 3 of plane wv; the one A
+      // fragment sits at tap slot 0
+#pragma unroll
+      for (int s2 = 0; s2 < 4 * C::LPO; s2 += C::LPO)
+        av[0][s2] = *reinterpret_cast<const u32x4*>(hb + s2 * C::HX * 16);
+      aw[0][0] = *reinterpret_cast<const u32x4*>(wb);
+    }
+    // the next chunk's halo and weights go to the other buffers (last read by
+    // chunk c - 1, which every wave finished before the previous barrier)
+    if (has_next) {
+      issue_halo(c + 1, (c + 1) & 1);
+      issue_w(c + 1, (c + 1) & 1);
+    }
+    if constexpr (TAPS == 27) {
+#pragma unroll
+      for (int g = 0; g < 9; ++g) {
+        if (g + 1 < 9) read_group(av[(g + 1) & 1], aw[(g + 1) & 1], g + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) sg_mfma(acc[m], aw[g & 1][dy], av[g & 1][m * C::LPO + dy]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) sg_mfma(acc[m], aw[0][0], av[0][m * C::LPO]);
+    }
+    if (has_next) {
+      // the next chunk's halo and weights have landed; every wave is past this
+      // chunk's reads of the buffers the chunk after next will fill
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+
+  // epilogue: lane (l16, kq) of operand m holds channels t16 16 + 4 kq + i of
+  // voxel (x0 + xl, y0 + m LPO + yl, z0 + wv)
+  const int ox = x0 + xl, oz = z0 + wv;
+  const long long HW = (long long)p.H * p.W;
+  float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
+  const int co = t16 * 16 + 4 * kq;
+  uint2 rq[4];
+  if (p.rmode >= 0) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int oy = y0 + m * C::LPO + yl;
+      long long rvox = ((long long)b * p.D + oz) * HW + (long long)oy * p.W + ox;
+      if (p.rmode == 1)
+        rvox = (((long long)b * (p.D >> 1) + (oz >> 1)) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1);
+      rq[m] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.res) + rvox * p.cout + co);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int oy = y0 + m * C::LPO + yl;
+    const long long vox = ((long long)b * p.D + oz) * HW + (long long)oy * p.W + ox;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = acc[m][i];
+    if (p.rmode >= 0) {
+      v[0] += __uint_as_float(rq[m].x << 16); v[1] += __uint_as_float(rq[m].x & 0xffff0000u);
+      v[2] += __uint_as_float(rq[m].y << 16); v[3] += __uint_as_float(rq[m].y & 0xffff0000u);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ssum[i] += v[i];
+      ssq[i] += v[i] * v[i];
+    }
+    uint2 sq;
+    sq.x = pack_bf16x2(v[0], v[1]);
+    sq.y = pack_bf16x2(v[2], v[3]);
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + vox * p.cout + co) = sq;
+  }
+  if (p.stats) {
+    // rows of 16 lanes hold 4 channels for 16 voxels: DPP row sums, then the 4
+    // plane waves through the halo padding slots of buffer 0
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ssum[i] = row16_sum(ssum[i]);
+      ssq[i] = row16_sum(ssq[i]);
+    }
+    __syncthreads();  // every wave is done with the halo buffers
+    float* R = reinterpret_cast<float*>(smem);  // [wave][16 sums | 16 squares]
+    if (l16 == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        R[wv * 32 + 4 * kq + i] = ssum[i];
+        R[wv * 32 + 16 + 4 * kq + i] = ssq[i];
+      }
+    }
+    __syncthreads();
+    if (tid < 16) {
+      float s = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        s += R[w * 32 + tid];
+        s2 += R[w * 32 + 16 + tid];
+      }
+      const long long pidx = ((long long)b * q.parts + brick) * p.cout + t16 * 16 + tid;
+      p.stats[pidx * 2 + 0] = s;
+      p.stats[pidx * 2 + 1] = s2;
+    }
+  }
+}
+
+template __global__ void conv3d_sg_kernel<16, 4, 0, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<16, 4, 1, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<16, 4, 0, 1>(SGParams);
+
+extern std::atomic<int> g_conv_path;
+
+namespace {
+bool sg_shape_ok(const cwdm_conv3d_desc* d) {
+  if (g_conv_path.load(std::memory_order_relaxed) == 1) return false;
+  if (d->dtype != CWDM_BF16 || d->out_dtype != CWDM_BF16 || d->accumulate || d->out1 || d->cout % 64) return false;
+  return d->W == 16 && d->H % 4 == 0 && d->D % 4 == 0;
+}
+}  // namespace
+
+// shapes the small-grid kernel takes: bf16, plain bf16 output (no fp32 / dual /
+// accumulating output), same-grid or upsampled source and residual, W = 16
+// (the 16x4x4 statistics bricks), 32-channel K chunks.  (At 8^3 there are only
+// 32 work items of this shape: measured slower than the split-K bricks.)
+bool sg_eligible(const cwdm_conv3d_desc* d) {
+  if (!sg_shape_ok(d) || !d->a_w) return false;
+  if (d->a_mode != 0 && d->a_mode != 1) return false;
+  if (d->res_mode < -1 || d->res_mode > 1) return false;
+  if ((d->a_c0 + d->a_c1) % 32 || d->a_c0 % 16) return false;
+  const int64_t V = d->D * d->H * d->W;
+  const int64_t SV = d->a_mode == 1 ? V / 8 : V;
+  return SV * (d->a_c0 + d->a_c1) * 2 < 0xFFFFE000LL && d->B * (V / 256) * (d->cout / 16) < (1LL << 31);
+}
+
+// the 1x1 skip segment alone (segment B of a desc, channels-last sources)
+bool sg_skip_eligible(const cwdm_conv3d_desc* d) {
+  if (!sg_shape_ok(d) || !d->b_w) return false;
+  if ((d->b_c0 + d->b_c1) % 32 || d->b_c0 % 16) return false;
+  const int64_t V = d->D * d->H * d->W;
+  return V * (d->b_c0 + d->b_c1) * 2 < 0xFFFFE000LL && d->B * (V / 256) * (d->cout / 16) < (1LL << 31);
+}
+
+namespace {
+int sg_go(const SGParams& q, const cwdm_conv3d_desc* d, int taps, double flops, hipStream_t s) {
+  const dim3 grid((unsigned)(d->B * q.parts * q.ntile16));
+  prof_begin(s);
+  if (taps == 1) hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 0, 1>), grid, dim3(256), 0, s, q);
+  else if (q.v.amode == 1) hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 1, 27>), grid, dim3(256), 0, s, q);
+  else hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 0, 27>), grid, dim3(256), 0, s, q);
+  prof_end(s, flops);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+}  // namespace
+
+int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, hipStream_t s) {
+  SGParams q{};
+  q.v = v;
+  q.ntile16 = d->cout / 16;
+  q.parts = (int)((d->D / 4) * (d->H / 4));
+  return sg_go(q, d, 27, 2.0 * d->B * d->D * d->H * d->W * (double)d->cout * 27.0 * (d->a_c0 + d->a_c1), s);
+}
+
+// out = W_skip . [b0 | b1] (bf16, no bias / residual / statistics): the skip pre-pass of conv3d_v4_forward
+int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, hipStream_t s) {
+  SGParams q{};
+  V4Params& p = q.v;
+  const int64_t V = d->D * d->H * d->W;
+  p.B = (int)d->B; p.D = (int)d->D; p.H = (int)d->H; p.W = (int)d->W;
+  p.cout = d->cout; p.nct = d->cout / 64;
+  p.nch0 = d->b_c0 / 16; p.nch = (d->b_c0 + d->b_c1) / 16;
+  p.a0 = d->b0; p.ac0 = d->b_c0; p.a1 = d->b1; p.ac1 = d->b_c1;
+  p.a0_bstride = V * d->b_c0 * 2; p.a1_bstride = V * d->b_c1 * 2;
+  p.a0_bytes = (unsigned)(V * d->b_c0 * 2); p.a1_bytes = (unsigned)(V * d->b_c1 * 2);
+  p.amode = 0; p.a0_cm = 0; p.a0_cvox = (int)V;
+  p.aw = reinterpret_cast<const unsigned char*>(d->b_w);
+  p.bias = nullptr; p.res = nullptr; p.rmode = -1;
+  p.out = out; p.stats = nullptr;
+  q.ntile16 = d->cout / 16;
+  q.parts = (int)((d->D / 4) * (d->H / 4));
+  return sg_go(q, d, 1, 2.0 * d->B * V * (double)d->cout * (d->b_c0 + d->b_c1), s);
+}
+
+}  // namespace cwdm

@@ -99,6 +99,11 @@ std::atomic<int> g_conv_path{[] {
 
 std::atomic<unsigned long long*> g_stamps{nullptr};
 
+bool sg_eligible(const cwdm_conv3d_desc* d);
+bool sg_skip_eligible(const cwdm_conv3d_desc* d);
+int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, hipStream_t s);
+int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, hipStream_t s);
+
 int64_t v4_items(const cwdm_conv3d_desc* d) {
   return d->B * ((d->W + 31) / 32) * (d->H / 4) * (d->D / 4) * (d->cout / 64);
 }
@@ -115,6 +120,7 @@ int64_t v4_ksplit_target() {
 // K split of a grid with fewer tiles than two workgroups per CU (the 32^3
 // level): enough K slices for ~512 work items, at least two chunks per slice
 int v4_ksplit(const cwdm_conv3d_desc* d) {
+  if (sg_eligible(d)) return 1;  // the small-grid kernel runs the whole K per work item
   const int ck = d->dtype == CWDM_BF16 ? 16 : 8;
   const int nch = (d->a_c0 + d->a_c1) / ck;
   const int64_t nblk = v4_items(d);
@@ -129,6 +135,7 @@ int v4_ksplit(const cwdm_conv3d_desc* d) {
 bool v4_eligible(const cwdm_conv3d_desc* d) {
   const int path = g_conv_path.load(std::memory_order_relaxed);
   if (path == 1) return false;
+  if (sg_eligible(d)) return true;  // 16^3 / 8^3 levels: conv3d_sg.hip behind the same pre-passes
   if (d->dtype != CWDM_BF16 && d->dtype != CWDM_F32) return false;
   // W >= 32: the statistics partials follow cwdm_conv3d_parts' 32-wide x tiles (pick_brick)
   if (!d->a_w || d->W < 32 || d->H % 4 || d->D % 4 || d->cout % 64) return false;
@@ -232,6 +239,7 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   // the fast epilogue addresses output / residual through 32-bit buffer offsets per batch
   const bool fast = !p.out_f32 && !p.accumulate && !p.out1 &&
                     (long long)p.D * p.H * p.W * p.cout * 2 < 0xFFFFE000LL;
+  if (sg_eligible(d)) return sg_launch(p, d, s);
   prof_begin(s);
   if (d->dtype == CWDM_BF16) {
     if (fast) {
@@ -299,7 +307,11 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     e.bias = nullptr; e.bias_bstride = 0; e.stats = nullptr;
     e.out = skip; e.out_dtype = d->dtype; e.out1 = nullptr; e.out_c0 = 0; e.accumulate = 0;
     e.workspace = nullptr; e.ws_bytes = 0;
-    if ((rc = legacy_conv3d_forward(&e, (cwdm_stream_t)s))) return rc;
+    if (sg_skip_eligible(&e)) {
+      if ((rc = sg_skip_launch(&e, skip, s))) return rc;
+    } else if ((rc = legacy_conv3d_forward(&e, (cwdm_stream_t)s))) {
+      return rc;
+    }
     res = skip; rmode = 0;
   }
   return v4_launch(d, a0, c0, a1, c1, a0_cm, res, rmode, v4_ksplit(d) > 1 ? ws : nullptr, s);

@@ -10,9 +10,11 @@ namespace {
 
 // One workgroup per (group, batch).  The group's (part, channel) items are
 // flattened so consecutive threads read consecutive channels of one part row
-// and every thread has up to 4 independent loads in flight: a small tensor
-// finishes in one load latency, a 128^3 one (4096 parts) in a few.
-constexpr int FIN_THREADS = 512;
+// and every thread has up to 8 independent loads in flight: a small tensor
+// finishes in one load latency, a 128^3 one (4096 parts x 2 channels per
+// group) in one round too.
+constexpr int FIN_THREADS = 1024;
+constexpr int FIN_LOADS = 8;
 
 __device__ __forceinline__ void fin_segment(const float2* __restrict__ base, long long parts, int cs, int lo, int w,
                                             double& s, double& q) {
@@ -20,15 +22,18 @@ __device__ __forceinline__ void fin_segment(const float2* __restrict__ base, lon
   // (32-bit item indices: parts * w is far below 2^32 for any grid the plan admits)
   const unsigned n = (unsigned)(parts * w), uw = (unsigned)w;
   unsigned i = threadIdx.x;
-  for (; i + 3 * FIN_THREADS < n; i += 4 * FIN_THREADS) {
-    float2 u[4];
+  for (; i + (FIN_LOADS - 1) * FIN_THREADS < n; i += FIN_LOADS * FIN_THREADS) {
+    float2 u[FIN_LOADS];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < FIN_LOADS; ++k) {
       const unsigned j = i + k * FIN_THREADS;
       u[k] = base[(long long)(j / uw) * cs + lo + (int)(j % uw)];
     }
-    s += ((double)u[0].x + (double)u[1].x) + ((double)u[2].x + (double)u[3].x);
-    q += ((double)u[0].y + (double)u[1].y) + ((double)u[2].y + (double)u[3].y);
+#pragma unroll
+    for (int k = 0; k < FIN_LOADS; ++k) {
+      s += (double)u[k].x;
+      q += (double)u[k].y;
+    }
   }
   for (; i < n; i += FIN_THREADS) {
     const float2 u = base[(long long)(i / uw) * cs + lo + (int)(i % uw)];

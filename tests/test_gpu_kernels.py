@@ -349,6 +349,28 @@ def test_conv3d_dma_kernel_vs_torch(case, dtype_name):
         L.cwdm_conv3d_set_path(prev)
 
 
+SG_CASES = [
+    # name, B, grid(out), c0, c1, cout, amode, gn, skip1x1, rmode  (bf16; W = 16, H % 4 == 0, D % 4 == 0,
+    # cout % 64 == 0, 32-channel K chunks: the small-grid kernel, conv3d_sg.hip, incl. its 1x1 skip mode;
+    # the W = 8 cases run the split-K brick kernels beside it)
+    ("sg16_gn_res", 1, (16, 16, 16), 64, 0, 64, 0, True, False, 0),
+    ("sg16_concat_skip", 2, (4, 8, 16), 48, 16, 128, 0, True, True, -1),
+    ("sg16_up_res", 1, (8, 4, 16), 32, 0, 64, 1, True, False, 1),
+    ("sg8_gn_concat_res", 1, (8, 8, 8), 96, 32, 64, 0, True, False, 0),
+    ("sg8_up_nogn", 2, (4, 8, 8), 32, 0, 128, 1, False, False, -1),
+    ("sg8_production", 1, (8, 8, 8), 256, 256, 256, 0, True, True, -1),
+    ("sg16_production_skip", 1, (16, 16, 16), 256, 256, 256, 0, True, True, -1),
+]
+
+
+@pytest.mark.parametrize("case", SG_CASES, ids=[c[0] for c in SG_CASES])
+def test_conv3d_small_grid_kernel_vs_torch(case):
+    """The small-grid kernel (16^3 / 8^3 levels: one statistics brick x 16 output
+    channels per workgroup, whole K, 16x16x32 MFMA) against F.conv3d, with the
+    per-brick GroupNorm partials."""
+    _run_conv_case(case, "bf16", True)
+
+
 @pytest.mark.parametrize("grid,B,cin", [((4, 4, 32), 1, 64), ((8, 8, 64), 2, 64), ((4, 8, 32), 1, 32)])
 def test_output_head_kernel_vs_torch(grid, B, cin):
     """The narrow-output head kernel (conv3d_head.hip: GN+SiLU fused, 16x16x32
