@@ -578,7 +578,7 @@ def main():
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_unit": "HBM bytes per step of those launches (2 x FETCH_SIZE + WRITE_SIZE, "
                                      f"{traffic_src})",
-                     "kernel": f"implicit-GEMM MFMA conv kernels (conv3d_v4 DMA-staged + brick + output head: "
+                     "kernel": f"implicit-GEMM MFMA conv kernels (conv3d_v4 DMA-staged, conv3d_sg small-grid, brick, output head: "
                                f"{n_conv} launches per step, {conv_ms:.2f} ms, {conv_flops / 1e12:.2f} TFLOP)"},
     }
     if cpu_state is not None:

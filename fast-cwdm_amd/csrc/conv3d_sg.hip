@@ -34,6 +34,7 @@
 //   * Epilogue: + bias, + residual (same grid / nearest-upsampled), bf16
 //     store, per-(brick, channel) (sum, sum^2) partials for the next
 //     GroupNorm.
+#include <algorithm>
 #include <atomic>
 #include <type_traits>
 
@@ -62,7 +63,18 @@ struct SGParams {
   V4Params v;   // shape / sources / weights / epilogue as for the wide kernel (ct counts 64-row tiles)
   int ntile16;  // output channel tiles of 16
   int parts;    // statistics bricks per batch
+  // K split (the 8^3 level: 32 tiles): slice ks runs chunks [ks kper, +kper); it
+  // stores its fp32 accumulators at part + (tile S + ks) 4096, and the slice
+  // that arrives last at the tile's counter sums all S in slice order (the
+  // result does not depend on the arrival order) and runs the epilogue
+  int ksplit, kper;
+  float* part;
 };
+
+// per-tile arrival counters of the K-split launches, zero between launches (the
+// last slice of a tile resets its counter).  One K-split small-grid launch at a
+// time per device: launches on one stream serialise.
+__device__ unsigned g_sg_count[1 << 16];
 
 __device__ __forceinline__ void sg_mfma(sg_f32x4& acc, const u32x4& a, const u32x4& b) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0,
@@ -84,12 +96,14 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   // work item -> (batch, brick, 16-channel tile); channel tile fastest (the 16
   // workgroups of a brick share its halo in L2)
   const int t16 = blockIdx.x % q.ntile16;
-  const int st = blockIdx.x / q.ntile16;
+  const int ks = (blockIdx.x / q.ntile16) % q.ksplit;
+  const int st = blockIdx.x / (q.ntile16 * q.ksplit);
   const int b = st / q.parts, brick = st - b * q.parts;
   const int tx = p.W / BX, ty = p.H / BY;
   const int x0 = (brick % tx) * BX, y0 = ((brick / tx) % ty) * BY, z0 = (brick / (tx * ty)) * 4;
   const int SH = MODE == 1 ? p.H >> 1 : p.H, SW = MODE == 1 ? p.W >> 1 : p.W;
   const int nch = p.nch / 2;  // 32-channel chunks
+  const int cb0 = ks * q.kper, cb1 = min(nch, cb0 + q.kper);  // this slice's chunks
 
   // halo DMA of 32-channel chunk c into buffer hbuf: pieces pc = wv + 4 j (44 in
   // all: quad plane pc / PCS, slot block pc % PCS); quads 0-1 / 2-3 are the two
@@ -155,19 +169,20 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
     float bi[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      bi[i] = p.bias ? p.bias[(long long)b * p.bias_bs + t16 * 16 + 4 * kq + i] : 0.f;
+      bi[i] = (p.bias && q.ksplit == 1) ? p.bias[(long long)b * p.bias_bs + t16 * 16 + 4 * kq + i] : 0.f;
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc[m] = sg_f32x4{bi[0], bi[1], bi[2], bi[3]};
   }
 
-  issue_halo(0, 0);
-  issue_w(0, 0);
+  issue_halo(cb0, 0);
+  issue_w(cb0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  for (int c = 0; c < nch; ++c) {
-    const bool has_next = c + 1 < nch;
-    const unsigned char* hb = smem + (c & 1) * C::BUF + hlane;
-    const unsigned char* wb = smem + 2 * C::BUF + (c & 1) * C::WBUF + lane * 16;
+  for (int c = cb0; c < cb1; ++c) {
+    const bool has_next = c + 1 < cb1;
+    const int buf = (c - cb0) & 1;
+    const unsigned char* hb = smem + buf * C::BUF + hlane;
+    const unsigned char* wb = smem + 2 * C::BUF + buf * C::WBUF + lane * 16;
     u32x4 av[2][C::NR], aw[2][3];
     auto read_group = [&](u32x4 (&a)[C::NR], u32x4 (&w)[3], int g) {
       const int dz = g / 3, dx = g % 3;
@@ -190,8 +205,8 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
     // the next chunk's halo and weights go to the other buffers (last read by
     // chunk c - 1, which every wave finished before the previous barrier)
     if (has_next) {
-      issue_halo(c + 1, (c + 1) & 1);
-      issue_w(c + 1, (c + 1) & 1);
+      issue_halo(c + 1, buf ^ 1);
+      issue_w(c + 1, buf ^ 1);
     }
     if constexpr (TAPS == 27) {
 #pragma unroll
@@ -213,6 +228,41 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
       // chunk's reads of the buffers the chunk after next will fill
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+    }
+  }
+
+  if (q.ksplit > 1) {
+    // K split: publish this slice, the tile's last arrival finishes it.  Hand-off
+    // across XCDs without fences (cdna_hip_programming.md, publish / consume
+    // recipe): the slice is stored write-through (sc1) and drained by every
+    // storing wave before the counter add; the finishing workgroup reads every
+    // slice with sc1 loads (past its stale L1 / L2 lines).
+    const int tile = st * q.ntile16 + t16;
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        q.part + (long long)tile * q.ksplit * 4096, (short)0, q.ksplit * 4096 * 4, 0x00020000);
+    const unsigned lofs = (unsigned)(wv * 4 * 64 + lane) * 16u;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[m]), prs,
+                                             (unsigned)ks * 16384u + lofs + (unsigned)m * 1024u, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* flag = reinterpret_cast<unsigned*>(smem);
+    if (tid == 0)
+      *flag = __hip_atomic_fetch_add(&g_sg_count[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag != (unsigned)(q.ksplit - 1)) return;
+    if (tid == 0) __hip_atomic_store(&g_sg_count[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float bi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bi[i] = p.bias ? p.bias[(long long)b * p.bias_bs + t16 * 16 + 4 * kq + i] : 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      sg_f32x4 sum = __builtin_bit_cast(sg_f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, lofs + m * 1024u, 0, 16));
+      for (int k = 1; k < q.ksplit; ++k)
+        sum += __builtin_bit_cast(sg_f32x4,
+                                  __builtin_amdgcn_raw_buffer_load_b128(prs, (unsigned)k * 16384u + lofs + m * 1024u, 0, 16));
+      acc[m] = sum + sg_f32x4{bi[0], bi[1], bi[2], bi[3]};
     }
   }
 
@@ -289,6 +339,9 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
 template __global__ void conv3d_sg_kernel<16, 4, 0, 27>(SGParams);
 template __global__ void conv3d_sg_kernel<16, 4, 1, 27>(SGParams);
 template __global__ void conv3d_sg_kernel<16, 4, 0, 1>(SGParams);
+template __global__ void conv3d_sg_kernel<8, 8, 0, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<8, 8, 1, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<8, 8, 0, 1>(SGParams);
 
 extern std::atomic<int> g_conv_path;
 
@@ -296,14 +349,15 @@ namespace {
 bool sg_shape_ok(const cwdm_conv3d_desc* d) {
   if (g_conv_path.load(std::memory_order_relaxed) == 1) return false;
   if (d->dtype != CWDM_BF16 || d->out_dtype != CWDM_BF16 || d->accumulate || d->out1 || d->cout % 64) return false;
-  return d->W == 16 && d->H % 4 == 0 && d->D % 4 == 0;
+  return (d->W == 16 && d->H % 4 == 0 && d->D % 4 == 0) || (d->W == 8 && d->H % 8 == 0 && d->D % 4 == 0);
 }
 }  // namespace
 
 // shapes the small-grid kernel takes: bf16, plain bf16 output (no fp32 / dual /
 // accumulating output), same-grid or upsampled source and residual, W = 16
-// (the 16x4x4 statistics bricks), 32-channel K chunks.  (At 8^3 there are only
-// 32 work items of this shape: measured slower than the split-K bricks.)
+// (16x4x4 statistics bricks) or W = 8 (8x8x4), 32-channel K chunks.  At 8^3
+// there are only 32 tiles: K split across workgroups (sg_ksplit), finished by
+// the last slice of each tile.
 bool sg_eligible(const cwdm_conv3d_desc* d) {
   if (!sg_shape_ok(d) || !d->a_w) return false;
   if (d->a_mode != 0 && d->a_mode != 1) return false;
@@ -322,29 +376,62 @@ bool sg_skip_eligible(const cwdm_conv3d_desc* d) {
   return V * (d->b_c0 + d->b_c1) * 2 < 0xFFFFE000LL && d->B * (V / 256) * (d->cout / 16) < (1LL << 31);
 }
 
+// K slices of a launch: enough work items for the chip (~256), at least one
+// 32-channel chunk per slice (the 16^3 level has 256 tiles: no split)
+namespace {
+int sg_split_for(const cwdm_conv3d_desc* d, int cin) {
+  const int64_t parts = d->W == 16 ? (d->D / 4) * (d->H / 4) : (d->D / 4) * (d->H / 8);
+  const int64_t tiles = d->B * parts * (d->cout / 16);
+  const int nch = cin / 32;
+  if (tiles >= 256 || nch < 2) return 1;
+  int S = (int)std::min<int64_t>((256 + tiles - 1) / tiles, nch);
+  const int per = (nch + S - 1) / S;
+  S = (nch + per - 1) / per;
+  return (tiles * S < (1 << 16) && S > 1) ? S : 1;
+}
+}  // namespace
+
+int sg_ksplit(const cwdm_conv3d_desc* d) { return sg_eligible(d) ? sg_split_for(d, d->a_c0 + d->a_c1) : 1; }
+int sg_skip_ksplit(const cwdm_conv3d_desc* d) { return sg_skip_eligible(d) ? sg_split_for(d, d->b_c0 + d->b_c1) : 1; }
+
 namespace {
 int sg_go(const SGParams& q, const cwdm_conv3d_desc* d, int taps, double flops, hipStream_t s) {
-  const dim3 grid((unsigned)(d->B * q.parts * q.ntile16));
+  const dim3 grid((unsigned)(d->B * q.parts * q.ntile16 * q.ksplit));
   prof_begin(s);
-  if (taps == 1) hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 0, 1>), grid, dim3(256), 0, s, q);
-  else if (q.v.amode == 1) hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 1, 27>), grid, dim3(256), 0, s, q);
-  else hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 0, 27>), grid, dim3(256), 0, s, q);
+  if (d->W == 8 && taps == 1) {
+    hipLaunchKernelGGL((conv3d_sg_kernel<8, 8, 0, 1>), grid, dim3(256), 0, s, q);
+  } else if (d->W == 8) {
+    if (q.v.amode == 1) hipLaunchKernelGGL((conv3d_sg_kernel<8, 8, 1, 27>), grid, dim3(256), 0, s, q);
+    else hipLaunchKernelGGL((conv3d_sg_kernel<8, 8, 0, 27>), grid, dim3(256), 0, s, q);
+  } else if (taps == 1) {
+    hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 0, 1>), grid, dim3(256), 0, s, q);
+  } else if (q.v.amode == 1) {
+    hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 1, 27>), grid, dim3(256), 0, s, q);
+  } else {
+    hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 0, 27>), grid, dim3(256), 0, s, q);
+  }
   prof_end(s, flops);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }
 }  // namespace
 
-int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, hipStream_t s) {
+// partial: fp32 scratch of sg_ksplit(d) x B x V x cout (the K-split slices), else unused
+int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, void* partial, hipStream_t s) {
   SGParams q{};
   q.v = v;
   q.ntile16 = d->cout / 16;
-  q.parts = (int)((d->D / 4) * (d->H / 4));
+  q.parts = (int)(d->W == 16 ? (d->D / 4) * (d->H / 4) : (d->D / 4) * (d->H / 8));
+  q.ksplit = sg_ksplit(d);
+  q.kper = ((d->a_c0 + d->a_c1) / 32 + q.ksplit - 1) / q.ksplit;
+  q.part = reinterpret_cast<float*>(partial);
+  CWDM_REQUIRE(q.ksplit == 1 || partial, CWDM_E_INVALID, "conv3d (small grid): K-split scratch missing");
   return sg_go(q, d, 27, 2.0 * d->B * d->D * d->H * d->W * (double)d->cout * 27.0 * (d->a_c0 + d->a_c1), s);
 }
 
-// out = W_skip . [b0 | b1] (bf16, no bias / residual / statistics): the skip pre-pass of conv3d_v4_forward
-int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, hipStream_t s) {
+// out = W_skip . [b0 | b1] (bf16, no bias / residual / statistics): the skip
+// pre-pass of conv3d_v4_forward; partial: fp32 scratch of sg_skip_ksplit(d) x B x V x cout
+int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, void* partial, hipStream_t s) {
   SGParams q{};
   V4Params& p = q.v;
   const int64_t V = d->D * d->H * d->W;
@@ -359,7 +446,11 @@ int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, hipStream_t s) {
   p.bias = nullptr; p.res = nullptr; p.rmode = -1;
   p.out = out; p.stats = nullptr;
   q.ntile16 = d->cout / 16;
-  q.parts = (int)((d->D / 4) * (d->H / 4));
+  q.parts = (int)(d->W == 16 ? (d->D / 4) * (d->H / 4) : (d->D / 4) * (d->H / 8));
+  q.ksplit = sg_skip_ksplit(d);
+  q.kper = ((d->b_c0 + d->b_c1) / 32 + q.ksplit - 1) / q.ksplit;
+  q.part = reinterpret_cast<float*>(partial);
+  CWDM_REQUIRE(q.ksplit == 1 || partial, CWDM_E_INVALID, "conv3d (small grid): K-split scratch missing");
   return sg_go(q, d, 1, 2.0 * d->B * V * (double)d->cout * (d->b_c0 + d->b_c1), s);
 }
 

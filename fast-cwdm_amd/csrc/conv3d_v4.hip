@@ -101,8 +101,10 @@ std::atomic<unsigned long long*> g_stamps{nullptr};
 
 bool sg_eligible(const cwdm_conv3d_desc* d);
 bool sg_skip_eligible(const cwdm_conv3d_desc* d);
-int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, hipStream_t s);
-int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, hipStream_t s);
+int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, void* partial, hipStream_t s);
+int sg_ksplit(const cwdm_conv3d_desc* d);
+int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, void* partial, hipStream_t s);
+int sg_skip_ksplit(const cwdm_conv3d_desc* d);
 
 int64_t v4_items(const cwdm_conv3d_desc* d) {
   return d->B * ((d->W + 31) / 32) * (d->H / 4) * (d->D / 4) * (d->cout / 64);
@@ -120,7 +122,7 @@ int64_t v4_ksplit_target() {
 // K split of a grid with fewer tiles than two workgroups per CU (the 32^3
 // level): enough K slices for ~512 work items, at least two chunks per slice
 int v4_ksplit(const cwdm_conv3d_desc* d) {
-  if (sg_eligible(d)) return 1;  // the small-grid kernel runs the whole K per work item
+  if (sg_eligible(d)) return sg_ksplit(d);  // the small-grid kernel's own K split (8^3 level)
   const int ck = d->dtype == CWDM_BF16 ? 16 : 8;
   const int nch = (d->a_c0 + d->a_c1) / ck;
   const int64_t nblk = v4_items(d);
@@ -157,7 +159,13 @@ int64_t v4_workspace_bytes(const cwdm_conv3d_desc* d) {
   int64_t ws = 0;
   if (d->a_gn) ws += align256(d->B * src_voxels(d) * (d->a_c0 + d->a_c1) * esz);
   if (d->b_w) ws += align256(d->B * d->D * d->H * d->W * d->cout * esz);
-  const int S = v4_ksplit(d);
+  // K-split slices of the conv, or of its 1x1 skip pre-pass (which runs first: one region serves both)
+  int S = v4_ksplit(d);
+  if (d->b_w) {
+    cwdm_conv3d_desc e = *d;
+    e.a_w = nullptr;
+    S = std::max(S, sg_skip_ksplit(&e));
+  }
   if (S > 1) ws += align256(S * d->B * d->D * d->H * d->W * d->cout * 4);
   return ws;
 }
@@ -210,6 +218,7 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   p.out1 = d->out1; p.out_c0 = d->out_c0;
   p.accumulate = d->accumulate;
   p.stamps = g_stamps.load(std::memory_order_relaxed);
+  if (sg_eligible(d)) return sg_launch(p, d, partial, s);
   const int S = v4_ksplit(d);
   p.ksplit = S;
   p.kper = (p.nch + S - 1) / S;
@@ -239,7 +248,6 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   // the fast epilogue addresses output / residual through 32-bit buffer offsets per batch
   const bool fast = !p.out_f32 && !p.accumulate && !p.out1 &&
                     (long long)p.D * p.H * p.W * p.cout * 2 < 0xFFFFE000LL;
-  if (sg_eligible(d)) return sg_launch(p, d, s);
   prof_begin(s);
   if (d->dtype == CWDM_BF16) {
     if (fast) {
@@ -308,7 +316,7 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     e.out = skip; e.out_dtype = d->dtype; e.out1 = nullptr; e.out_c0 = 0; e.accumulate = 0;
     e.workspace = nullptr; e.ws_bytes = 0;
     if (sg_skip_eligible(&e)) {
-      if ((rc = sg_skip_launch(&e, skip, s))) return rc;
+      if ((rc = sg_skip_launch(&e, skip, ws, s))) return rc;   // ws: the K-split region, free until the conv
     } else if ((rc = legacy_conv3d_forward(&e, (cwdm_stream_t)s))) {
       return rc;
     }

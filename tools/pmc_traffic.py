@@ -17,7 +17,7 @@ import glob
 import json
 import sys
 
-CONV_FAMILY = ("conv3d_v4_kernel", "conv3d_kernel", "conv3d_wide_kernel", "conv3d_reduce_kernel",
+CONV_FAMILY = ("conv3d_v4_kernel", "conv3d_sg_kernel", "conv3d_kernel", "conv3d_wide_kernel", "conv3d_reduce_kernel",
                "splitk_sum_kernel", "gn_apply_kernel", "gn_apply_skip_kernel", "head_conv_kernel")
 
 
@@ -58,7 +58,7 @@ def main():
         e[0] += 1
         e[1] += rb
         e[2] += wb
-    mfma = ("conv3d_v4_kernel", "conv3d_kernel", "conv3d_wide_kernel", "head_conv_kernel")
+    mfma = ("conv3d_v4_kernel", "conv3d_sg_kernel", "conv3d_kernel", "conv3d_wide_kernel", "head_conv_kernel")
     mk = {k: v for k, v in per.items() if k in mfma}
     res = {"scope": "conv family of one 128^3 bf16 denoising step (bench.py)", "launches": n,
            "mfma_conv_kernels": {"kernels": sorted(mk), "launches": sum(v[0] for v in mk.values()),
