@@ -12,6 +12,8 @@
 namespace cwdm {
 
 template __global__ void conv3d_v4_kernel<bf16_t, 0, true>(V4Params);
+template __global__ void conv3d_v4_kernel<bf16_t, 0, true, true>(V4Params);
+template __global__ void conv3d_v4_kernel<bf16_t, 1, true, true>(V4Params);
 template __global__ void conv3d_v4_kernel<bf16_t, 1, true>(V4Params);
 template __global__ void conv3d_v4_kernel<bf16_t, 0, false>(V4Params);
 template __global__ void conv3d_v4_kernel<bf16_t, 1, false>(V4Params);
@@ -228,6 +230,13 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
     p.bias = nullptr; p.res = nullptr; p.rmode = -1; p.stats = nullptr;
     p.out = partial; p.out_f32 = 1; p.out1 = nullptr; p.out_c0 = 0; p.accumulate = 0;
   }
+  // fewer 64-channel tiles than CUs (the 32^3 level): 32-channel tiles, one
+  // z-plane per wave (twice the work items; the statistics bricks are the same)
+  static const bool ct32_on = [] { const char* e = std::getenv("CWDM_V4_CT32"); return !(e && e[0] == '0'); }();
+  const bool ct32 = ct32_on && d->dtype == CWDM_BF16 && S == 1 && !p.out_f32 && !p.accumulate && !p.out1 &&
+                    (long long)p.B * p.tx * p.ty * p.tz * p.nct < 256 &&
+                    (long long)p.D * p.H * p.W * p.cout * 2 < 0xFFFFE000LL;
+  if (ct32) p.nct = d->cout / 32;
   const long long nblk = (long long)p.B * p.tx * p.ty * p.tz * p.nct * S;
   p.nblk = (int)nblk;
   // persistent: two workgroups per CU (80 KB LDS, <= 256 registers per lane each)
@@ -249,7 +258,10 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   const bool fast = !p.out_f32 && !p.accumulate && !p.out1 &&
                     (long long)p.D * p.H * p.W * p.cout * 2 < 0xFFFFE000LL;
   prof_begin(s);
-  if (d->dtype == CWDM_BF16) {
+  if (ct32) {
+    if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 1, true, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 0, true, true>), grid, dim3(256), 0, s, p);
+  } else if (d->dtype == CWDM_BF16) {
     if (fast) {
       if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 1, true>), grid, dim3(256), 0, s, p);
       else hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 0, true>), grid, dim3(256), 0, s, p);

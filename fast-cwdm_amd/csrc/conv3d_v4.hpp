@@ -134,11 +134,17 @@ __device__ __forceinline__ void v4_read_step(u32x4 (&av)[6], const unsigned char
 // store (or accumulate), per-channel (sum, sum^2) partials for the next
 // GroupNorm.  R: 4 x 256 B of LDS (one slice per wave) for the cross-wave
 // statistics; every wave of the workgroup calls this.
-template <typename T, bool FAST>
+// CT32: 32-channel tiles (ct counts 32-channel tiles; wave wv = z-plane wv, one
+// plane per wave); else 64-channel tiles, wave = (32-channel half wv & 1, plane
+// pair wv >> 1)
+template <typename T, bool FAST, bool CT32 = false>
 __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][4], int b, int sl, int ct, int x0,
                                             int y0, int z0, int ks, int tid, int wv, unsigned char* smem) {
-  const int lane = tid & 63, lr = lane & 31, hh = lane >> 5, f = wv & 1, vg = wv >> 1;
-  const int cbase = ct * 64 + f * 32 + 4 * hh;
+  constexpr int NPL = CT32 ? 1 : 2;
+  const int lane = tid & 63, lr = lane & 31, hh = lane >> 5;
+  const int zb = CT32 ? wv : 2 * (wv >> 1);                    // the wave's first z-plane in the tile
+  const int c0w = CT32 ? ct * 32 : ct * 64 + (wv & 1) * 32;    // the wave's first output channel
+  const int cbase = c0w + 4 * hh;
   float ssum[16], ssq[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { ssum[i] = 0.f; ssq[i] = 0.f; }
@@ -147,7 +153,7 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
   const float xm = xin ? 1.f : 0.f;   // and add nothing to the statistics
   const long long HW = (long long)p.H * p.W;
   // voxel of (plane pl, line m) = vox0 + pl * HW + m * W
-  const long long vox0 = (((long long)b * p.D + z0 + 2 * vg) * p.H + y0) * p.W + ox;
+  const long long vox0 = (((long long)b * p.D + z0 + zb) * p.H + y0) * p.W + ox;
   if constexpr (FAST) {
     // bf16 fast path: 16-byte residual loads and stores.  A lane pair (l, l+32)
     // holds channels 8j..8j+7 of one voxel split 4 / 4; v_permlane32_swap turns
@@ -158,11 +164,11 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
     // variants are separate straight-line code: with branches inside, the
     // waitcnt pass fell back to vmcnt(0) after every store (measured: the
     // residual epilogue serialised its 16 stores).
-    const int cl = ct * 64 + f * 32 + 8 * hh;   // this lane's first channel (jj = 0)
+    const int cl = c0w + 8 * hh;   // this lane's first channel (jj = 0)
     const long long V = (long long)p.D * HW;
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<bf16_t*>(p.out) + (long long)b * V * p.cout, (short)0, (int)(V * p.cout * 2), 0x00020000);
-    const unsigned vb0 = (unsigned)((((z0 + 2 * vg) * p.H) + y0) * p.W + ox);  // (plane 0, line 0) in the batch
+    const unsigned vb0 = (unsigned)((((z0 + zb) * p.H) + y0) * p.W + ox);  // (plane 0, line 0) in the batch
     const unsigned rowb = (unsigned)p.W * (unsigned)p.cout * 2u, planeb = (unsigned)HW * (unsigned)p.cout * 2u;
     const unsigned obase = vb0 * (unsigned)p.cout * 2u + (unsigned)cl * 2u;
     auto run = [&](auto res_c) {
@@ -174,12 +180,12 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
             (void*)(reinterpret_cast<const bf16_t*>(p.res) + (long long)b * rV * p.cout), (short)0,
             (int)(rV * p.cout * 2), 0x00020000);
 #pragma unroll
-        for (int pl = 0; pl < 2; ++pl)
+        for (int pl = 0; pl < NPL; ++pl)
 #pragma unroll
           for (int m = 0; m < 4; ++m) {
             unsigned r0 = obase + (unsigned)pl * planeb + (unsigned)m * rowb;
             if (p.rmode == 1) {
-              const int oy = y0 + m, oz = z0 + 2 * vg + pl;
+              const int oy = y0 + m, oz = z0 + zb + pl;
               const unsigned rvb = (unsigned)(((oz >> 1) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1));
               r0 = rvb * (unsigned)p.cout * 2u + (unsigned)cl * 2u;
             }
@@ -192,7 +198,7 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
-      for (int pl = 0; pl < 2; ++pl) {
+      for (int pl = 0; pl < NPL; ++pl) {
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const unsigned oo = obase + (unsigned)pl * planeb + (unsigned)m * rowb;
@@ -232,11 +238,11 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
     else run(std::false_type{});
   } else {
 #pragma unroll
-    for (int pl = 0; pl < 2; ++pl) {
+    for (int pl = 0; pl < NPL; ++pl) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         if (!xin) continue;
-        const int oy = y0 + m, oz = z0 + 2 * vg + pl;
+        const int oy = y0 + m, oz = z0 + zb + pl;
         const long long vox = vox0 + pl * HW + (long long)m * p.W;
         long long rvox = vox;
         if (p.rmode == 1)
@@ -315,16 +321,29 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
     // (__syncthreads' fence would drain them: vmcnt(0))
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (tid < 64) {
+    if (CT32 ? tid < 32 : tid < 64) {
       const int ff = tid >> 5, c32 = tid & 31, j = c32 >> 3, h2 = (c32 >> 2) & 1, k = c32 & 3;
       const int i = 4 * j + k;
-      const float* R0 = reinterpret_cast<const float*>(smem + V4Cfg::pad(ff)) + h2 * 32;       // vg 0
-      const float* R1 = reinterpret_cast<const float*>(smem + V4Cfg::pad(ff + 2)) + h2 * 32;   // vg 1
       const int tiles = p.tx * p.ty * p.tz;
-      const int c = ct * 64 + tid;
+      float su, sq;
+      if constexpr (CT32) {  // the 4 plane waves hold the same 32 channels
+        su = 0.f; sq = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float* Rw = reinterpret_cast<const float*>(smem + V4Cfg::pad(w)) + h2 * 32;
+          su += Rw[i];
+          sq += Rw[16 + i];
+        }
+      } else {
+        const float* R0 = reinterpret_cast<const float*>(smem + V4Cfg::pad(ff)) + h2 * 32;       // vg 0
+        const float* R1 = reinterpret_cast<const float*>(smem + V4Cfg::pad(ff + 2)) + h2 * 32;   // vg 1
+        su = R0[i] + R1[i];
+        sq = R0[16 + i] + R1[16 + i];
+      }
+      const int c = (CT32 ? ct * 32 : ct * 64) + tid;
       const long long pidx = ((long long)b * tiles + sl) * p.cout + c;
-      p.stats[pidx * 2 + 0] = R0[i] + R1[i];
-      p.stats[pidx * 2 + 1] = R0[16 + i] + R1[16 + i];
+      p.stats[pidx * 2 + 0] = su;
+      p.stats[pidx * 2 + 1] = sq;
     }
   }
 }
@@ -413,7 +432,7 @@ __device__ __forceinline__ void v4_issue_halo(const V4Params& p, const V4Tile& t
 // Persistent: gridDim.x <= the number of tiles; workgroup k runs tiles
 // k, k + gridDim.x, ... as one continuous chunk stream, so the next tile's halo,
 // weights and bias are prefetched under the current tile's last chunk.
-template <typename T, int MODE, bool FAST>
+template <typename T, int MODE, bool FAST, bool CT32 = false>
 __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   static_assert(!FAST || sizeof(T) == 2, "the fast epilogue is bf16 only");
   using C = V4Cfg;
@@ -422,6 +441,10 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, hh = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int f = wv & 1, vg = wv >> 1;
+  // CT32: one z-plane per wave, the tile's 32 channels (the 64-row weight tile
+  // ct >> 1, rows 32 (ct & 1) + lr); else planes 2 vg, 2 vg + 1 and channels f 32 + lr
+  constexpr int NPL = CT32 ? 1 : 2;
+  const int zb = CT32 ? wv : 2 * vg;
   V4_STAMP(0);
 #ifdef CWDM_CONV_STAMPS
   if (p.stamps && tid == 0) p.stamps[(long long)blockIdx.x * 24 + 20] = __builtin_amdgcn_s_memrealtime();
@@ -460,29 +483,33 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   };
   // weight fragments of group g of chunk c, channel tile ct: the 3 dy taps, this
   // lane's row (output channel) lr of the wave's 32-channel slice, quad hh
-  const unsigned char* wlane = p.aw + f * 1024 + lr * 32 + ((hh ^ ((lr >> 3) & 1)) << 4);
+  const unsigned char* wlane = p.aw + (CT32 ? 0 : f * 1024) + lr * 32 + ((hh ^ ((lr >> 3) & 1)) << 4);
+  auto wtile = [&](int ct, int c) {  // this lane's weights of chunk c, channel tile ct
+    return CT32 ? wlane + (ct & 1) * 1024 + ((long long)(ct >> 1) * p.nch + c) * 27 * 2048
+                : wlane + ((long long)ct * p.nch + c) * 27 * 2048;
+  };
   auto load_w = [&](u32x4 (&w)[3], int ct, int c, int g) {
-    const unsigned char* src = wlane + (((long long)ct * p.nch + c) * 27 + (g / 3) * 9 + (g % 3)) * 2048;
+    const unsigned char* src = wtile(ct, c) + ((g / 3) * 9 + (g % 3)) * 2048;
     v4_gload(w[0], src);
     v4_gload(w[1], src + 3 * 2048);
     v4_gload(w[2], src + 6 * 2048);
   };
   // the 64 bias values of a tile into this wave's LDS padding slice (one 4-byte DMA per lane)
   auto issue_bias = [&](const Tile& tt) {
-    if (p.bias && wv == 0)
+    if (p.bias && wv == 0 && (!CT32 || lane < 32))
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(
-                                           p.bias + (long long)tt.b * p.bias_bs + tt.ct * 64 + lane),
+                                           p.bias + (long long)tt.b * p.bias_bs + tt.ct * (CT32 ? 32 : 64) + lane),
                                        (__attribute__((address_space(3))) void*)(smem + C::pad(0) + 256), 4, 0, 0);
   };
   // accumulators start at the bias of their output channel (i = 4 j + k -> channel 8 j + 4 hh + k)
   f32x16 acc[2][4];
   auto init_acc = [&](int ks) {
     float bia[16];
-    const float* bl = reinterpret_cast<const float*>(smem + C::pad(0) + 256) + f * 32 + 4 * hh;
+    const float* bl = reinterpret_cast<const float*>(smem + C::pad(0) + 256) + (CT32 ? 0 : f * 32) + 4 * hh;
 #pragma unroll
     for (int i = 0; i < 16; ++i) bia[i] = (p.bias && ks == 0) ? bl[8 * (i >> 2) + (i & 3)] : 0.f;
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < NPL; ++a)
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -490,12 +517,12 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   };
 
   // lane read base: halo voxel (z = 2 vg, line 0, x = lr) of quad plane hh
-  const int hlane = hh * (C::HVP * 16) + ((2 * vg) * (C::HX * C::HY) + lr) * 16;
+  const int hlane = hh * (C::HVP * 16) + (zb * (C::HX * C::HY) + lr) * 16;
 
   // a tile's first weight group: ordinary (compiler-tracked) loads, issued
   // before the previous tile's epilogue so their latency hides under it
   auto load_w0 = [&](u32x4 (&w)[3], int ct, int c) {
-    const unsigned char* src = wlane + ((long long)ct * p.nch + c) * 27 * 2048;
+    const unsigned char* src = wtile(ct, c);
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) w[dy] = *reinterpret_cast<const u32x4*>(src + dy * 3 * 2048);
   };
@@ -525,8 +552,10 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
       u32x4 av[2][6];
       v4_read_step<0>(av[0], hb);
 #define V4_STEP(K)                                                                                            \
-      {                                                                                                       \
+      if constexpr (!CT32 || (K) % 2 == 0) {                                                                  \
         constexpr int GI = (K) / 2, PL = (K) % 2;                                                             \
+        constexpr int KN = CT32 ? (K) + 2 : (K) + 1;       /* next step */                                    \
+        constexpr int BC = CT32 ? ((K) / 2) & 1 : (K) & 1; /* its operand buffer; next: BC ^ 1 */             \
         if (PL == 0) {                                                                                        \
           /* weights of group GI + 1: this chunk or the next.  Nothing past the tile's last */                \
           /* group: a load nobody waits for would land in registers the epilogue reuses */                    \
@@ -534,7 +563,7 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
           else if (!LAST) load_w(wr[(GI + 1) % 3], cur.ct, c + 1, 0);                                         \
           if (GI == 1 && has_next) issue_halo(cur, c + 1, (gch + 1) & 1);                                     \
         }                                                                                                     \
-        if ((K) < 17) v4_read_step<((K) + 1) % 18>(av[((K) + 1) & 1], hb);                                    \
+        if (KN < 18) v4_read_step<KN % 18>(av[BC ^ 1], hb);                                                   \
         /* W(G) is retired with the younger weight group (and at group 2 the next */                          \
         /* chunk's halo pieces) still in flight; W(0) landed before the chunk */                              \
         if (PL == 0 && GI == 1) { if (has_next) V4_WAIT_W(13, wr[1]); else V4_WAIT_W(3, wr[1]); }             \
@@ -544,7 +573,7 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
         __builtin_amdgcn_sched_barrier(0);                                                                    \
         _Pragma("unroll") for (int dy = 0; dy < 3; ++dy)                                                      \
         _Pragma("unroll") for (int m = 0; m < 4; ++m)                                                         \
-          v4_mfma<T>(acc[PL][m], wr[GI % 3][dy], av[(K) & 1][m + dy]);                                        \
+          v4_mfma<T>(acc[PL][m], wr[GI % 3][dy], av[BC][m + dy]);                                             \
         __builtin_amdgcn_sched_barrier(0);                                                                    \
       }
       V4_STEP(0) V4_STEP(1) V4_STEP(2) V4_STEP(3) V4_STEP(4) V4_STEP(5)
@@ -576,7 +605,7 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
       load_w0(wr[0], nxt.ct, nxt.c0);
     }
     // (K split: out is this slice's fp32 partial, see V4Params)
-    v4_epilogue<T, FAST>(p, acc, cur.b, cur.sl, cur.ct, cur.x0, cur.y0, cur.z0, cur.ks, tid, wv, smem);
+    v4_epilogue<T, FAST, CT32>(p, acc, cur.b, cur.sl, cur.ct, cur.x0, cur.y0, cur.z0, cur.ks, tid, wv, smem);
     if (it == 0) V4_STAMP(13);
     cur = nxt;
   }
