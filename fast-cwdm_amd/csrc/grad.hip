@@ -214,38 +214,68 @@ __global__ void __launch_bounds__(512) gn_bwd_finalize_kernel(const float* __res
   }
 }
 
+template <typename T> __device__ __forceinline__ float stored(float v) {
+  if constexpr (sizeof(T) == 2) return bf2f(f2bf(v));
+  else return v;
+}
+
+// Grid-stride over the (voxel, 8-channel group) items of batch blockIdx.y.
+// chs (optional): per-channel sums of the written dx (the value as stored),
+// atomically added to chs[b * chs_stride + c] -- the emb-projection gradient of
+// the block's conv1 output (sum over voxels of d h1) without a second read of
+// dx.  The stride gridDim.x * 256 is then a multiple of C / 8 (host-checked), so
+// every thread keeps one channel group.
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__ x0, int c0, const T* __restrict__ x1,
                                                           int c1, const T* __restrict__ du,
                                                           const float* __restrict__ ss,
                                                           const float* __restrict__ coef, int d, int h, int w,
                                                           T* __restrict__ dx0, int acc0, T* __restrict__ dx1,
-                                                          int acc1) {
+                                                          int acc1, float* __restrict__ chs, long long chs_stride) {
   const int C = c0 + c1, ncg = C >> 3;
   const long long V = (long long)d * h * w;
   const int b = blockIdx.y;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= V * ncg) return;
-  const int cg = (int)(i % ncg);
-  const long long v = i / ncg;
-  const int c = cg * 8;
-  const bool first = c < c0;
-  const T* xs = first ? x0 : x1;
-  T* dx = first ? dx0 : dx1;
-  const int xc = first ? c0 : c1, xo = first ? c : c - c0;
-  const int acc = first ? acc0 : acc1;
-  float xv[8], g[8], o[8];
-  load8<T>(xs + ((long long)b * V + v) * xc + xo, xv);
-  load_du<T, MODE>(du, C, c, b, (unsigned)v, d, h, w, g);
-  if (acc) load8<T>(dx + ((long long)b * V + v) * xc + xo, o);
+  const long long n = V * ncg, step = (long long)gridDim.x * 256;
+  float sum[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const long long bc = (long long)b * C + c + e;
-    const float dz = dsilu(xv[e] * ss[bc * 2] + ss[bc * 2 + 1], g[e]);
-    const float r = coef[bc * 4] * dz + coef[bc * 4 + 1] * xv[e] + coef[bc * 4 + 2];
-    o[e] = acc ? o[e] + r : r;
+  for (int e = 0; e < 8; ++e) sum[e] = 0.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += step) {
+    const int cg = (int)(i % ncg);
+    const long long v = i / ncg;
+    const int c = cg * 8;
+    const bool first = c < c0;
+    const T* xs = first ? x0 : x1;
+    T* dx = first ? dx0 : dx1;
+    const int xc = first ? c0 : c1, xo = first ? c : c - c0;
+    const int acc = first ? acc0 : acc1;
+    float xv[8], g[8], o[8];
+    load8<T>(xs + ((long long)b * V + v) * xc + xo, xv);
+    load_du<T, MODE>(du, C, c, b, (unsigned)v, d, h, w, g);
+    if (acc) load8<T>(dx + ((long long)b * V + v) * xc + xo, o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const long long bc = (long long)b * C + c + e;
+      const float dz = dsilu(xv[e] * ss[bc * 2] + ss[bc * 2 + 1], g[e]);
+      const float r = coef[bc * 4] * dz + coef[bc * 4 + 1] * xv[e] + coef[bc * 4 + 2];
+      o[e] = acc ? o[e] + r : r;
+    }
+    store8<T>(dx + ((long long)b * V + v) * xc + xo, o);
+    if (chs) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum[e] += stored<T>(o[e]);
+    }
   }
-  store8<T>(dx + ((long long)b * V + v) * xc + xo, o);
+  if (!chs) return;
+  __shared__ float red[256 * 8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = sum[e];
+  __syncthreads();
+  const int nslots = 256 / ncg;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int k = 0; k < nslots; ++k) s += red[(k * ncg + (c >> 3)) * 8 + (c & 7)];
+    atomicAdd(chs + (long long)b * chs_stride + c, s);
+  }
 }
 
 template <typename T, int MODE>
@@ -467,6 +497,10 @@ int launch_temb_bwd(const float* t, int B, int mc, const float* w1, const float*
   return CWDM_OK;
 }
 
+int gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode, const float* ss,
+                     const float* mr, const float* gamma, int groups, int64_t B, int64_t d, int64_t h, int64_t w,
+                     int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma, float* dbeta, void* ws,
+                     int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream);
 }  // namespace cwdm
 
 using namespace cwdm;
@@ -478,10 +512,16 @@ extern "C" int64_t cwdm_gn_silu_bwd_workspace_bytes(int C, int64_t B, int64_t d,
   return (part + 255) / 256 * 256 + B * (int64_t)C * 4 * 4;
 }
 
-extern "C" int cwdm_gn_silu_bwd(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode,
-                                const float* ss, const float* mr, const float* gamma, int groups, int64_t B,
-                                int64_t d, int64_t h, int64_t w, int dtype, void* dx0, int acc0, void* dx1, int acc1,
-                                float* dgamma, float* dbeta, void* ws, int64_t ws_bytes, cwdm_stream_t stream) {
+// cwdm_gn_silu_bwd, plus (chs != nullptr, single source, C / 8 dividing 256)
+// the per-channel sums of dx0 added to chs[b * chs_stride + c] (unet_plan.cpp:
+// the conv1-output sums of the emb-projection backward).
+int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode,
+                           const float* ss, const float* mr, const float* gamma, int groups, int64_t B, int64_t d,
+                           int64_t h, int64_t w, int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma,
+                           float* dbeta, void* ws, int64_t ws_bytes, float* chs, int64_t chs_stride,
+                           cwdm_stream_t stream) {
+  CWDM_REQUIRE(!chs || (c1 == 0 && 256 % (c0 / 8) == 0 && chs_stride >= c0), CWDM_E_UNSUPPORTED,
+               "gn_silu_bwd: fused channel sums need one source with C / 8 dividing 256");
   CWDM_REQUIRE(x0 && du && ss && mr && gamma && dx0 && dgamma && dbeta && ws, CWDM_E_INVALID,
                "cwdm_gn_silu_bwd: null pointer");
   CWDM_REQUIRE(c1 == 0 || (x1 && dx1), CWDM_E_INVALID, "cwdm_gn_silu_bwd: second source missing");
@@ -520,20 +560,32 @@ extern "C" int cwdm_gn_silu_bwd(const void* x0, int c0, const void* x1, int c1, 
   hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(512), 0, s, part, (int)nb, C, (int)B, gamma, mr, groups, V,
                      coef, dgamma, dbeta);
   CWDM_LAUNCHED();
-  dim3 grid((unsigned)ceil_div(V * (C / 8), 256), (unsigned)B);
+  // with channel sums: at most 1024 workgroups per batch entry (1024 atomic
+  // adds per channel), each looping over its share of the items
+  long long nblk = ceil_div(V * (C / 8), 256);
+  if (chs && nblk > 1024) nblk = 1024;
+  dim3 grid((unsigned)nblk, (unsigned)B);
   return dispatch_mode(du_mode, [&](auto M) -> int {
     constexpr int MD = decltype(M)::value;
     if (dtype == CWDM_BF16)
       hipLaunchKernelGGL((gn_bwd_apply_kernel<bf16_t, MD>), grid, dim3(256), 0, s, (const bf16_t*)x0, c0,
                          (const bf16_t*)x1, c1, (const bf16_t*)du, ss, coef, (int)d, (int)h, (int)w, (bf16_t*)dx0, acc0,
-                         (bf16_t*)dx1, acc1);
+                         (bf16_t*)dx1, acc1, chs, (long long)chs_stride);
     else
       hipLaunchKernelGGL((gn_bwd_apply_kernel<float, MD>), grid, dim3(256), 0, s, (const float*)x0, c0,
                          (const float*)x1, c1, (const float*)du, ss, coef, (int)d, (int)h, (int)w, (float*)dx0, acc0,
-                         (float*)dx1, acc1);
+                         (float*)dx1, acc1, chs, (long long)chs_stride);
     CWDM_LAUNCHED();
     return CWDM_OK;
   });
+}
+
+extern "C" int cwdm_gn_silu_bwd(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode,
+                                const float* ss, const float* mr, const float* gamma, int groups, int64_t B,
+                                int64_t d, int64_t h, int64_t w, int dtype, void* dx0, int acc0, void* dx1, int acc1,
+                                float* dgamma, float* dbeta, void* ws, int64_t ws_bytes, cwdm_stream_t stream) {
+  return gn_silu_bwd_impl(x0, c0, x1, c1, du, du_mode, ss, mr, gamma, groups, B, d, h, w, dtype, dx0, acc0, dx1, acc1,
+                          dgamma, dbeta, ws, ws_bytes, nullptr, 0, stream);
 }
 
 extern "C" int cwdm_resample_add(void* dst, const void* src, int C, int64_t B, int64_t d, int64_t h, int64_t w,

@@ -25,6 +25,10 @@ int launch_emb_bwd(const float* dEb, int R, int n, int B, const float* temb, int
 int launch_temb_bwd(const float* t, int B, int mc, const float* w1, const float* b1, const float* w2,
                     const float* temb, const float* dsil, float* dw1, float* db1, float* dw2, float* db2,
                     hipStream_t s);
+int gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode, const float* ss,
+                     const float* mr, const float* gamma, int groups, int64_t B, int64_t d, int64_t h, int64_t w,
+                     int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma, float* dbeta, void* ws,
+                     int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream);
 }  // namespace cwdm
 
 using namespace cwdm;
@@ -1301,13 +1305,24 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
           return rc;
       }
       if ((rc = dgrad(bk.c2, grd(o)))) return rc;
-      // ---- GN2 -> dh1
-      if ((rc = gn_bwd(bk.g2, h1, -1, 0))) return rc;
-      // ---- conv1: emb projection, wgrad, dgrad
+      // ---- GN2 -> dh1, with the per-channel sums of dh1 (the emb projection's
+      // gradient) taken in the same pass when dh1 is written, not accumulated
       const int k = bk.emb_k;
       const int roff = u->emb_rows_off[k], rn = u->emb_rows_n[k];
-      if ((rc = cwdm_channel_sum(grd(h1), dt, B, Vo, cout, cout, deb + roff, u->R, nullptr, nullptr, stream)))
-        return rc;
+      const bool fuse_sum = !u->ginit[h1] && 256 % (cout / 8) == 0;
+      if (fuse_sum) {
+        const auto& g = u->gns[bk.g2];
+        if ((rc = gn_silu_bwd_impl(act(h1), cout, nullptr, 0, tmp, 0, ss_of(bk.g2), mr_of(bk.g2), P(g.gamma_off),
+                                   u->cfg.num_groups, B, D >> lout, H >> lout, W >> lout, dt, grd(h1), take_acc(h1),
+                                   nullptr, 0, GR(g.gamma_p), GR(g.beta_p), gb + G.gnws, G.gnws_bytes, deb + roff, u->R,
+                                   stream)))
+          return rc;
+      } else {
+        if ((rc = gn_bwd(bk.g2, h1, -1, 0))) return rc;
+        if ((rc = cwdm_channel_sum(grd(h1), dt, B, Vo, cout, cout, deb + roff, u->R, nullptr, nullptr, stream)))
+          return rc;
+      }
+      // ---- conv1: emb projection, wgrad, dgrad
       if ((rc = launch_emb_bwd(deb + roff, u->R, rn, (int)B, temb, u->E, P(u->off_emb_w) + (int64_t)roff * u->E,
                                GR(u->emb_rows_w[k]), GR(u->emb_rows_b[k]), GR(u->emb_rows_cb[k]), dsil, s)))
         return rc;
