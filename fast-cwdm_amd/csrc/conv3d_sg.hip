@@ -36,6 +36,7 @@
 //     GroupNorm.
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <type_traits>
 
 #include "conv3d_v4.hpp"
@@ -383,8 +384,10 @@ int sg_split_for(const cwdm_conv3d_desc* d, int cin) {
   const int64_t parts = d->W == 16 ? (d->D / 4) * (d->H / 4) : (d->D / 4) * (d->H / 8);
   const int64_t tiles = d->B * parts * (d->cout / 16);
   const int nch = cin / 32;
-  if (tiles >= 256 || nch < 2) return 1;
-  int S = (int)std::min<int64_t>((256 + tiles - 1) / tiles, nch);
+  // work-item target (env CWDM_SG_TARGET, A/B knob)
+  static const int64_t target = [] { const char* e = std::getenv("CWDM_SG_TARGET"); return e ? std::atoll(e) : 256LL; }();
+  if (tiles >= target || nch < 2) return 1;
+  int S = (int)std::min<int64_t>((target + tiles - 1) / tiles, nch);
   const int per = (nch + S - 1) / S;
   S = (nch + per - 1) / per;
   return (tiles * S < (1 << 16) && S > 1) ? S : 1;
