@@ -8,7 +8,8 @@ timeout -k 10 900 python -u -m pytest -m gpu -x -q --timeout 240 --timeout-metho
 tail -1 $O/pytest.log
 for rep in 1 2; do
   for e in "$A" "$B"; do
-    env $e timeout -k 10 200 python -u bench.py --cpu-baseline 0 --train 0 --fp32 0 --batched 0 --respaced 0 --config5 0 --wavunet 0 --train5 0 --steps 30 > $O/b.json 2> $O/b.err
+    ee=$e; [ "$e" = "-" ] && ee=""
+    env $ee timeout -k 10 200 python -u bench.py --cpu-baseline 0 --train 0 --fp32 0 --batched 0 --respaced 0 --config5 0 --wavunet 0 --train5 0 --steps 30 > $O/b.json 2> $O/b.err
     python3 -c "import json; d=json.loads(open('$O/b.json').read().strip().splitlines()[-1]); print('$e', d['value'], d['ms_per_step'], d['roofline']['frac'])"
   done
 done
