@@ -22,32 +22,49 @@ template __global__ void conv3d_v4_kernel<float, 1, false>(V4Params);
 
 namespace {
 
+// Division by a launch constant without the integer-division sequence: q =
+// (mulhi(n, m) + n) >> s with s = ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1
+// (exact for n < 2^31; the sum then stays below 2^32).  The index arithmetic of
+// the 64-bit version (three 64-bit divisions per voxel) cost as much issue as
+// the memory traffic the kernel moves.
+struct FastDiv {
+  unsigned d, m, s;
+};
+inline FastDiv make_fastdiv(unsigned d) {
+  unsigned s = 0;
+  while ((1ull << s) < d) ++s;
+  return {d, (unsigned)(((1ull << 32) * ((1ull << s) - d)) / d + 1), s};
+}
+__device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.s; }
+
 // out[v][c] = SiLU(x[v][c] * sc[b][c] + sh[b][c]); a thread handles one
 // 8-channel group of VPT voxels a quarter of the volume apart (each load /
 // store instruction still covers consecutive voxels across the lanes), so
 // VPT loads are in flight together and the scale/shift reload only when the
-// batch index changes.
+// batch index changes.  32-bit item indices (host-checked: B * V * C / 8 < 2^31).
 // cm: write the chunk-major layout [B][C / CK][V][CK] the DMA-staged conv reads
 // as contiguous halo rows (CK = 16 bf16 / 8 fp32 channels = 32 bytes per voxel)
 template <typename T, int VPT>
 __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x0, int c0, const T* __restrict__ x1,
-                                                      int c1, const float* __restrict__ gn, long long vpb,
-                                                      long long n8, T* __restrict__ out, int cm) {
-  const int C = c0 + c1, G8 = C >> 3;
-  const long long nvox = n8 / G8;
-  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // (voxel slot, group)
-  const int g = (int)(i0 % G8);
-  const long long vq = i0 / G8, nq = (nvox + VPT - 1) / VPT;   // voxels vq, vq + nq, ...
+                                                      int c1, const float* __restrict__ gn, FastDiv dvpb,
+                                                      FastDiv dg8, unsigned nvox, unsigned nq, T* __restrict__ out,
+                                                      int cm) {
+  const int C = c0 + c1;
+  const unsigned i0 = blockIdx.x * 256u + threadIdx.x;   // (voxel slot, group)
+  const unsigned vq = fdiv(i0, dg8);                     // voxels vq, vq + nq, ...
   if (vq >= nq) return;
-  const int c = g * 8;
+  const int c = (int)(i0 - vq * dg8.d) * 8;
   constexpr int CK = 32 / sizeof(T);
+  const bool first = c < c0;
+  const T* xs = first ? x0 + c : x1 + (c - c0);
+  const unsigned xc = first ? c0 : c1;
   float xv[VPT][8];
-  long long vs[VPT];
+  unsigned vs[VPT];
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
-    const long long v = vq + k * nq < nvox ? vq + k * nq : nvox - 1;
+    const unsigned v = vq + k * nq < nvox ? vq + k * nq : nvox - 1;
     vs[k] = v;
-    const T* src = c < c0 ? x0 + v * c0 + c : x1 + v * c1 + (c - c0);
+    const T* src = xs + (size_t)v * xc;
     if constexpr (sizeof(T) == 2) {
       unpack<bf16_t>(*reinterpret_cast<const u32x4*>(src), xv[k]);
     } else {
@@ -55,15 +72,15 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x0,
       unpack<float>(*reinterpret_cast<const u32x4*>(src + 4), xv[k] + 4);
     }
   }
-  long long bprev = -1;
+  unsigned bprev = 0xFFFFFFFFu;
   float sc[8], sh[8];
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
     if (vq + k * nq >= nvox) break;
-    const long long v = vs[k];
-    const long long b = v / vpb;
+    const unsigned v = vs[k];
+    const unsigned b = fdiv(v, dvpb);
     if (b != bprev) {
-      const float4* g4 = reinterpret_cast<const float4*>(gn + (b * C + c) * 2);
+      const float4* g4 = reinterpret_cast<const float4*>(gn + ((size_t)b * C + c) * 2);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float4 t = g4[e];  // (sc, sh) of channels c + 2e, c + 2e + 1
@@ -74,7 +91,8 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x0,
     float y[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) y[e] = silu(xv[k][e] * sc[e] + sh[e]);
-    T* dst = cm ? out + ((b * (C / CK) + c / CK) * vpb + (v - b * vpb)) * CK + (c % CK) : out + v * C + c;
+    T* dst = cm ? out + ((size_t)(b * (unsigned)(C / CK) + (unsigned)(c / CK)) * dvpb.d + (v - b * dvpb.d)) * CK + (c % CK)
+                : out + (size_t)v * C + c;
     if constexpr (sizeof(T) == 2) {
       *reinterpret_cast<u32x4*>(dst) = pack<bf16_t>(y);
     } else {
@@ -178,15 +196,18 @@ int gn_apply(const void* x0, int c0, const void* x1, int c1, const float* gn, in
              void* out, hipStream_t s, int cm = 0) {
   constexpr int VPT = 4;
   const int G8 = (c0 + c1) / 8;
-  const int64_t n8 = B * vpb * G8;
-  const dim3 grid((unsigned)ceil_div(ceil_div(B * vpb, VPT) * G8, 256));
+  CWDM_REQUIRE(B * vpb * G8 < (1LL << 31) - 256 * VPT, CWDM_E_UNSUPPORTED,
+               "gn_apply: more than 2^31 channel groups in one launch");
+  const int64_t nvox = B * vpb, nq = ceil_div(nvox, VPT);
+  const dim3 grid((unsigned)ceil_div(nq * G8, 256));
+  const FastDiv dvpb = make_fastdiv((unsigned)vpb), dg8 = make_fastdiv((unsigned)G8);
   if (dtype == CWDM_BF16)
     hipLaunchKernelGGL((gn_apply_kernel<bf16_t, VPT>), grid, dim3(256), 0, s, reinterpret_cast<const bf16_t*>(x0), c0,
-                       reinterpret_cast<const bf16_t*>(x1), c1, gn, (long long)vpb, (long long)n8,
+                       reinterpret_cast<const bf16_t*>(x1), c1, gn, dvpb, dg8, (unsigned)nvox, (unsigned)nq,
                        reinterpret_cast<bf16_t*>(out), cm);
   else
     hipLaunchKernelGGL((gn_apply_kernel<float, VPT>), grid, dim3(256), 0, s, reinterpret_cast<const float*>(x0), c0,
-                       reinterpret_cast<const float*>(x1), c1, gn, (long long)vpb, (long long)n8,
+                       reinterpret_cast<const float*>(x1), c1, gn, dvpb, dg8, (unsigned)nvox, (unsigned)nq,
                        reinterpret_cast<float*>(out), cm);
   CWDM_LAUNCHED();
   return CWDM_OK;
@@ -381,30 +402,36 @@ __global__ void __launch_bounds__(256) gn_apply_skip_kernel(ApplySkipParams p) {
   // computes (consecutive lanes read consecutive 16-byte quads), then copied
   // to LDS: HBM latency hides under the MFMA / store work
   u32x4 pf[QT];
+  // quad i = tid + 256 j of a block: source 0 rows first (nq0 quads), then
+  // source 1; its global offset within the block's rows is i (or i - nq0) x 16
+  // bytes, its LDS offset (row vl, column) is fixed per thread: computed once,
+  // so the block loop carries no integer division
+  int loff[QT];
+#pragma unroll
+  for (int j = 0; j < QT; ++j) {
+    const int i = tid + 256 * j;
+    int vl, col;
+    if (i < nq0) { vl = i / q0; col = i - vl * q0; }
+    else { const int i1 = i - nq0; vl = i1 / q1; col = q0 + (i1 - vl * q1); }
+    loff[j] = vl * RS + col * 16;
+  }
+  const unsigned char* xb0 = reinterpret_cast<const unsigned char*>(p.x0);
+  const unsigned char* xb1 = reinterpret_cast<const unsigned char*>(p.x1);
   auto fetch = [&](long long blk) {
-    const long long v0 = blk * 128;
+    const unsigned char* s0 = xb0 + blk * 128 * q0 * 16;
+    const unsigned char* s1 = xb1 + blk * 128 * q1 * 16 - (long long)nq0 * 16;
 #pragma unroll
     for (int j = 0; j < QT; ++j) {
       if (j >= nqt) break;
       const int i = tid + 256 * j;
-      if (i < nq0) {
-        const int vl = i / q0, qq = i - vl * q0;
-        pf[j] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(p.x0) + ((v0 + vl) * q0 + qq) * 16);
-      } else {
-        const int i1 = i - nq0, vl = i1 / q1, qq = i1 - vl * q1;
-        pf[j] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(p.x1) + ((v0 + vl) * q1 + qq) * 16);
-      }
+      pf[j] = *reinterpret_cast<const u32x4*>((i < nq0 ? s0 : s1) + (long long)i * 16);
     }
   };
   auto put = [&]() {
 #pragma unroll
     for (int j = 0; j < QT; ++j) {
       if (j >= nqt) break;
-      const int i = tid + 256 * j;
-      int vl, col;
-      if (i < nq0) { vl = i / q0; col = i - vl * q0; }
-      else { const int i1 = i - nq0; vl = i1 / q1; col = q0 + (i1 - vl * q1); }
-      *reinterpret_cast<u32x4*>(xt + vl * RS + col * 16) = pf[j];
+      *reinterpret_cast<u32x4*>(xt + loff[j]) = pf[j];
     }
   };
   if ((long long)blockIdx.x < nblocks) fetch(blockIdx.x);
