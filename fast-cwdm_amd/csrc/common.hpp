@@ -77,4 +77,19 @@ template <> struct Elem<bf16_t> {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Division by a launch constant without the integer-division sequence: q =
+// (mulhi(n, m) + n) >> s with s = ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1
+// (exact for n < 2^31; the sum then stays below 2^32).  For the index
+// arithmetic of the streaming kernels, where 64-bit divisions cost as much
+// issue as the memory traffic they move.
+struct FastDiv {
+  unsigned d, m, s;
+};
+inline FastDiv make_fastdiv(unsigned d) {
+  unsigned s = 0;
+  while ((1ull << s) < d) ++s;
+  return {d, (unsigned)(((1ull << 32) * ((1ull << s) - d)) / d + 1), s};
+}
+__device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.s; }
+
 }  // namespace cwdm

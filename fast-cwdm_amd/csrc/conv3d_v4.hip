@@ -22,26 +22,13 @@ template __global__ void conv3d_v4_kernel<float, 1, false>(V4Params);
 
 namespace {
 
-// Division by a launch constant without the integer-division sequence: q =
-// (mulhi(n, m) + n) >> s with s = ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1
-// (exact for n < 2^31; the sum then stays below 2^32).  The index arithmetic of
-// the 64-bit version (three 64-bit divisions per voxel) cost as much issue as
-// the memory traffic the kernel moves.
-struct FastDiv {
-  unsigned d, m, s;
-};
-inline FastDiv make_fastdiv(unsigned d) {
-  unsigned s = 0;
-  while ((1ull << s) < d) ++s;
-  return {d, (unsigned)(((1ull << 32) * ((1ull << s) - d)) / d + 1), s};
-}
-__device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.s; }
-
 // out[v][c] = SiLU(x[v][c] * sc[b][c] + sh[b][c]); a thread handles one
 // 8-channel group of VPT voxels a quarter of the volume apart (each load /
 // store instruction still covers consecutive voxels across the lanes), so
 // VPT loads are in flight together and the scale/shift reload only when the
-// batch index changes.  32-bit item indices (host-checked: B * V * C / 8 < 2^31).
+// batch index changes.  32-bit item indices (host-checked: B * V * C / 8 < 2^31;
+// the 64-bit version's three 64-bit divisions per voxel cost as much issue as
+// the traffic it moves).
 // cm: write the chunk-major layout [B][C / CK][V][CK] the DMA-staged conv reads
 // as contiguous halo rows (CK = 16 bf16 / 8 fp32 channels = 32 bytes per voxel)
 template <typename T, int VPT>

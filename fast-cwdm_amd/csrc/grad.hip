@@ -77,9 +77,11 @@ __device__ __forceinline__ void load_du(const T* du, int C, int c, int b, unsign
   }
 }
 
-// d/dz SiLU(z) * du
+// d/dz SiLU(z) * du, the sigmoid from the hardware exp2 / reciprocal like the
+// forward's silu() (1-2 ulp): the IEEE expf + division sequence made the
+// GroupNorm backward passes issue-bound instead of HBM-bound
 __device__ __forceinline__ float dsilu(float z, float du) {
-  const float s = 1.0f / (1.0f + expf(-z));
+  const float s = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
   return du * (s * (1.0f + z * (1.0f - s)));
 }
 
@@ -231,18 +233,18 @@ __global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__
                                                           const float* __restrict__ ss,
                                                           const float* __restrict__ coef, int d, int h, int w,
                                                           T* __restrict__ dx0, int acc0, T* __restrict__ dx1,
-                                                          int acc1, float* __restrict__ chs, long long chs_stride) {
+                                                          int acc1, float* __restrict__ chs, long long chs_stride,
+                                                          FastDiv dncg) {
   const int C = c0 + c1, ncg = C >> 3;
   const long long V = (long long)d * h * w;
   const int b = blockIdx.y;
-  const long long n = V * ncg, step = (long long)gridDim.x * 256;
+  const unsigned n = (unsigned)(V * ncg), step = gridDim.x * 256u;   // < 2^31 (host-checked)
   float sum[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) sum[e] = 0.f;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += step) {
-    const int cg = (int)(i % ncg);
-    const long long v = i / ncg;
-    const int c = cg * 8;
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += step) {
+    const unsigned v = fdiv(i, dncg);
+    const int c = (int)(i - v * dncg.d) * 8;
     const bool first = c < c0;
     const T* xs = first ? x0 : x1;
     T* dx = first ? dx0 : dx1;
@@ -250,7 +252,7 @@ __global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__
     const int acc = first ? acc0 : acc1;
     float xv[8], g[8], o[8];
     load8<T>(xs + ((long long)b * V + v) * xc + xo, xv);
-    load_du<T, MODE>(du, C, c, b, (unsigned)v, d, h, w, g);
+    load_du<T, MODE>(du, C, c, b, v, d, h, w, g);
     if (acc) load8<T>(dx + ((long long)b * V + v) * xc + xo, o);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -280,16 +282,16 @@ __global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__
 
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) resample_add_kernel(T* __restrict__ dst, const T* __restrict__ src, int C,
-                                                          int d, int h, int w, int acc) {
+                                                          int d, int h, int w, int acc, FastDiv dncg) {
   const int ncg = C >> 3;
   const long long V = (long long)d * h * w;
   const int b = blockIdx.y;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= V * ncg) return;
-  const int c = (int)(i % ncg) * 8;
-  const long long v = i / ncg;
+  const unsigned i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= (unsigned)(V * ncg)) return;   // < 2^31 (host-checked)
+  const unsigned v = fdiv(i, dncg);
+  const int c = (int)(i - v * dncg.d) * 8;
   float g[8], o[8];
-  load_du<T, MODE>(src, C, c, b, (unsigned)v, d, h, w, g);
+  load_du<T, MODE>(src, C, c, b, v, d, h, w, g);
   T* p = dst + ((long long)b * V + v) * C + c;
   if (acc) {
     load8<T>(p, o);
@@ -536,7 +538,10 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
   CWDM_REQUIRE(B > 0 && B < 65536 && d > 0 && h > 0 && w > 0, CWDM_E_SHAPE, "cwdm_gn_silu_bwd: empty grid");
   CWDM_REQUIRE(ws_bytes >= cwdm_gn_silu_bwd_workspace_bytes(C, B, d, h, w), CWDM_E_WORKSPACE,
                "cwdm_gn_silu_bwd: workspace too small");
+  CWDM_REQUIRE(d * h * w * (C / 8) < (1LL << 31) - 256LL * 1024, CWDM_E_UNSUPPORTED,
+               "cwdm_gn_silu_bwd: more than 2^31 channel groups per batch entry");
   const long long V = d * h * w;
+  const FastDiv dncg = make_fastdiv((unsigned)(C / 8));
   const long long nb = gn_bwd_blocks(C, V);
   const long long vpb = ceil_div(V, nb);
   float* part = reinterpret_cast<float*>(ws);
@@ -570,11 +575,11 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
     if (dtype == CWDM_BF16)
       hipLaunchKernelGGL((gn_bwd_apply_kernel<bf16_t, MD>), grid, dim3(256), 0, s, (const bf16_t*)x0, c0,
                          (const bf16_t*)x1, c1, (const bf16_t*)du, ss, coef, (int)d, (int)h, (int)w, (bf16_t*)dx0, acc0,
-                         (bf16_t*)dx1, acc1, chs, (long long)chs_stride);
+                         (bf16_t*)dx1, acc1, chs, (long long)chs_stride, dncg);
     else
       hipLaunchKernelGGL((gn_bwd_apply_kernel<float, MD>), grid, dim3(256), 0, s, (const float*)x0, c0,
                          (const float*)x1, c1, (const float*)du, ss, coef, (int)d, (int)h, (int)w, (float*)dx0, acc0,
-                         (float*)dx1, acc1, chs, (long long)chs_stride);
+                         (float*)dx1, acc1, chs, (long long)chs_stride, dncg);
     CWDM_LAUNCHED();
     return CWDM_OK;
   });
@@ -595,17 +600,20 @@ extern "C" int cwdm_resample_add(void* dst, const void* src, int C, int64_t B, i
   CWDM_REQUIRE(mode >= 0 && mode <= 2, CWDM_E_INVALID, "cwdm_resample_add: bad mode");
   CWDM_REQUIRE(mode != 2 || (d % 2 == 0 && h % 2 == 0 && w % 2 == 0), CWDM_E_SHAPE, "cwdm_resample_add: odd grid");
   CWDM_REQUIRE(B > 0 && B < 65536 && d > 0 && h > 0 && w > 0, CWDM_E_SHAPE, "cwdm_resample_add: empty grid");
+  CWDM_REQUIRE(d * h * w * (C / 8) < (1LL << 31) - 256, CWDM_E_UNSUPPORTED,
+               "cwdm_resample_add: more than 2^31 channel groups per batch entry");
   const long long V = d * h * w;
+  const FastDiv dncg = make_fastdiv((unsigned)(C / 8));
   dim3 grid((unsigned)ceil_div(V * (C / 8), 256), (unsigned)B);
   hipStream_t s = (hipStream_t)stream;
   return dispatch_mode(mode, [&](auto M) -> int {
     constexpr int MD = decltype(M)::value;
     if (dtype == CWDM_BF16)
       hipLaunchKernelGGL((resample_add_kernel<bf16_t, MD>), grid, dim3(256), 0, s, (bf16_t*)dst, (const bf16_t*)src, C,
-                         (int)d, (int)h, (int)w, accumulate);
+                         (int)d, (int)h, (int)w, accumulate, dncg);
     else
       hipLaunchKernelGGL((resample_add_kernel<float, MD>), grid, dim3(256), 0, s, (float*)dst, (const float*)src, C,
-                         (int)d, (int)h, (int)w, accumulate);
+                         (int)d, (int)h, (int)w, accumulate, dncg);
     CWDM_LAUNCHED();
     return CWDM_OK;
   });
