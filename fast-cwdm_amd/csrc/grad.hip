@@ -111,15 +111,25 @@ __global__ void __launch_bounds__(256) gn_bwd_reduce_kernel(const T* __restrict_
   const int xc = c < c0 ? c0 : c1, xo = c < c0 ? c : c - c0;
   if (slot < nslots) {
     const long long v0 = blk * vpb, v1 = v0 + vpb < V ? v0 + vpb : V;
-    for (long long v = v0 + slot; v < v1; v += nslots) {
-      float xv[8], g[8];
-      load8<T>(xs + ((long long)b * V + v) * xc + xo, xv);
-      load_du<T, MODE>(du, C, c, b, (unsigned)v, d, h, w, g);
+    // UNR voxels per trip, all their loads issued before the arithmetic
+    constexpr int UNR = MODE == 1 ? 1 : 4;
+    for (long long vb = v0 + slot; vb < v1; vb += (long long)UNR * nslots) {
+      float xv[UNR][8], g[UNR][8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float dz = dsilu(xv[e] * sc[e] + sh[e], g[e]);
-        A[e] += dz;
-        Bs[e] += dz * ((xv[e] - mu[e]) * rs[e]);
+      for (int u = 0; u < UNR; ++u) {
+        const long long v = vb + (long long)u * nslots < v1 ? vb + (long long)u * nslots : vb;
+        load8<T>(xs + ((long long)b * V + v) * xc + xo, xv[u]);
+        load_du<T, MODE>(du, C, c, b, (unsigned)v, d, h, w, g[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (vb + (long long)u * nslots >= v1) break;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dz = dsilu(xv[u][e] * sc[e] + sh[e], g[u][e]);
+          A[e] += dz;
+          Bs[e] += dz * ((xv[u][e] - mu[e]) * rs[e]);
+        }
       }
     }
   }
@@ -221,50 +231,69 @@ template <typename T> __device__ __forceinline__ float stored(float v) {
   else return v;
 }
 
-// Grid-stride over the (voxel, 8-channel group) items of batch blockIdx.y.
+// Batch blockIdx.y.  A workgroup of blockDim.x = (256 / ncg) * ncg threads
+// (ncg = C / 8 channel groups) keeps each thread on ONE channel group (tid %
+// ncg), so its 8 channels' scale / shift and coefficients sit in registers for
+// the whole grid-stride loop over voxels (a per-item reload of the 40
+// coefficient words cost more issue than the tensor traffic).
 // chs (optional): per-channel sums of the written dx (the value as stored),
 // atomically added to chs[b * chs_stride + c] -- the emb-projection gradient of
-// the block's conv1 output (sum over voxels of d h1) without a second read of
-// dx.  The stride gridDim.x * 256 is then a multiple of C / 8 (host-checked), so
-// every thread keeps one channel group.
+// the block's conv1 output (sum over voxels of d h1) without a second read of dx.
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__ x0, int c0, const T* __restrict__ x1,
                                                           int c1, const T* __restrict__ du,
                                                           const float* __restrict__ ss,
                                                           const float* __restrict__ coef, int d, int h, int w,
                                                           T* __restrict__ dx0, int acc0, T* __restrict__ dx1,
-                                                          int acc1, float* __restrict__ chs, long long chs_stride,
-                                                          FastDiv dncg) {
+                                                          int acc1, float* __restrict__ chs, long long chs_stride) {
   const int C = c0 + c1, ncg = C >> 3;
-  const long long V = (long long)d * h * w;
+  const unsigned V = (unsigned)d * h * w;   // < 2^31 (host-checked)
   const int b = blockIdx.y;
-  const unsigned n = (unsigned)(V * ncg), step = gridDim.x * 256u;   // < 2^31 (host-checked)
+  const int nvb = blockDim.x / ncg;         // voxels per workgroup trip
+  const int cg = threadIdx.x % ncg, c = cg * 8;
+  const bool first = c < c0;
+  const T* xs = first ? x0 : x1;
+  T* dx = first ? dx0 : dx1;
+  const int xc = first ? c0 : c1, xo = first ? c : c - c0;
+  const int acc = first ? acc0 : acc1;
+  float k_sc[8], k_sh[8], k0[8], k1[8], k2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const long long bc = (long long)b * C + c + e;
+    k_sc[e] = ss[bc * 2]; k_sh[e] = ss[bc * 2 + 1];
+    k0[e] = coef[bc * 4]; k1[e] = coef[bc * 4 + 1]; k2[e] = coef[bc * 4 + 2];
+  }
+  const T* xb = xs + (size_t)b * V * xc + xo;
+  T* ob = dx + (size_t)b * V * xc + xo;
   float sum[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) sum[e] = 0.f;
-  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += step) {
-    const unsigned v = fdiv(i, dncg);
-    const int c = (int)(i - v * dncg.d) * 8;
-    const bool first = c < c0;
-    const T* xs = first ? x0 : x1;
-    T* dx = first ? dx0 : dx1;
-    const int xc = first ? c0 : c1, xo = first ? c : c - c0;
-    const int acc = first ? acc0 : acc1;
-    float xv[8], g[8], o[8];
-    load8<T>(xs + ((long long)b * V + v) * xc + xo, xv);
-    load_du<T, MODE>(du, C, c, b, v, d, h, w, g);
-    if (acc) load8<T>(dx + ((long long)b * V + v) * xc + xo, o);
+  const unsigned vstep = gridDim.x * (unsigned)nvb;
+  // UNR voxels per trip: all loads first, then the arithmetic and stores
+  constexpr int UNR = MODE == 1 ? 1 : 2;
+  for (unsigned v0 = blockIdx.x * (unsigned)nvb + threadIdx.x / ncg; v0 < V; v0 += UNR * vstep) {
+    float xv[UNR][8], g[UNR][8], o[UNR][8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const long long bc = (long long)b * C + c + e;
-      const float dz = dsilu(xv[e] * ss[bc * 2] + ss[bc * 2 + 1], g[e]);
-      const float r = coef[bc * 4] * dz + coef[bc * 4 + 1] * xv[e] + coef[bc * 4 + 2];
-      o[e] = acc ? o[e] + r : r;
+    for (int u = 0; u < UNR; ++u) {
+      const unsigned v = v0 + u * vstep < V ? v0 + u * vstep : v0;
+      load8<T>(xb + (size_t)v * xc, xv[u]);
+      load_du<T, MODE>(du, C, c, b, v, d, h, w, g[u]);
+      if (acc) load8<T>(ob + (size_t)v * xc, o[u]);
     }
-    store8<T>(dx + ((long long)b * V + v) * xc + xo, o);
-    if (chs) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) sum[e] += stored<T>(o[e]);
+    for (int u = 0; u < UNR; ++u) {
+      if (v0 + u * vstep >= V) break;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dz = dsilu(xv[u][e] * k_sc[e] + k_sh[e], g[u][e]);
+        const float r = k0[e] * dz + k1[e] * xv[u][e] + k2[e];
+        o[u][e] = acc ? o[u][e] + r : r;
+      }
+      store8<T>(ob + (size_t)(v0 + u * vstep) * xc, o[u]);
+      if (chs) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sum[e] += stored<T>(o[u][e]);
+      }
     }
   }
   if (!chs) return;
@@ -272,11 +301,10 @@ __global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__
 #pragma unroll
   for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = sum[e];
   __syncthreads();
-  const int nslots = 256 / ncg;
-  for (int c = threadIdx.x; c < C; c += 256) {
+  for (int cc = threadIdx.x; cc < C; cc += blockDim.x) {
     float s = 0.f;
-    for (int k = 0; k < nslots; ++k) s += red[(k * ncg + (c >> 3)) * 8 + (c & 7)];
-    atomicAdd(chs + (long long)b * chs_stride + c, s);
+    for (int k = 0; k < nvb; ++k) s += red[(k * ncg + (cc >> 3)) * 8 + (cc & 7)];
+    atomicAdd(chs + (long long)b * chs_stride + cc, s);
   }
 }
 
@@ -522,8 +550,8 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
                            int64_t h, int64_t w, int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma,
                            float* dbeta, void* ws, int64_t ws_bytes, float* chs, int64_t chs_stride,
                            cwdm_stream_t stream) {
-  CWDM_REQUIRE(!chs || (c1 == 0 && 256 % (c0 / 8) == 0 && chs_stride >= c0), CWDM_E_UNSUPPORTED,
-               "gn_silu_bwd: fused channel sums need one source with C / 8 dividing 256");
+  CWDM_REQUIRE(!chs || (c1 == 0 && chs_stride >= c0), CWDM_E_UNSUPPORTED,
+               "gn_silu_bwd: fused channel sums need one source");
   CWDM_REQUIRE(x0 && du && ss && mr && gamma && dx0 && dgamma && dbeta && ws, CWDM_E_INVALID,
                "cwdm_gn_silu_bwd: null pointer");
   CWDM_REQUIRE(c1 == 0 || (x1 && dx1), CWDM_E_INVALID, "cwdm_gn_silu_bwd: second source missing");
@@ -541,7 +569,6 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
   CWDM_REQUIRE(d * h * w * (C / 8) < (1LL << 31) - 256LL * 1024, CWDM_E_UNSUPPORTED,
                "cwdm_gn_silu_bwd: more than 2^31 channel groups per batch entry");
   const long long V = d * h * w;
-  const FastDiv dncg = make_fastdiv((unsigned)(C / 8));
   const long long nb = gn_bwd_blocks(C, V);
   const long long vpb = ceil_div(V, nb);
   float* part = reinterpret_cast<float*>(ws);
@@ -567,19 +594,24 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
   CWDM_LAUNCHED();
   // with channel sums: at most 1024 workgroups per batch entry (1024 atomic
   // adds per channel), each looping over its share of the items
-  long long nblk = ceil_div(V * (C / 8), 256);
+  // workgroups of (256 / ncg) voxels x ncg channel groups; two voxels per
+  // thread (the kernel's UNR; du_mode 1 loops twice instead); with channel
+  // sums at most 1024 workgroups per batch entry (1024 atomic adds per channel)
+  const int ncg = C / 8, nvb = 256 / ncg;
+  long long nblk = ceil_div(V, 2LL * nvb);
   if (chs && nblk > 1024) nblk = 1024;
   dim3 grid((unsigned)nblk, (unsigned)B);
+  const dim3 block((unsigned)(nvb * ncg));
   return dispatch_mode(du_mode, [&](auto M) -> int {
     constexpr int MD = decltype(M)::value;
     if (dtype == CWDM_BF16)
-      hipLaunchKernelGGL((gn_bwd_apply_kernel<bf16_t, MD>), grid, dim3(256), 0, s, (const bf16_t*)x0, c0,
+      hipLaunchKernelGGL((gn_bwd_apply_kernel<bf16_t, MD>), grid, block, 0, s, (const bf16_t*)x0, c0,
                          (const bf16_t*)x1, c1, (const bf16_t*)du, ss, coef, (int)d, (int)h, (int)w, (bf16_t*)dx0, acc0,
-                         (bf16_t*)dx1, acc1, chs, (long long)chs_stride, dncg);
+                         (bf16_t*)dx1, acc1, chs, (long long)chs_stride);
     else
-      hipLaunchKernelGGL((gn_bwd_apply_kernel<float, MD>), grid, dim3(256), 0, s, (const float*)x0, c0,
+      hipLaunchKernelGGL((gn_bwd_apply_kernel<float, MD>), grid, block, 0, s, (const float*)x0, c0,
                          (const float*)x1, c1, (const float*)du, ss, coef, (int)d, (int)h, (int)w, (float*)dx0, acc0,
-                         (float*)dx1, acc1, chs, (long long)chs_stride, dncg);
+                         (float*)dx1, acc1, chs, (long long)chs_stride);
     CWDM_LAUNCHED();
     return CWDM_OK;
   });

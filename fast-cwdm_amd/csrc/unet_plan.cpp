@@ -1309,7 +1309,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
       // gradient) taken in the same pass when dh1 is written, not accumulated
       const int k = bk.emb_k;
       const int roff = u->emb_rows_off[k], rn = u->emb_rows_n[k];
-      const bool fuse_sum = !u->ginit[h1] && 256 % (cout / 8) == 0;
+      const bool fuse_sum = !u->ginit[h1];
       if (fuse_sum) {
         const auto& g = u->gns[bk.g2];
         if ((rc = gn_silu_bwd_impl(act(h1), cout, nullptr, 0, tmp, 0, ss_of(bk.g2), mr_of(bk.g2), P(g.gamma_off),
