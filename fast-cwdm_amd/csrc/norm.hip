@@ -122,44 +122,76 @@ extern "C" int cwdm_gn_finalize(const float* s0, int64_t p0, int c0, const float
 // runs at the low resolution with no prologue transform.
 namespace cwdm {
 namespace {
+template <typename T> __device__ __forceinline__ void pool_load8(const T* p, float* f);
+template <> __device__ __forceinline__ void pool_load8<float>(const float* p, float* f) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+template <> __device__ __forceinline__ void pool_load8<bf16_t>(const bf16_t* p, float* f) {
+  const uint4 a = *reinterpret_cast<const uint4*>(p);
+  const unsigned u[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(u[i] << 16); f[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u); }
+}
+template <typename T> __device__ __forceinline__ void pool_store8(T* p, const float* f);
+template <> __device__ __forceinline__ void pool_store8<float>(float* p, const float* f) {
+  *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+}
+template <> __device__ __forceinline__ void pool_store8<bf16_t>(bf16_t* p, const float* f) {
+  uint4 a;
+  a.x = (unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16);
+  a.y = (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16);
+  a.z = (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16);
+  a.w = (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16);
+  *reinterpret_cast<uint4*>(p) = a;
+}
+
+// one thread = one 8-channel group of one pooled voxel: 8 16-byte loads (the
+// 2x2x2 sources), GroupNorm + SiLU (hardware exp2 / reciprocal, as the conv
+// kernels' GroupNorm prologue), 16-byte stores; 32-bit indices with magic
+// divisors (host-checked: B * d * h * w * C / 8 < 2^31)
 template <typename T>
 __global__ void __launch_bounds__(256) gn_silu_pool_kernel(const T* __restrict__ x, int C,
-                                                          const float* __restrict__ gn, long long B, int d, int h,
-                                                          int w, T* __restrict__ oh, T* __restrict__ ox) {
-  const int G8 = C / 8;
-  const long long n = B * (long long)d * h * w * G8;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+                                                          const float* __restrict__ gn, unsigned n, FastDiv dg8,
+                                                          FastDiv dw, FastDiv dh, FastDiv dd, T* __restrict__ oh,
+                                                          T* __restrict__ ox) {
+  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int g = (int)(i % G8);
-  long long v = i / G8;
-  const int xx = (int)(v % w), yy = (int)((v / w) % h), zz = (int)((v / ((long long)w * h)) % d);
-  const long long b = v / ((long long)w * h * d);
+  const unsigned v = fdiv(i, dg8);
+  const int g = (int)(i - v * dg8.d);
+  const unsigned vy = fdiv(v, dw), xx = v - vy * dw.d;
+  const unsigned vz = fdiv(vy, dh), yy = vy - vz * dh.d;
+  const unsigned b = fdiv(vz, dd), zz = vz - b * dd.d;
   float sc[8], sh[8], ah[8], ax[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    sc[e] = gn[(b * C + g * 8 + e) * 2];
-    sh[e] = gn[(b * C + g * 8 + e) * 2 + 1];
+    sc[e] = gn[((size_t)b * C + g * 8 + e) * 2];
+    sh[e] = gn[((size_t)b * C + g * 8 + e) * 2 + 1];
     ah[e] = 0.f;
     ax[e] = 0.f;
   }
-  const int H = 2 * h, W = 2 * w, D = 2 * d;
+  const unsigned H = 2 * dh.d, W = 2 * dw.d, D = 2 * dd.d;
+  float xv[8][8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const long long src = (((b * D + 2 * zz + (k >> 2)) * H + 2 * yy + ((k >> 1) & 1)) * W + 2 * xx + (k & 1)) * C + g * 8;
+    const size_t src = ((((size_t)b * D + 2 * zz + (k >> 2)) * H + 2 * yy + ((k >> 1) & 1)) * W + 2 * xx + (k & 1)) * C +
+                       g * 8;
+    pool_load8<T>(x + src, xv[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float xv = Elem<T>::to_f(x[src + e]);
-      const float y = xv * sc[e] + sh[e];
-      ah[e] += y / (1.0f + __expf(-y));
-      ax[e] += xv;
+      const float y = xv[k][e] * sc[e] + sh[e];
+      ah[e] += y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(y * -1.4426950408889634f));
+      ax[e] += xv[k][e];
     }
-  }
-  const long long dst = v * C + g * 8;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    oh[dst + e] = Elem<T>::from_f(ah[e] * 0.125f);
-    ox[dst + e] = Elem<T>::from_f(ax[e] * 0.125f);
-  }
+  for (int e = 0; e < 8; ++e) { ah[e] *= 0.125f; ax[e] *= 0.125f; }
+  const size_t dst = (size_t)v * C + g * 8;
+  pool_store8<T>(oh + dst, ah);
+  pool_store8<T>(ox + dst, ax);
 }
 }  // namespace
 }  // namespace cwdm
@@ -170,14 +202,17 @@ extern "C" int cwdm_gn_silu_pool(const void* x, int C, const float* gn, int64_t 
   CWDM_REQUIRE(C > 0 && C % 8 == 0 && B > 0 && d > 0 && h > 0 && w > 0, CWDM_E_SHAPE,
                "cwdm_gn_silu_pool: bad shape (channels must be a multiple of 8)");
   const int64_t n = B * d * h * w * (C / 8);
+  CWDM_REQUIRE(n < (1LL << 31) - 256, CWDM_E_UNSUPPORTED, "cwdm_gn_silu_pool: more than 2^31 channel groups");
   dim3 grid((unsigned)ceil_div(n, 256));
+  const FastDiv dg8 = make_fastdiv((unsigned)(C / 8)), dw = make_fastdiv((unsigned)w), dh = make_fastdiv((unsigned)h),
+                dd = make_fastdiv((unsigned)d);
   if (dtype == CWDM_BF16)
     hipLaunchKernelGGL(gn_silu_pool_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream,
-                       reinterpret_cast<const bf16_t*>(x), C, gn, (long long)B, (int)d, (int)h, (int)w,
+                       reinterpret_cast<const bf16_t*>(x), C, gn, (unsigned)n, dg8, dw, dh, dd,
                        reinterpret_cast<bf16_t*>(out_h), reinterpret_cast<bf16_t*>(out_x));
   else if (dtype == CWDM_F32)
     hipLaunchKernelGGL(gn_silu_pool_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream,
-                       reinterpret_cast<const float*>(x), C, gn, (long long)B, (int)d, (int)h, (int)w,
+                       reinterpret_cast<const float*>(x), C, gn, (unsigned)n, dg8, dw, dh, dd,
                        reinterpret_cast<float*>(out_h), reinterpret_cast<float*>(out_x));
   else
     return fail(CWDM_E_INVALID, "cwdm_gn_silu_pool: bad dtype");
