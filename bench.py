@@ -131,6 +131,19 @@ def cpu_baseline(state, cond, x_T, threads, T=1000, warmup=1, steps=2):
     return dts[warmup:]
 
 
+def cpu_config1(threads):
+    """BASELINE.md §3 / config 1 end to end on CPU: the 64^3 phantom set ->
+    Haar DWT conditioning -> 2-step 'sampled' p_sample_loop with the tiny U-Net
+    (seeded non-zero weights) -> IDWT, clamp, brain mask (oracle.cases.c1_run),
+    wall clock of one full run after one warm-up run."""
+    from oracle import cases
+    torch.set_num_threads(threads)
+    cases.c1_run()
+    t0 = time.perf_counter()
+    cases.c1_run()
+    return time.perf_counter() - t0
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -364,7 +377,12 @@ def main():
     # of the N-rank code path; the driver's N-GPU runs use RCCL, one GPU per rank)
     rehearse = os.environ.get("CWDM_BENCH_REHEARSE") == "1" or args.dry_run
     if world > 1:
-        dist.init_process_group("gloo" if rehearse else "nccl")
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            # one GPU per rank, bound at init (RCCL communicator on cuda:LOCAL_RANK)
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.dry_run:
         def mor(v):
             tt = torch.tensor([v], dtype=torch.float64)
@@ -595,7 +613,11 @@ def main():
                                "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
                                "seconds_per_step": [round(d, 2) for d in dts],
                                "extrapolated_s_per_volume": {"1000_steps": round(1000 * per, 1),
-                                                             "50_steps": round(50 * per, 1)}}
+                                                             "50_steps": round(50 * per, 1)},
+                               "config1_end_to_end_s": round(cpu_config1(threads), 3),
+                               "config1_workload": "config 1 on CPU, end to end: 64^3 phantoms -> DWT "
+                                                   "conditioning -> 2-step 'sampled' loop, tiny U-Net (mc 32, "
+                                                   "mult 1,2) -> IDWT, clamp, mask (oracle.cases.c1_run)"}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -70,12 +70,19 @@ struct SGParams {
   // result does not depend on the arrival order) and runs the epilogue
   int ksplit, kper;
   float* part;
+  // per-tile arrival counters of this launch (K split only): caller memory,
+  // zero when the launch starts (the last slice of a tile resets its counter, so
+  // launches in stream order can share one block zeroed once: the U-Net plan
+  // zeroes one per forward / backward, a lone cwdm_conv3d_forward memsets its
+  // own in the workspace).  Never a process-wide array: launches on other
+  // streams or plans would share tiles' counters.
+  unsigned* count;
 };
 
-// per-tile arrival counters of the K-split launches, zero between launches (the
-// last slice of a tile resets its counter).  One K-split small-grid launch at a
-// time per device: launches on one stream serialise.
-__device__ unsigned g_sg_count[1 << 16];
+// counter block pre-zeroed by the caller (the U-Net plan, per forward /
+// backward, thread-local for the duration of its launch list) or null
+thread_local unsigned* g_sg_sync = nullptr;
+constexpr int64_t kSgSyncWords = 1 << 16;   // tiles of one K-split launch (sg_split_for keeps tiles * S below)
 
 __device__ __forceinline__ void sg_mfma(sg_f32x4& acc, const u32x4& a, const u32x4& b) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0,
@@ -234,10 +241,13 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
 
   if (q.ksplit > 1) {
     // K split: publish this slice, the tile's last arrival finishes it.  Hand-off
-    // across XCDs without fences (cdna_hip_programming.md, publish / consume
-    // recipe): the slice is stored write-through (sc1) and drained by every
-    // storing wave before the counter add; the finishing workgroup reads every
-    // slice with sc1 loads (past its stale L1 / L2 lines).
+    // across XCDs without fences: the in-launch split-K recipe of
+    // cdna_hip_programming.md §5 item 2 ("sc1 (write-through) slab stores, which
+    // need no release fence -> every wave s_waitcnt vmcnt(0) -> __syncthreads()
+    // -> lane 0 relaxed agent fetch_add; the reducer then reads the slabs with
+    // sc1 loads, EVERY load of them"), valid for any placement of a tile's slices
+    // over XCDs.  A __threadfence() release / acquire per slice measured 2x slower
+    // here.
     const int tile = st * q.ntile16 + t16;
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
         q.part + (long long)tile * q.ksplit * 4096, (short)0, q.ksplit * 4096 * 4, 0x00020000);
@@ -250,10 +260,10 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
     __syncthreads();
     unsigned* flag = reinterpret_cast<unsigned*>(smem);
     if (tid == 0)
-      *flag = __hip_atomic_fetch_add(&g_sg_count[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = __hip_atomic_fetch_add(&q.count[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (*flag != (unsigned)(q.ksplit - 1)) return;
-    if (tid == 0) __hip_atomic_store(&g_sg_count[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(&q.count[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     float bi[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) bi[i] = p.bias ? p.bias[(long long)b * p.bias_bs + t16 * 16 + 4 * kq + i] : 0.f;
@@ -397,7 +407,27 @@ int sg_split_for(const cwdm_conv3d_desc* d, int cin) {
 int sg_ksplit(const cwdm_conv3d_desc* d) { return sg_eligible(d) ? sg_split_for(d, d->a_c0 + d->a_c1) : 1; }
 int sg_skip_ksplit(const cwdm_conv3d_desc* d) { return sg_skip_eligible(d) ? sg_split_for(d, d->b_c0 + d->b_c1) : 1; }
 
+// bytes of the K-split counter block a lone launch keeps behind its slices (0 without a split)
+int64_t sg_sync_bytes(int ksplit) { return ksplit > 1 ? kSgSyncWords * 4 : 0; }
+
 namespace {
+// counters of a K-split launch: the plan's pre-zeroed block, else `own` (the
+// workspace tail behind the slices), zeroed here by a memset node
+int sg_counters(SGParams& q, void* own, hipStream_t s) {
+  q.count = nullptr;
+  if (q.ksplit == 1) return CWDM_OK;
+  const int64_t tiles = (int64_t)q.v.B * q.parts * q.ntile16;
+  CWDM_REQUIRE(tiles <= kSgSyncWords, CWDM_E_UNSUPPORTED, "conv3d (small grid): too many K-split tiles");
+  if (g_sg_sync) {
+    q.count = g_sg_sync;
+    return CWDM_OK;
+  }
+  CWDM_REQUIRE(own, CWDM_E_INVALID, "conv3d (small grid): K-split counters missing");
+  q.count = reinterpret_cast<unsigned*>(own);
+  CWDM_HIP(hipMemsetAsync(own, 0, (size_t)((tiles * 4 + 15) & ~15LL), s));
+  return CWDM_OK;
+}
+
 int sg_go(const SGParams& q, const cwdm_conv3d_desc* d, int taps, double flops, hipStream_t s) {
   const dim3 grid((unsigned)(d->B * q.parts * q.ntile16 * q.ksplit));
   prof_begin(s);
@@ -419,7 +449,8 @@ int sg_go(const SGParams& q, const cwdm_conv3d_desc* d, int taps, double flops, 
 }
 }  // namespace
 
-// partial: fp32 scratch of sg_ksplit(d) x B x V x cout (the K-split slices), else unused
+// partial: fp32 scratch of sg_ksplit(d) x B x V x cout (the K-split slices) followed
+// by sg_sync_bytes of counters, else unused
 int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, void* partial, hipStream_t s) {
   SGParams q{};
   q.v = v;
@@ -429,6 +460,11 @@ int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, void* partial, hipSt
   q.kper = ((d->a_c0 + d->a_c1) / 32 + q.ksplit - 1) / q.ksplit;
   q.part = reinterpret_cast<float*>(partial);
   CWDM_REQUIRE(q.ksplit == 1 || partial, CWDM_E_INVALID, "conv3d (small grid): K-split scratch missing");
+  int rc;
+  if ((rc = sg_counters(q, q.ksplit > 1 ? reinterpret_cast<unsigned char*>(partial) +
+                                              (int64_t)q.ksplit * d->B * d->D * d->H * d->W * d->cout * 4
+                                        : nullptr, s)))
+    return rc;
   return sg_go(q, d, 27, 2.0 * d->B * d->D * d->H * d->W * (double)d->cout * 27.0 * (d->a_c0 + d->a_c1), s);
 }
 
@@ -454,6 +490,11 @@ int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, void* partial, hipStrea
   q.kper = ((d->b_c0 + d->b_c1) / 32 + q.ksplit - 1) / q.ksplit;
   q.part = reinterpret_cast<float*>(partial);
   CWDM_REQUIRE(q.ksplit == 1 || partial, CWDM_E_INVALID, "conv3d (small grid): K-split scratch missing");
+  int rc;
+  if ((rc = sg_counters(q, q.ksplit > 1 ? reinterpret_cast<unsigned char*>(partial) +
+                                              (int64_t)q.ksplit * d->B * V * d->cout * 4
+                                        : nullptr, s)))
+    return rc;
   return sg_go(q, d, 1, 2.0 * d->B * V * (double)d->cout * (d->b_c0 + d->b_c1), s);
 }
 

@@ -112,6 +112,7 @@ int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, void* partial, hipSt
 int sg_ksplit(const cwdm_conv3d_desc* d);
 int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, void* partial, hipStream_t s);
 int sg_skip_ksplit(const cwdm_conv3d_desc* d);
+int64_t sg_sync_bytes(int ksplit);
 
 int64_t v4_items(const cwdm_conv3d_desc* d) {
   return d->B * ((d->W + 31) / 32) * (d->H / 4) * (d->D / 4) * (d->cout / 64);
@@ -173,7 +174,8 @@ int64_t v4_workspace_bytes(const cwdm_conv3d_desc* d) {
     e.a_w = nullptr;
     S = std::max(S, sg_skip_ksplit(&e));
   }
-  if (S > 1) ws += align256(S * d->B * d->D * d->H * d->W * d->cout * 4);
+  // (+ the small-grid kernel's K-split arrival counters behind the slices)
+  if (S > 1) ws += align256(S * d->B * d->D * d->H * d->W * d->cout * 4) + sg_sync_bytes(S);
   return ws;
 }
 

@@ -312,11 +312,32 @@ __global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__
 #pragma unroll
   for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = sum[e];
   __syncthreads();
+  // this workgroup's channel sums -> its row of the partials [B][gridDim.x][C]
+  // (chs_reduce_kernel adds them in workgroup order: deterministic)
   for (int cc = threadIdx.x; cc < C; cc += blockDim.x) {
     float s = 0.f;
     for (int k = 0; k < nvb; ++k) s += red[(k * ncg + (cc >> 3)) * 8 + (cc & 7)];
-    atomicAdd(chs + (long long)b * chs_stride + cc, s);
+    chs[((long long)b * gridDim.x + blockIdx.x) * C + cc] = s;
   }
+}
+
+// out[b * stride + c] += sum_k part[b][k][c], k in order (fixed-order finish of
+// per-workgroup channel sums: the result does not depend on arrival order)
+__global__ void __launch_bounds__(256) chs_reduce_kernel(const float* __restrict__ part, int nk, int C,
+                                                        float* __restrict__ out_bc, long long bc_stride,
+                                                        float* __restrict__ out_c, float* __restrict__ out_c2, int B) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float tot = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float* p = part + (long long)b * nk * C + c;
+    float s = 0.f;
+    for (int k = 0; k < nk; ++k) s += p[(long long)k * C];
+    if (out_bc) out_bc[(long long)b * bc_stride + c] += s;
+    tot += s;
+  }
+  if (out_c) out_c[c] += tot;
+  if (out_c2) out_c2[c] += tot;
 }
 
 template <typename T, int MODE>
@@ -347,7 +368,7 @@ template <typename T>
 __global__ void __launch_bounds__(256) channel_sum_kernel(const T* __restrict__ src, long long V, int C, int cs,
                                                          long long vpb, float* __restrict__ out_bc,
                                                          long long bc_stride, float* __restrict__ out_c,
-                                                         float* __restrict__ out_c2) {
+                                                         float* __restrict__ out_c2, float* __restrict__ part) {
   __shared__ float red[256 * 8];
   const int ncg = (C + 7) >> 3, nslots = 256 / ncg;
   const int b = blockIdx.y, blk = blockIdx.x;
@@ -370,6 +391,10 @@ __global__ void __launch_bounds__(256) channel_sum_kernel(const T* __restrict__ 
   for (int c = threadIdx.x; c < C; c += 256) {
     float s = 0.f;
     for (int k = 0; k < nslots; ++k) s += red[(k * ncg + (c >> 3)) * 8 + (c & 7)];
+    if (part) {   // deterministic: [B][gridDim.x][C] partials, chs_reduce_kernel finishes
+      part[((long long)b * gridDim.x + blk) * C + c] = s;
+      continue;
+    }
     if (out_bc) atomicAdd(out_bc + (long long)b * bc_stride + c, s);
     if (out_c) atomicAdd(out_c + c, s);
     if (out_c2) atomicAdd(out_c2 + c, s);
@@ -550,7 +575,8 @@ extern "C" int64_t cwdm_gn_silu_bwd_workspace_bytes(int C, int64_t B, int64_t d,
   if (C <= 0 || B <= 0 || d <= 0 || h <= 0 || w <= 0) return -1;
   const long long nb = gn_bwd_blocks(C, d * h * w);
   const int64_t part = B * nb * C * 2 * 4;
-  return (part + 255) / 256 * 256 + B * (int64_t)C * 4 * 4;
+  // partials, coefficients, then the fused channel sums' per-workgroup partials (<= 1024 per batch entry)
+  return (part + 255) / 256 * 256 + (B * (int64_t)C * 4 * 4 + 255) / 256 * 256 + B * 1024LL * C * 4;
 }
 
 // cwdm_gn_silu_bwd, plus (chs != nullptr, single source, C / 8 dividing 256)
@@ -584,6 +610,7 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
   const long long vpb = ceil_div(V, nb);
   float* part = reinterpret_cast<float*>(ws);
   float* coef = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(ws) + (B * nb * C * 2 * 4 + 255) / 256 * 256);
+  float* chs_part = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(coef) + (B * (int64_t)C * 4 * 4 + 255) / 256 * 256);
   hipStream_t s = (hipStream_t)stream;
   int rc;
   if ((rc = dispatch_mode(du_mode, [&](auto M) -> int {
@@ -603,29 +630,36 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
   hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(512), 0, s, part, (int)nb, C, (int)B, gamma, mr, groups, V,
                      coef, dgamma, dbeta);
   CWDM_LAUNCHED();
-  // with channel sums: at most 1024 workgroups per batch entry (1024 atomic
-  // adds per channel), each looping over its share of the items
   // workgroups of (256 / ncg) voxels x ncg channel groups; two voxels per
   // thread (the kernel's UNR; du_mode 1 loops twice instead); with channel
-  // sums at most 1024 workgroups per batch entry (1024 atomic adds per channel)
+  // sums at most 1024 workgroups per batch entry (one partial row each, summed
+  // in workgroup order by chs_reduce_kernel), each looping over its share
   const int ncg = C / 8, nvb = 256 / ncg;
   long long nblk = ceil_div(V, 2LL * nvb);
   if (chs && nblk > 1024) nblk = 1024;
   dim3 grid((unsigned)nblk, (unsigned)B);
   const dim3 block((unsigned)(nvb * ncg));
-  return dispatch_mode(du_mode, [&](auto M) -> int {
-    constexpr int MD = decltype(M)::value;
-    if (dtype == CWDM_BF16)
-      hipLaunchKernelGGL((gn_bwd_apply_kernel<bf16_t, MD>), grid, block, 0, s, (const bf16_t*)x0, c0,
-                         (const bf16_t*)x1, c1, (const bf16_t*)du, ss, coef, (int)d, (int)h, (int)w, (bf16_t*)dx0, acc0,
-                         (bf16_t*)dx1, acc1, chs, (long long)chs_stride);
-    else
-      hipLaunchKernelGGL((gn_bwd_apply_kernel<float, MD>), grid, block, 0, s, (const float*)x0, c0,
-                         (const float*)x1, c1, (const float*)du, ss, coef, (int)d, (int)h, (int)w, (float*)dx0, acc0,
-                         (float*)dx1, acc1, chs, (long long)chs_stride);
+  float* cp = chs ? chs_part : nullptr;
+  if ((rc = dispatch_mode(du_mode, [&](auto M) -> int {
+         constexpr int MD = decltype(M)::value;
+         if (dtype == CWDM_BF16)
+           hipLaunchKernelGGL((gn_bwd_apply_kernel<bf16_t, MD>), grid, block, 0, s, (const bf16_t*)x0, c0,
+                              (const bf16_t*)x1, c1, (const bf16_t*)du, ss, coef, (int)d, (int)h, (int)w, (bf16_t*)dx0,
+                              acc0, (bf16_t*)dx1, acc1, cp, (long long)chs_stride);
+         else
+           hipLaunchKernelGGL((gn_bwd_apply_kernel<float, MD>), grid, block, 0, s, (const float*)x0, c0,
+                              (const float*)x1, c1, (const float*)du, ss, coef, (int)d, (int)h, (int)w, (float*)dx0,
+                              acc0, (float*)dx1, acc1, cp, (long long)chs_stride);
+         CWDM_LAUNCHED();
+         return CWDM_OK;
+       })))
+    return rc;
+  if (chs) {
+    hipLaunchKernelGGL(chs_reduce_kernel, dim3((unsigned)ceil_div(C, 256)), dim3(256), 0, s, chs_part, (int)nblk, C,
+                       chs, (long long)chs_stride, nullptr, nullptr, (int)B);
     CWDM_LAUNCHED();
-    return CWDM_OK;
-  });
+  }
+  return CWDM_OK;
 }
 
 extern "C" int cwdm_gn_silu_bwd(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode,
@@ -662,24 +696,44 @@ extern "C" int cwdm_resample_add(void* dst, const void* src, int C, int64_t B, i
   });
 }
 
+namespace {
+long long channel_sum_blocks(int64_t V) {
+  long long nb = ceil_div(V, 2048);
+  return nb > 512 ? 512 : nb;
+}
+}  // namespace
+
+extern "C" int64_t cwdm_channel_sum_workspace_bytes(int64_t B, int64_t V, int C) {
+  if (B <= 0 || V <= 0 || C <= 0) return -1;
+  return B * channel_sum_blocks(V) * C * 4;
+}
+
 extern "C" int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V, int C, int cs, float* out_bc,
-                                int64_t bc_stride, float* out_c, float* out_c2, cwdm_stream_t stream) {
+                                int64_t bc_stride, float* out_c, float* out_c2, void* workspace, int64_t ws_bytes,
+                                cwdm_stream_t stream) {
   CWDM_REQUIRE(src, CWDM_E_INVALID, "cwdm_channel_sum: null pointer");
   CWDM_REQUIRE(C > 0 && cs >= ((C + 7) / 8) * 8 && cs % 8 == 0 && cs <= 2048, CWDM_E_UNSUPPORTED,
                "cwdm_channel_sum: stride must be a multiple of 8 covering C (<= 2048)");
   CWDM_REQUIRE(B > 0 && B < 65536 && V > 0, CWDM_E_SHAPE, "cwdm_channel_sum: empty input");
-  long long nb = ceil_div(V, 2048);
-  if (nb > 512) nb = 512;
+  CWDM_REQUIRE(!workspace || ws_bytes >= cwdm_channel_sum_workspace_bytes(B, V, C), CWDM_E_WORKSPACE,
+               "cwdm_channel_sum: workspace too small");
+  const long long nb = channel_sum_blocks(V);
   const long long vpb = ceil_div(V, nb);
   dim3 grid((unsigned)nb, (unsigned)B);
   hipStream_t s = (hipStream_t)stream;
+  float* part = reinterpret_cast<float*>(workspace);
   if (dtype == CWDM_BF16)
     hipLaunchKernelGGL(channel_sum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)src, (long long)V, C, cs, vpb,
-                       out_bc, (long long)bc_stride, out_c, out_c2);
+                       out_bc, (long long)bc_stride, out_c, out_c2, part);
   else
     hipLaunchKernelGGL(channel_sum_kernel<float>, grid, dim3(256), 0, s, (const float*)src, (long long)V, C, cs, vpb,
-                       out_bc, (long long)bc_stride, out_c, out_c2);
+                       out_bc, (long long)bc_stride, out_c, out_c2, part);
   CWDM_LAUNCHED();
+  if (part) {
+    hipLaunchKernelGGL(chs_reduce_kernel, dim3((unsigned)ceil_div(C, 256)), dim3(256), 0, s, part, (int)nb, C, out_bc,
+                       (long long)bc_stride, out_c, out_c2, (int)B);
+    CWDM_LAUNCHED();
+  }
   return CWDM_OK;
 }
 

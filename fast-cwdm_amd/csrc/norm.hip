@@ -201,6 +201,9 @@ extern "C" int cwdm_gn_silu_pool(const void* x, int C, const float* gn, int64_t 
   CWDM_REQUIRE(x && gn && out_h && out_x, CWDM_E_INVALID, "cwdm_gn_silu_pool: null pointer");
   CWDM_REQUIRE(C > 0 && C % 8 == 0 && B > 0 && d > 0 && h > 0 && w > 0, CWDM_E_SHAPE,
                "cwdm_gn_silu_pool: bad shape (channels must be a multiple of 8)");
+  // 16-byte accesses (pool_load8 / pool_store8): every 8-channel group starts on a 16-byte boundary
+  CWDM_REQUIRE(((uintptr_t)x | (uintptr_t)out_h | (uintptr_t)out_x) % 16 == 0, CWDM_E_INVALID,
+               "cwdm_gn_silu_pool: x, out_h and out_x must be 16-byte aligned");
   const int64_t n = B * d * h * w * (C / 8);
   CWDM_REQUIRE(n < (1LL << 31) - 256, CWDM_E_UNSUPPORTED, "cwdm_gn_silu_pool: more than 2^31 channel groups");
   dim3 grid((unsigned)ceil_div(n, 256));

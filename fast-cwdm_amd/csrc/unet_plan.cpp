@@ -557,11 +557,23 @@ int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* g
                   const void* wskip, int cout, void* act, void* skip, hipStream_t s);
 int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
               const void* res, int rmode, void* partial, hipStream_t s);
+extern thread_local unsigned* g_sg_sync;
+int64_t sg_sync_bytes(int ksplit);
 }  // namespace cwdm
+namespace {
+// the small-grid conv's K-split arrival counters for one launch list: one block
+// in the plan's workspace, zeroed once (a memset node) before the list -- each
+// K-split launch leaves its counters zero again -- and handed to the launches
+// for the duration of the call (conv3d_sg.hip)
+struct SgSyncScope {
+  SgSyncScope(void* block) { cwdm::g_sg_sync = reinterpret_cast<unsigned*>(block); }
+  ~SgSyncScope() { cwdm::g_sg_sync = nullptr; }
+};
+}  // namespace
 namespace {
 
 struct Layout {
-  int64_t temb, ebias, split, split_bytes;
+  int64_t temb, ebias, split, split_bytes, sync;
   int64_t skipbuf = 0;          // conv2 residual written by the fused GroupNorm + 1x1-skip pass
   std::vector<char> skip_fused; // per conv1 with a skip: that pass is used
   std::vector<int64_t> t_off, s_off, s_parts;
@@ -596,6 +608,7 @@ Layout layout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
   Layout L;
   int64_t off = 0;
   auto take = [&](int64_t bytes) { int64_t o = off; off = align_up(off + bytes); return o; };
+  L.sync = take(cwdm::sg_sync_bytes(2));   // first: a memset block at a 256-byte boundary
   L.temb = take(B * u->E * 4);
   L.ebias = take(B * (int64_t)u->R * 4);
   const int es = esize(u->cfg.dtype);
@@ -816,6 +829,8 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
   hipStream_t s = (hipStream_t)stream;
   auto* pk = reinterpret_cast<const unsigned char*>(packed);
   auto* wb = reinterpret_cast<unsigned char*>(ws);
+  CWDM_HIP(hipMemsetAsync(wb + L.sync, 0, cwdm::sg_sync_bytes(2), s));
+  SgSyncScope sync_scope(wb + L.sync);
   float* temb = reinterpret_cast<float*>(wb + L.temb);
   float* ebias = reinterpret_cast<float*>(wb + L.ebias);
   int rc;
@@ -1002,7 +1017,7 @@ namespace {
 
 struct GLayout {
   std::vector<int64_t> g_off;
-  int64_t tmp, dout, deb, dsil, gnws, gnws_bytes, split, split_bytes, wgws, dwe, total;
+  int64_t sync, tmp, dout, deb, dsil, gnws, gnws_bytes, split, split_bytes, wgws, dwe, chs, chs_bytes, total;
 };
 
 int ckpad(const cwdm_unet* u, int c) {
@@ -1030,6 +1045,7 @@ GLayout glayout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) 
   int64_t off = 0;
   auto take = [&](int64_t bytes) { int64_t o = off; off = align_up(off + bytes); return o; };
   const int es = esize(u->cfg.dtype);
+  G.sync = take(cwdm::sg_sync_bytes(2));
   for (size_t i = 0; i < u->tensors.size(); ++i) {
     const auto& t = u->tensors[i];
     if ((int)i == u->input_tensor) { G.g_off.push_back(-1); continue; }
@@ -1064,6 +1080,12 @@ GLayout glayout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) 
   for (const auto& cs : u->convs)
     if (cs.s2) dwe = std::max(dwe, (int64_t)cs.cout * cs.cin_a * 27 * 4);
   G.dwe = take(dwe);
+  int64_t chs = 0;   // per-workgroup partials of the bias-gradient channel sums (fixed-order finish)
+  for (const auto& cs : u->convs)
+    chs = std::max(chs, cwdm_channel_sum_workspace_bytes(B, (D >> cs.level) * (H >> cs.level) * (W >> cs.level),
+                                                         std::max(cs.cout, 8)));
+  G.chs_bytes = chs;
+  G.chs = take(chs);
   G.total = off;
   return G;
 }
@@ -1154,6 +1176,9 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
   auto* pb = reinterpret_cast<const unsigned char*>(packed_bwd);
   auto* wb = reinterpret_cast<const unsigned char*>(ws);
   auto* gb = reinterpret_cast<unsigned char*>(gws);
+  // (every call: a caller may run segments on a fresh grad workspace)
+  CWDM_HIP(hipMemsetAsync(gb + G.sync, 0, cwdm::sg_sync_bytes(2), s));
+  SgSyncScope sync_scope(gb + G.sync);
   auto P = [&](int64_t off) { return reinterpret_cast<const float*>(pk + off); };
   auto GR = [&](int pi) { return grads + u->goff[pi]; };
   auto act = [&](int id) -> const void* {
@@ -1223,7 +1248,9 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
       if ((rc = cwdm_copy3(dout, CWDM_F32, ss_, d16, dt, ds_, B, oc, V0, stream))) return rc;
       const auto& co = u->convs[u->head_c];
       const auto& hg = u->gns[u->head_g];
-      if ((rc = cwdm_channel_sum(d16, dt, B, V0, oc, ocp, nullptr, 0, GR(co.b_p), nullptr, stream))) return rc;
+      if ((rc = cwdm_channel_sum(d16, dt, B, V0, oc, ocp, nullptr, 0, GR(co.b_p), nullptr, gb + G.chs, G.chs_bytes,
+                                 stream)))
+        return rc;
       if ((rc = wgrad(0, 3, act(co.a0), co.cin_a, nullptr, 0, 0, ss_of(u->head_g), d16, ocp, oc, GR(co.w_p))))
         return rc;
       if ((rc = dgrad(u->head_c, d16))) return rc;
@@ -1237,7 +1264,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
       const int o = cs.out, xt = bk.x0;
       const int chn = u->tensors[xt].channels, lx = u->tensors[xt].level;
       if ((rc = cwdm_channel_sum(grd(o), dt, B, vox(cs.level), cs.cout, cs.cout, nullptr, 0, GR(cs.b_p), nullptr,
-                                 stream)))
+                                 gb + G.chs, G.chs_bytes, stream)))
         return rc;
       if (bk.updown == 4) {
         if ((rc = wgrad(cs.level, 3, act(xt), chn, nullptr, 0, 1, nullptr, grd(o), cs.cout, cs.cout, GR(cs.w_p))))
@@ -1269,7 +1296,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
       const int cout = c2.cout;
       // ---- conv2 (+ skip / residual)
       if ((rc = cwdm_channel_sum(grd(o), dt, B, Vo, cout, cout, nullptr, 0, GR(c2.b_p),
-                                 c2.wsb_p >= 0 ? GR(c2.wsb_p) : nullptr, stream)))
+                                 c2.wsb_p >= 0 ? GR(c2.wsb_p) : nullptr, gb + G.chs, G.chs_bytes, stream)))
         return rc;
       if ((rc = wgrad(lout, 3, act(h1), cout, nullptr, 0, 0, ss_of(bk.g2), grd(o), cout, cout, GR(c2.w_p))))
         return rc;
@@ -1319,7 +1346,8 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
           return rc;
       } else {
         if ((rc = gn_bwd(bk.g2, h1, -1, 0))) return rc;
-        if ((rc = cwdm_channel_sum(grd(h1), dt, B, Vo, cout, cout, deb + roff, u->R, nullptr, nullptr, stream)))
+        if ((rc = cwdm_channel_sum(grd(h1), dt, B, Vo, cout, cout, deb + roff, u->R, nullptr, nullptr, gb + G.chs,
+                                   G.chs_bytes, stream)))
           return rc;
       }
       // ---- conv1: emb projection, wgrad, dgrad
@@ -1345,7 +1373,8 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
     // conv_in + time_embed
     const auto& c0 = u->convs[0];
     const int64_t V0 = D * H * W;
-    if ((rc = cwdm_channel_sum(grd(c0.out), dt, B, V0, c0.cout, c0.cout, nullptr, 0, GR(c0.b_p), nullptr, stream)))
+    if ((rc = cwdm_channel_sum(grd(c0.out), dt, B, V0, c0.cout, c0.cout, nullptr, 0, GR(c0.b_p), nullptr, gb + G.chs,
+                               G.chs_bytes, stream)))
       return rc;
     if ((rc = wgrad(0, 3, x, c0.cin_a, nullptr, 0, 0, nullptr, grd(c0.out), c0.cout, c0.cout, GR(c0.w_p)))) return rc;
     if ((rc = launch_temb_bwd(t, (int)B, u->cfg.model_channels, P(u->off_te_w1), P(u->off_te_b1), P(u->off_te_w2),

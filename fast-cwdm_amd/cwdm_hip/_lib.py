@@ -149,8 +149,9 @@ _PROTOS = {
                                         ctypes.c_int, vp, vp, vp, i64, vp]),
     "cwdm_resample_add": (ctypes.c_int, [vp, vp, ctypes.c_int, i64, i64, i64, i64, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, vp]),
+    "cwdm_channel_sum_workspace_bytes": (i64, [i64, i64, ctypes.c_int]),
     "cwdm_channel_sum": (ctypes.c_int, [vp, ctypes.c_int, i64, i64, ctypes.c_int, ctypes.c_int, vp, i64, vp, vp,
-                                        vp]),
+                                        vp, i64, vp]),
     "cwdm_adamw": (ctypes.c_int, [vp, vp, vp, vp, i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, ctypes.c_double, i64, vp]),
     "cwdm_unet_create": (ctypes.c_int, [ctypes.POINTER(UNetConfig), ctypes.POINTER(vp)]),
@@ -216,12 +217,28 @@ def check_build_id(L):
     """Refuse a library built from other sources than the tree's (the .so is
     untracked and travels to the GPU box as a file; CWDM_ALLOW_STALE_LIB=1
     skips the check for kernel experiments)."""
-    from .srchash import source_hash
+    from .srchash import source_files, source_hash
+    if os.environ.get("CWDM_ALLOW_STALE_LIB") == "1":
+        return
+    if not all(os.path.exists(f) for f in source_files_or_empty(source_files)):
+        # a deployment that ships only the .so: nothing to compare against
+        import warnings
+        warnings.warn(f"libcwdm sources not found next to the package: build id of {LIB_PATH} not checked")
+        return
     built = L.cwdm_build_id().decode()
     want = source_hash()
-    if built != want and os.environ.get("CWDM_ALLOW_STALE_LIB") != "1":
+    if built != want:
         raise OSError(f"{LIB_PATH} was built from sources {built}, the tree has {want}: "
                       f"rebuild with `make -C fast-cwdm_amd/csrc`")
+
+
+def source_files_or_empty(source_files):
+    """The source list the build id covers, or [""] (a path that does not
+    exist) when the csrc directory itself is absent."""
+    try:
+        return source_files()
+    except OSError:
+        return [""]
 
 
 def check(rc, what=""):

@@ -40,14 +40,19 @@ def setup_dist(devices=(0,)):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     cuda = th.cuda.device_count() > 0 and th.cuda.is_available()
     backend = "nccl" if cuda else "gloo"
+    kw = {}
     if cuda:
         local = int(os.environ.get("LOCAL_RANK", "0"))
         if launched:
-            th.cuda.set_device(local % th.cuda.device_count())
+            idx = local % th.cuda.device_count()
         else:
             first = devices[0] if isinstance(devices, (list, tuple)) else devices
-            th.cuda.set_device(int(first) % th.cuda.device_count())
-    dist.init_process_group(backend=backend, init_method="env://")
+            idx = int(first) % th.cuda.device_count()
+        th.cuda.set_device(idx)
+        # bind the communicator to this rank's GPU up front (no "guessing device
+        # ID based on global rank" at the first collective)
+        kw["device_id"] = th.device("cuda", idx)
+    dist.init_process_group(backend=backend, init_method="env://", **kw)
 
 
 def dev(device_number=None):

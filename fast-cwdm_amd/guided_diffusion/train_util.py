@@ -152,6 +152,7 @@ class TrainLoop:
             if self.step % self.save_interval == 0:
                 self.save_if_best(float(lossmse))
                 if os.environ.get("DIFFUSION_TRAINING_TEST", "") and self.step > 0:
+                    self.flush_finite_check()   # the last step's non-finite-loss warning still logs
                     return
             self.step += 1
         self.flush_finite_check()

@@ -324,7 +324,8 @@ int cwdm_gn_finalize(const float* stats0, int64_t parts0, int c0,
 /* Down-ResBlock pre-pass: h = AvgPool2(SiLU(x*scale+shift)), x_upd = AvgPool2(x)
  * (ResBlock._forward with down=True, guided_diffusion/unet.py:286-291,
  * Downsample :73-100).  x: NDHWC high-res (B, 2d, 2h, 2w, C); outputs NDHWC
- * (B, d, h, w, C) in dtype; gn as for cwdm_conv3d_desc.a_gn. */
+ * (B, d, h, w, C) in dtype; gn as for cwdm_conv3d_desc.a_gn.  x, out_h and
+ * out_x must be 16-byte aligned (16-byte loads / stores per 8 channels). */
 int cwdm_gn_silu_pool(const void* x, int C, const float* gn, int64_t B, int64_t d, int64_t h, int64_t w,
                       int dtype, void* out_h, void* out_x, cwdm_stream_t stream);
 
@@ -398,10 +399,15 @@ int cwdm_resample_add(void* dst, const void* src, int C, int64_t B, int64_t d, i
                       int mode, int accumulate, int dtype, cwdm_stream_t stream);
 
 /* Per-channel sums of src [B][V][cs] (first C channels): out_bc[b*bc_stride+c]
- * += sum_v, out_c[c] += sum_{b,v}, out_c2 likewise (each may be NULL; fp32
- * atomics -- zero first).  Bias gradients and the emb-projection gradient. */
+ * += sum_v, out_c[c] += sum_{b,v}, out_c2 likewise (each may be NULL).  Bias
+ * gradients and the emb-projection gradient.  With a workspace of
+ * cwdm_channel_sum_workspace_bytes the per-workgroup sums are added in a fixed
+ * order (bitwise repeatable); workspace NULL adds them with fp32 atomics
+ * (arrival order: not repeatable). */
+int64_t cwdm_channel_sum_workspace_bytes(int64_t B, int64_t V, int C);
 int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V, int C, int cs,
-                     float* out_bc, int64_t bc_stride, float* out_c, float* out_c2, cwdm_stream_t stream);
+                     float* out_bc, int64_t bc_stride, float* out_c, float* out_c2,
+                     void* workspace, int64_t ws_bytes, cwdm_stream_t stream);
 
 /* torch.optim.AdamW step (decoupled weight decay) over a flat fp32 buffer:
  * p *= 1 - lr*wd; m = lerp(m, g, 1-beta1); v = beta2*v + (1-beta2)*g*g;

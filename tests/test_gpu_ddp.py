@@ -141,12 +141,13 @@ def _rccl_rank(port, q):
         model, diffusion = _model("c1")
         vols, t, noise = _inputs("c1")
         g_plain, _ = _grad(model, diffusion, vols, t, noise)
-        red = GradBucketReducer(bucket_bytes=256 << 10, force=True)
+        red = GradBucketReducer(bucket_bytes=256 << 10, force=True, timing=True)
         model._grad_hook = red
         for p in model.parameters():
             p.grad = None
         g_red, _ = _grad(model, diffusion, vols, t, noise)
-        q.put((red.launched, float((g_red - g_plain).abs().max()), float(g_plain.abs().max())))
+        bwd_end, buckets = red.timeline()
+        q.put((red.launched, float((g_red - g_plain).abs().max()), float(g_plain.abs().max()), bwd_end, buckets))
     finally:
         dist.destroy_process_group()
 
@@ -156,8 +157,16 @@ def test_reducer_over_rccl_world1():
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_rank, args=(_free_port(), q))
     p.start()
-    launched, diff, scale = q.get(timeout=240)
+    launched, diff, scale, bwd_end, buckets = q.get(timeout=240)
     p.join(timeout=60)
     assert p.exitcode == 0
     assert launched >= 2          # several buckets went through RCCL
     assert diff <= 1e-6 * scale, (diff, scale)
+    # overlap, measured on the GPU timeline: bucket collectives start (on the
+    # reducer's stream) while later backward segments still run on the compute
+    # stream, i.e. before the backward's last segment ends
+    assert len(buckets) == launched
+    early = [b for b in buckets if b[1] < bwd_end]
+    print("backward end %.3f ms; buckets (ready, start, end) ms:" % bwd_end, buckets)
+    assert len(early) >= launched - 1, (bwd_end, buckets)
+    assert all(s >= r - 1e-3 for r, s, _ in buckets)   # a collective never starts before its gradients

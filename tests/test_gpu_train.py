@@ -275,13 +275,24 @@ def test_resample_add_and_channel_sum(mode):
     s = _nd(src).to(DEV)
     check(L.cwdm_resample_add(d.data_ptr(), s.data_ptr(), C, B, *grid, mode, 1, _lib.CWDM_F32, None))
     assert rel_err(_nc(d.cpu()) - dst0, xr.grad) < 1e-6
+    V = s[0, ..., 0].numel()
+    ref_bc = src.sum(dim=(2, 3, 4))[:, :12]
+    runs = []
+    for ws in (None, torch.empty(L.cwdm_channel_sum_workspace_bytes(B, V, 12), dtype=torch.uint8, device=DEV)):
+        out_bc = torch.zeros(B, 24, device=DEV)
+        out_c = torch.zeros(C, device=DEV)
+        check(L.cwdm_channel_sum(s.data_ptr(), _lib.CWDM_F32, B, V, 12, C, out_bc.data_ptr(), 24, out_c.data_ptr(),
+                                 None, None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(), None))
+        assert rel_err(out_bc[:, :12], ref_bc) < 1e-5
+        assert rel_err(out_c[:12], ref_bc.sum(0)) < 1e-5
+        runs.append((out_bc.clone(), out_c.clone()))
+    # with a workspace the per-workgroup sums finish in a fixed order: bitwise repeatable
+    ws = torch.empty(L.cwdm_channel_sum_workspace_bytes(B, V, 12), dtype=torch.uint8, device=DEV)
     out_bc = torch.zeros(B, 24, device=DEV)
     out_c = torch.zeros(C, device=DEV)
-    check(L.cwdm_channel_sum(s.data_ptr(), _lib.CWDM_F32, B, s[0, ..., 0].numel(), 12, C, out_bc.data_ptr(), 24,
-                             out_c.data_ptr(), None, None))
-    ref_bc = src.sum(dim=(2, 3, 4))[:, :12]
-    assert rel_err(out_bc[:, :12], ref_bc) < 1e-5
-    assert rel_err(out_c[:12], ref_bc.sum(0)) < 1e-5
+    check(L.cwdm_channel_sum(s.data_ptr(), _lib.CWDM_F32, B, V, 12, C, out_bc.data_ptr(), 24, out_c.data_ptr(),
+                             None, ws.data_ptr(), ws.numel(), None))
+    assert torch.equal(out_bc, runs[1][0]) and torch.equal(out_c, runs[1][1])
 
 
 def test_adamw_matches_torch():

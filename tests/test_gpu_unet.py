@@ -81,8 +81,9 @@ def test_production_unet_forward_dma_kernel(grid):
         m32 = _product_model(cfg, 32, P, "fp32")
         with torch.no_grad():
             out = m32(x.to(DEV), t.to(DEV))
-            if grid[0] <= 16:
-                assert rel_err(out, ou.unet_forward(P, x, t)) < 1e-3
+            # the oracle at every grid, including 32x32x64 (R0 and R1 on the DMA kernel, the
+            # 16^3-class levels on the small-grid kernel)
+            assert rel_err(out, ou.unet_forward(P, x, t)) < 1e-3
             m16 = _product_model(cfg, 32, P, "bf16")
             assert rel_err(m16(x.to(DEV), t.to(DEV)), out) < 6e-2
     finally:
