@@ -225,7 +225,7 @@ def config5_leg(args, device, rank, world, sync, max_over_ranks):
     model = script_util.create_model(image_size=n, num_channels=64, num_res_blocks=2, channel_mult="1,2,2",
                                      attention_resolutions="", dims=3, num_groups=32, in_channels=256,
                                      out_channels=64, bottleneck_attention=False, resample_2d=False,
-                                     resblock_updown=True, compute_dtype=args.dtype)
+                                     resblock_updown=True, compute_dtype=args.config5_dtype)
     seeded_weights(model, 5)
     model.to(device)
     t0 = time.perf_counter()
@@ -250,13 +250,11 @@ def config5_leg(args, device, rank, world, sync, max_over_ranks):
     fl = model.plan.flops(1, g, g, g)
     res = {"workload": "config5: 224^3 input, 2-level block wavelet (56^3 x 64 ch per modality, 15 subbands), "
                        "FATS per-subband schedules, 3-level U-Net (256->64 ch, mc 64, mult 1,2,2, 2 res blocks), "
-                       f"{args.dtype}, {'HIP-graph' if args.graph else 'eager'} loop, one volume per GPU",
+                       f"{args.config5_dtype}, {'HIP-graph' if args.graph else 'eager'} loop, one volume per GPU",
            "denoising_steps_per_s": round(world * K / dt, 3), "ms_per_step": round(1000 * per, 3), "steps": K,
            "s_per_volume": {"1000_steps": round(1000 * per, 2), "50_steps": round(50 * per, 3)},
            "front_end_ms": round(1000 * t_front, 2), "unet_tflop_per_step": round(fl / 1e12, 3),
-           "mfma_frac": round(fl / per / 1e12 / BF16_PEAK_TFLOPS, 4),
-           "precision_note": "fp16 requested by the config is served by bf16 (same MFMA rate on gfx950; the "
-                             "reference's use_fp16 is a no-op, DESIGN.md)"}
+           "mfma_frac": round(fl / per / 1e12 / BF16_PEAK_TFLOPS, 4), "dtype": args.config5_dtype}
     del model, loop
     torch.cuda.empty_cache()
     return res
@@ -266,7 +264,8 @@ def train5_leg(args, device, rank, world, sync, max_over_ranks):
     """Config 5 training: TrainLoop.run_step on the 2-level representation
     (224^3 phantoms x 4 modalities -> cwdm_prepare_batch2 -> the config-5
     3-level U-Net, FATS per-channel q_sample rows -> segmented native backward
-    (+ RCCL bucketed all-reduce when N > 1) -> fused AdamW), batch 1 per GPU."""
+    (+ RCCL bucketed all-reduce when N > 1) -> fused AdamW), batch 1 per GPU, in --config5-dtype
+    (fp16: dynamic loss scaling, TrainLoop's GradScaler)."""
     import numpy as np
     from cwdm_hip import ops
     from guided_diffusion import fats, script_util, train_util
@@ -275,7 +274,7 @@ def train5_leg(args, device, rank, world, sync, max_over_ranks):
     model = script_util.create_model(image_size=n, num_channels=64, num_res_blocks=2, channel_mult="1,2,2",
                                      attention_resolutions="", dims=3, num_groups=32, in_channels=256,
                                      out_channels=64, bottleneck_attention=False, resample_2d=False,
-                                     resblock_updown=True, compute_dtype=args.dtype)
+                                     resblock_updown=True, compute_dtype=args.config5_dtype)
     seeded_weights(model, 5)
     model.to(device)
     batch = {k: phantom_gpu(n, 700 + 100 * rank + j, device) for j, k in enumerate(("t1n", "t1c", "t2w", "t2f"))}
@@ -302,11 +301,14 @@ def train5_leg(args, device, rank, world, sync, max_over_ranks):
     per = dt / K
     res = {"workload": "config5 training: TrainLoop.run_step, 224^3 phantoms x 4 modalities -> 2-level block "
                        "wavelets (56^3 x 64 ch per modality), FATS per-channel q_sample, 3-level U-Net (256->64 ch), "
-                       f"{args.dtype}, batch 1 per GPU, gradient all-reduce "
+                       f"{args.config5_dtype}{' (dynamic loss scaling)' if loop.grad_scaler.is_enabled() else ''}, "
+                       "batch 1 per GPU, gradient all-reduce "
                        f"({'RCCL' if world > 1 and dist.get_backend() == 'nccl' else dist.get_backend() if world > 1 else 'none'})",
            "volumes_per_s": round(world * K / dt, 4), "ms_per_step": round(1000 * per, 2), "steps": K,
            "conv_tflop_per_step": round(fl / 1e12, 3), "mfma_frac": round(fl / per / 1e12 / BF16_PEAK_TFLOPS, 4),
-           "loss": round(float(loss), 6), "scaling": "weak"}
+           "loss": round(float(loss), 6), "scaling": "weak", "dtype": args.config5_dtype}
+    if loop.grad_scaler.is_enabled():
+        res["loss_scale"] = float(loop.grad_scaler.get_scale())
     del model, loop
     torch.cuda.empty_cache()
     return res
@@ -363,6 +365,10 @@ def main():
                                                             "timed steps (0 = skip)")
     ap.add_argument("--train5", type=int, default=3, help="config-5 training side figure (224^3, 2-level "
                                                           "wavelets + FATS): timed steps (0 = skip)")
+    ap.add_argument("--config5-dtype", default="fp16", help="compute dtype of the config-5 legs (BASELINE.json "
+                                                            "config 5: fp16)")
+    ap.add_argument("--fp16", type=int, default=5, help="also time K config-2 steps with the U-Net in fp16 "
+                                                        "(0 = skip)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the rank launch / barrier / max-over-ranks plumbing only")
     args = ap.parse_args()
@@ -527,6 +533,21 @@ def main():
                 "steps": args.fp32, "mfma_frac_of_fp32_peak": round(step_flops * args.fp32 / tf / 1e12 / F32_PEAK_TFLOPS, 4)}
         torch.cuda.empty_cache()
 
+    # fp16 mode: the same config-2 step with 16-bit IEEE half activations and
+    # weights (fp32 accumulation, statistics and diffusion state), the
+    # finer-mantissa alternative to bf16 at the same MFMA rate
+    fp16 = None
+    if args.fp16 and args.dtype != "fp16":
+        model.set_compute_dtype("fp16")
+        lf = diffusion._native_loop(model, x_T, list(range(T))[::-1][:args.fp16 + 3], cond, True,
+                                    graph=bool(args.graph), fresh_outputs=False, need_pred=False)
+        tf = max_over_ranks(time_loop(lf, (2, args.fp16), world, sync))
+        lf.close()
+        model.set_compute_dtype(args.dtype)
+        fp16 = {"denoising_steps_per_s": round(world * args.fp16 / tf, 3), "ms_per_step": round(1000 * tf / args.fp16, 3),
+                "steps": args.fp16, "mfma_frac": round(step_flops * args.fp16 / tf / 1e12 / BF16_PEAK_TFLOPS, 4)}
+        torch.cuda.empty_cache()
+
     # snapshot for the CPU baseline before the training leg moves the weights
     cpu_state = None
     if rank == 0 and world == 1 and args.cpu_baseline:
@@ -562,7 +583,7 @@ def main():
 
     ms_per_step = 1000.0 * elapsed / args.steps
     value = world * args.steps / elapsed
-    peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
+    peak = F32_PEAK_TFLOPS if args.dtype == "fp32" else BF16_PEAK_TFLOPS   # fp16 MFMA: the bf16 rate
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
     res = {
         "metric": "denoising-steps/sec on 8-ch 128^3 volumes (1000-step DDPM, i2i cWDM)",
@@ -587,6 +608,7 @@ def main():
         "fast_ddpm_sampled10": fast10,
         "batched_serving": batched,
         "fp32_parity_mode": fp32,
+        "fp16_mode": fp16,
         "train_ddp": train,
         "config5_224": config5,
         "train_config5_224": train5,

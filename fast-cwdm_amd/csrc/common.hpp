@@ -62,6 +62,11 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// ---- fp16 (IEEE binary16, storage = _Float16) --------------------------------
+typedef _Float16 f16_t;
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
 template <typename T> struct Elem;
 template <> struct Elem<float> {
   static constexpr int kDtype = CWDM_F32;
@@ -74,6 +79,48 @@ template <> struct Elem<bf16_t> {
   __device__ __forceinline__ static float to_f(bf16_t v) { return bf2f(v); }
   __device__ __forceinline__ static bf16_t from_f(float v) { return f2bf(v); }
 };
+template <> struct Elem<f16_t> {
+  static constexpr int kDtype = CWDM_F16;
+  __device__ __forceinline__ static float to_f(f16_t v) { return (float)v; }
+  __device__ __forceinline__ static f16_t from_f(float v) { return (f16_t)v; }  // round to nearest even
+};
+
+// ---- 16-bit pairs in one 32-bit word (element 0 in the low half) -------------
+// the bf16 forms are the bit tricks the kernels used from the start; the fp16
+// forms convert (v_cvt_f32_f16 / a packed round-to-nearest-even convert)
+template <typename T> __device__ __forceinline__ float lo2f(unsigned u);
+template <typename T> __device__ __forceinline__ float hi2f(unsigned u);
+template <> __device__ __forceinline__ float lo2f<bf16_t>(unsigned u) { return __uint_as_float(u << 16); }
+template <> __device__ __forceinline__ float hi2f<bf16_t>(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+template <> __device__ __forceinline__ float lo2f<f16_t>(unsigned u) {
+  return (float)__builtin_bit_cast(f16_t, (unsigned short)(u & 0xffffu));
+}
+template <> __device__ __forceinline__ float hi2f<f16_t>(unsigned u) {
+  return (float)__builtin_bit_cast(f16_t, (unsigned short)(u >> 16));
+}
+template <typename T> __device__ __forceinline__ unsigned pack2(float a, float b);
+template <> __device__ __forceinline__ unsigned pack2<bf16_t>(float a, float b) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_t));
+}
+template <> __device__ __forceinline__ unsigned pack2<f16_t>(float a, float b) {
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, f16x2_t));
+}
+
+// storage dtype <-> element size / K chunk (32 bytes of input channels per voxel)
+inline int dtype_size(int dtype) { return dtype == CWDM_F32 ? 4 : 2; }
+inline bool dtype_half(int dtype) { return dtype == CWDM_BF16 || dtype == CWDM_F16; }
+inline bool dtype_compute(int dtype) { return dtype == CWDM_F32 || dtype == CWDM_BF16 || dtype == CWDM_F16; }
+
+// host dispatch over the three compute dtypes: f(T{}) with T = float / bf16_t / f16_t
+template <typename F>
+inline int dispatch_dtype(int dtype, F&& f) {
+  if (dtype == CWDM_BF16) return f(bf16_t{});
+  if (dtype == CWDM_F16) return f(f16_t{});
+  return f(float{});
+}
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

@@ -15,6 +15,14 @@ extern template int launch_wide<bf16_t, 2>(const ConvParams&, hipStream_t);
 extern template int launch_conv<bf16_t, 32, 4, 2, 2>(const ConvParams&, hipStream_t);
 extern template int launch_conv<bf16_t, 16, 4, 4, 2>(const ConvParams&, hipStream_t);
 extern template int launch_conv<bf16_t, 8, 8, 4, 2>(const ConvParams&, hipStream_t);
+extern template int launch_wide<f16_t, 1>(const ConvParams&, hipStream_t);
+extern template int launch_conv<f16_t, 32, 4, 2, 1>(const ConvParams&, hipStream_t);
+extern template int launch_conv<f16_t, 16, 4, 4, 1>(const ConvParams&, hipStream_t);
+extern template int launch_conv<f16_t, 8, 8, 4, 1>(const ConvParams&, hipStream_t);
+extern template int launch_wide<f16_t, 2>(const ConvParams&, hipStream_t);
+extern template int launch_conv<f16_t, 32, 4, 2, 2>(const ConvParams&, hipStream_t);
+extern template int launch_conv<f16_t, 16, 4, 4, 2>(const ConvParams&, hipStream_t);
+extern template int launch_conv<f16_t, 8, 8, 4, 2>(const ConvParams&, hipStream_t);
 extern template int launch_wide<float, 1>(const ConvParams&, hipStream_t);
 extern template int launch_conv<float, 32, 4, 2, 1>(const ConvParams&, hipStream_t);
 extern template int launch_conv<float, 16, 4, 4, 1>(const ConvParams&, hipStream_t);
@@ -85,7 +93,7 @@ inline int pick_ksplit(long long nblk, int total_chunks) {
   return (total_chunks + per - 1) / per;
 }
 
-int ck_of(int dtype) { return dtype == CWDM_BF16 ? 16 : 8; }
+int ck_of(int dtype) { return 32 / dtype_size(dtype); }
 
 }  // namespace cwdm
 
@@ -98,7 +106,8 @@ extern "C" int64_t cwdm_conv3d_packed_bytes(int cout, int cin, int ksize, int dt
   const int NT = 32 * pick_nf(cout);
   const int nct = (int)ceil_div(cout, NT);
   const int ntaps = ksize * ksize * ksize;
-  const int esz = dtype == CWDM_BF16 ? 2 : 4;
+  if (!dtype_compute(dtype)) return -1;
+  const int esz = dtype_size(dtype);
   return (int64_t)nct * (cin / ck) * ntaps * NT * ck * esz;
 }
 
@@ -129,7 +138,7 @@ static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, vo
                      cwdm_stream_t stream, int s2_ci0) {
   CWDM_REQUIRE(w && packed, CWDM_E_INVALID, "cwdm_conv3d_pack: null pointer");
   CWDM_REQUIRE(ksize == 1 || ksize == 3, CWDM_E_UNSUPPORTED, "cwdm_conv3d_pack: kernel size must be 1 or 3");
-  CWDM_REQUIRE(dtype == CWDM_F32 || dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_conv3d_pack: bad dtype");
+  CWDM_REQUIRE(dtype_compute(dtype), CWDM_E_INVALID, "cwdm_conv3d_pack: bad dtype");
   const int ck = ck_of(dtype);
   const int cin_real = cin;
   if (transpose) cin = (int)ceil_div(cin, ck) * ck;
@@ -140,14 +149,13 @@ static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, vo
   const int ntaps = ksize * ksize * ksize;
   const long long total = (long long)nct * (cin / ck) * ntaps * NT * ck;
   dim3 grid((unsigned)ceil_div(total, 256));
-  if (dtype == CWDM_BF16)
-    hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, w, cout, cin, ntaps, NT, nct,
-                       reinterpret_cast<bf16_t*>(packed), transpose, cin_real, s2_ci0);
-  else
-    hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, w, cout, cin, ntaps, NT, nct,
-                       reinterpret_cast<float*>(packed), transpose, cin_real, s2_ci0);
-  CWDM_LAUNCHED();
-  return CWDM_OK;
+  return dispatch_dtype(dtype, [&](auto tag) -> int {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(pack_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, w, cout, cin, ntaps, NT, nct,
+                       reinterpret_cast<T*>(packed), transpose, cin_real, s2_ci0);
+    CWDM_LAUNCHED();
+    return CWDM_OK;
+  });
 }
 
 namespace {
@@ -190,7 +198,7 @@ extern "C" int64_t cwdm_conv3d_parts(int dtype, int64_t D, int64_t H, int64_t W,
 extern "C" int cwdm_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream) {
   CWDM_REQUIRE(d && d->out && (d->a_w || d->b_w), CWDM_E_INVALID, "cwdm_conv3d_forward: null pointer");
   CWDM_REQUIRE(!d->a_w || (d->a0 && d->a_c0 > 0), CWDM_E_INVALID, "cwdm_conv3d_forward: segment A input missing");
-  CWDM_REQUIRE(d->dtype == CWDM_F32 || d->dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_conv3d_forward: bad dtype");
+  CWDM_REQUIRE(dtype_compute(d->dtype), CWDM_E_INVALID, "cwdm_conv3d_forward: bad dtype");
   CWDM_REQUIRE(d->B > 0 && d->D > 0 && d->H > 0 && d->W > 0 && d->cout > 0, CWDM_E_SHAPE,
                "cwdm_conv3d_forward: empty shape");
   const int ck = ck_of(d->dtype);
@@ -246,8 +254,9 @@ int cwdm::legacy_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream)
     p.partial = reinterpret_cast<float*>(d->workspace);
   }
   hipStream_t s = (hipStream_t)stream;
-  if (d->dtype == CWDM_BF16)
-    return nf == 2 ? dispatch_brick<bf16_t, 2>(p, br, s) : dispatch_brick<bf16_t, 1>(p, br, s);
-  return nf == 2 ? dispatch_brick<float, 2>(p, br, s) : dispatch_brick<float, 1>(p, br, s);
+  return dispatch_dtype(d->dtype, [&](auto tag) -> int {
+    using T = decltype(tag);
+    return nf == 2 ? dispatch_brick<T, 2>(p, br, s) : dispatch_brick<T, 1>(p, br, s);
+  });
 }
 

@@ -4,7 +4,7 @@
 //
 // The general kernels tile 32 / 64 output channels per MFMA; with 8 outputs
 // that wastes 4-8x of the matrix work and the head ran at ~130 TF/s
-// (~0.55 ms of the 128^3 step).  Here the MFMA is v_mfma_f32_16x16x32_bf16
+// (~0.55 ms of the 128^3 step).  Here the MFMA is v_mfma_f32_16x16x32_bf16 (/ _f16)
 // with A = 16 voxels x 32 input channels (from LDS) and B = 32 input channels
 // x 16 output channels (8 real + zero rows, held in registers per tap): half
 // the lanes of the product are useful instead of an eighth.
@@ -28,7 +28,7 @@ namespace cwdm {
 struct HeadParams {
   int B, D, H, W, C, cout;
   int tx, ty, tz;
-  const bf16_t* x;          // [B][V][C] channels-last
+  const void* x;            // [B][V][C] channels-last, bf16 or fp16
   const float* gn;          // [B][C][2] scale / shift (null: no GroupNorm+SiLU)
   const unsigned char* w;   // packed, NT = 32
   const float* bias; long long bias_bs;
@@ -43,6 +43,17 @@ constexpr int HEAD_LDS = HHV * 64;                                 // 78336 B
 typedef __bf16 hbf16x8 __attribute__((ext_vector_type(8)));
 typedef float hf32x4 __attribute__((ext_vector_type(4)));
 
+__device__ __forceinline__ hf32x4 head_mfma(const u32x4& a, const u32x4& b, hf32x4 acc, bf16_t*) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hbf16x8, a), __builtin_bit_cast(hbf16x8, b), acc,
+                                                 0, 0, 0);
+}
+__device__ __forceinline__ hf32x4 head_mfma(const u32x4& a, const u32x4& b, hf32x4 acc, f16_t*) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), acc, 0,
+                                                0, 0);
+}
+
+// T: the 16-bit storage type (bf16 / fp16)
+template <typename T>
 __global__ void __launch_bounds__(256, 2) head_conv_kernel(HeadParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char halo[HEAD_LDS];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -87,7 +98,7 @@ __global__ void __launch_bounds__(256, 2) head_conv_kernel(HeadParams p) {
       v[k] = u32x4{0u, 0u, 0u, 0u};
       if (ok[k]) {
         const long long vox = (long long)b * V + ((long long)oz * p.H + oy) * p.W + ox;
-        v[k] = *reinterpret_cast<const u32x4*>(p.x + vox * p.C + cq);
+        v[k] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(p.x) + vox * p.C + cq);
       }
     }
 #pragma unroll
@@ -97,10 +108,10 @@ __global__ void __launch_bounds__(256, 2) head_conv_kernel(HeadParams p) {
         u32x4 q = u32x4{0u, 0u, 0u, 0u};
         if (ok[k]) {
           float f[8];
-          unpack<bf16_t>(v[k], f);
+          unpack<T>(v[k], f);
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] = p.gn ? silu(f[e] * sc[e] + sh[e]) : f[e];
-          q = pack<bf16_t>(f);
+          q = pack<T>(f);
         }
         *reinterpret_cast<u32x4*>(halo + (i >> 2) * 64 + fq * 16) = q;
       }
@@ -126,13 +137,11 @@ __global__ void __launch_bounds__(256, 2) head_conv_kernel(HeadParams p) {
           a[L][xb] = *reinterpret_cast<const u32x4*>(halo + abase + (((dz * HHY) + L) * HHX + xb * 16 + dx) * 64);
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy) {
-        const hbf16x8 wb = __builtin_bit_cast(hbf16x8, wr[dz * 9 + dy * 3 + dx]);
+        const u32x4 wb = wr[dz * 9 + dy * 3 + dx];
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
-          for (int xb = 0; xb < 2; ++xb)
-            acc[m][xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hbf16x8, a[m + dy][xb]), wb,
-                                                                 acc[m][xb], 0, 0, 0);
+          for (int xb = 0; xb < 2; ++xb) acc[m][xb] = head_mfma(a[m + dy][xb], wb, acc[m][xb], (T*)nullptr);
       }
     }
   }
@@ -149,7 +158,7 @@ __global__ void __launch_bounds__(256, 2) head_conv_kernel(HeadParams p) {
               (long long)b * V + ((long long)(z0 + wv) * p.H + y0 + m) * p.W + x0 + xb * 16 + 4 * kg + i;
           const float r = acc[m][xb][i] + bn;
           if (p.out_f32) reinterpret_cast<float*>(p.out)[vox * p.cout + n] = r;
-          else reinterpret_cast<bf16_t*>(p.out)[vox * p.cout + n] = f2bf(r);
+          else reinterpret_cast<T*>(p.out)[vox * p.cout + n] = Elem<T>::from_f(r);
         }
   }
 }
@@ -160,7 +169,7 @@ extern std::atomic<int> g_conv_path;
 
 bool head_eligible(const cwdm_conv3d_desc* d) {
   if (g_conv_path.load(std::memory_order_relaxed) == 1) return false;
-  return d->dtype == CWDM_BF16 && d->a_w && d->cout <= 16 && d->a_c1 == 0 && d->a_c0 % 32 == 0 && d->a_c0 <= 256 &&
+  return dtype_half(d->dtype) && d->a_w && d->cout <= 16 && d->a_c1 == 0 && d->a_c0 % 32 == 0 && d->a_c0 <= 256 &&
          d->a_mode == 0 && !d->b_w && d->res_mode < 0 && !d->stats && !d->out1 && !d->accumulate &&
          d->W % 32 == 0 && d->H % 4 == 0 && d->D % 4 == 0;
 }
@@ -169,7 +178,7 @@ int head_conv_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   HeadParams p{};
   p.B = (int)d->B; p.D = (int)d->D; p.H = (int)d->H; p.W = (int)d->W; p.C = d->a_c0; p.cout = d->cout;
   p.tx = p.W / 32; p.ty = p.H / 4; p.tz = p.D / 4;
-  p.x = reinterpret_cast<const bf16_t*>(d->a0);
+  p.x = d->a0;
   p.gn = d->a_gn;
   p.w = reinterpret_cast<const unsigned char*>(d->a_w);
   p.bias = d->bias; p.bias_bs = d->bias_bstride;
@@ -177,7 +186,8 @@ int head_conv_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   const long long nblk = (long long)p.B * p.tx * p.ty * p.tz;
   CWDM_REQUIRE(nblk < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d head: grid too large");
   prof_begin(s);
-  hipLaunchKernelGGL(head_conv_kernel, dim3((unsigned)nblk), dim3(256), 0, s, p);
+  if (d->dtype == CWDM_F16) hipLaunchKernelGGL(head_conv_kernel<f16_t>, dim3((unsigned)nblk), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(head_conv_kernel<bf16_t>, dim3((unsigned)nblk), dim3(256), 0, s, p);
   prof_end(s, 2.0 * p.B * p.D * p.H * p.W * (double)p.cout * 27.0 * p.C);
   CWDM_LAUNCHED();
   return CWDM_OK;

@@ -23,8 +23,9 @@
 //   * epilogue: accumulators -> LDS (fp32) -> row-major, + per-(b, c) bias,
 //     + residual (same / upsampled / pooled), store, and per-tile per-channel
 //     (sum, sum^2) partials for the next GroupNorm.
-// bf16 uses v_mfma_f32_32x32x16_bf16; fp32 (parity mode) uses exact-f32
-// v_mfma_f32_32x32x2_f32.  Accumulation is fp32 in both.
+// bf16 uses v_mfma_f32_32x32x16_bf16, fp16 v_mfma_f32_32x32x16_f16 (same rate);
+// fp32 (parity mode) uses exact-f32 v_mfma_f32_32x32x2_f32.  Accumulation is
+// fp32 in all three.
 #include "common.hpp"
 
 namespace cwdm {
@@ -51,6 +52,7 @@ struct ConvParams {
 
 template <typename T> struct ConvTr;
 template <> struct ConvTr<bf16_t> { static constexpr int CK = 16; static constexpr int EPQ = 8; };
+template <> struct ConvTr<f16_t> { static constexpr int CK = 16; static constexpr int EPQ = 8; };
 template <> struct ConvTr<float> { static constexpr int CK = 8; static constexpr int EPQ = 4; };
 
 // SiLU with the hardware exp2 / reciprocal (1-2 ulp; the reference's fp32 SiLU is
@@ -72,6 +74,14 @@ __device__ __forceinline__ void unpack<bf16_t>(const u32x4& q, float* f) {
   }
 }
 template <>
+__device__ __forceinline__ void unpack<f16_t>(const u32x4& q, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = lo2f<f16_t>(q[i]);
+    f[2 * i + 1] = hi2f<f16_t>(q[i]);
+  }
+}
+template <>
 __device__ __forceinline__ void unpack<float>(const u32x4& q, float* f) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) f[i] = __uint_as_float(q[i]);
@@ -86,11 +96,35 @@ __device__ __forceinline__ u32x4 pack<bf16_t>(const float* f) {
   return q;
 }
 template <>
+__device__ __forceinline__ u32x4 pack<f16_t>(const float* f) {
+  u32x4 q;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = pack2<f16_t>(f[2 * i], f[2 * i + 1]);
+  return q;
+}
+template <>
 __device__ __forceinline__ u32x4 pack<float>(const float* f) {
   u32x4 q;
 #pragma unroll
   for (int i = 0; i < 4; ++i) q[i] = __float_as_uint(f[i]);
   return q;
+}
+
+// one MFMA step of K = 32 bytes per operand lane (16 bf16 / fp16 elements over
+// the lane pair, or 4 x the exact-fp32 K = 2 form): acc += A . B
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void mfma_acc(f32x16& acc, const u32x4& a, const u32x4& b, bf16_t*) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0,
+                                               0, 0);
+}
+__device__ __forceinline__ void mfma_acc(f32x16& acc, const u32x4& a, const u32x4& b, f16_t*) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), acc, 0,
+                                              0, 0);
+}
+__device__ __forceinline__ void mfma_acc(f32x16& acc, const u32x4& a, const u32x4& b, float*) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a[s]), __uint_as_float(b[s]), acc, 0, 0, 0);
 }
 
 __device__ __forceinline__ u32x4 ldg16(const void* p) { return *reinterpret_cast<const u32x4*>(p); }
@@ -444,7 +478,7 @@ __device__ __forceinline__ void epilogue_rows(const ConvParams& p, float* E, int
       }
       if (nvalid == 8) {
         if constexpr (sizeof(T) == 2) {
-          *reinterpret_cast<u32x4*>(o) = pack<bf16_t>(v);
+          *reinterpret_cast<u32x4*>(o) = pack<T>(v);
         } else {
           *reinterpret_cast<u32x4*>(o) = pack<float>(v);
           *reinterpret_cast<u32x4*>(o + 4) = pack<float>(v + 4);
@@ -642,17 +676,7 @@ __global__ void __launch_bounds__(256) conv3d_kernel(ConvParams p) {
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int n = 0; n < NF; ++n) {
-          if constexpr (sizeof(T) == 2) {
-            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, aq[m]),
-                                                                __builtin_bit_cast(bf16x8, bq[n]), acc[m][n], 0, 0, 0);
-          } else {
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(aq[m][s]), __uint_as_float(bq[n][s]),
-                                                               acc[m][n], 0, 0, 0);
-          }
-        }
+        for (int n = 0; n < NF; ++n) mfma_acc(acc[m][n], aq[m], bq[n], (T*)nullptr);
     }
     if (!has_next) break;
     __syncthreads();  // every wave is done reading this chunk's halo and weights
@@ -765,16 +789,6 @@ struct WideCfg {
   static constexpr int MAIN_B = HALO_B + 2 * WB;
   static constexpr int SMEM = MAIN_B > EPI_B ? MAIN_B : EPI_B;
 };
-
-__device__ __forceinline__ void mfma_acc(f32x16& acc, const u32x4& a, const u32x4& b, bf16_t*) {
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0,
-                                               0, 0);
-}
-__device__ __forceinline__ void mfma_acc(f32x16& acc, const u32x4& a, const u32x4& b, float*) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a[s]), __uint_as_float(b[s]), acc, 0, 0, 0);
-}
 
 template <int G, int NI, typename SG>
 __device__ __forceinline__ void transform_group(SG* sg) {

@@ -1,5 +1,5 @@
 // Conv3d 3x3x3 (stride 1, pad 1) for the small-grid U-Net levels (16^3, 8^3:
-// W = 16 or 8), bf16, on v_mfma_f32_16x16x32_bf16.  Same contract as the
+// W = 16 or 8), bf16 or fp16, on v_mfma_f32_16x16x32_{bf16,f16}.  Same contract as the
 // DMA-staged wide-grid kernel (V4Params: GroupNorm+SiLU and the 1x1 skip are
 // pre-passes in conv3d_v4_forward; this kernel stages raw copies), called from
 // v4_launch for shapes sg_eligible() accepts.
@@ -84,14 +84,19 @@ struct SGParams {
 thread_local unsigned* g_sg_sync = nullptr;
 constexpr int64_t kSgSyncWords = 1 << 16;   // tiles of one K-split launch (sg_split_for keeps tiles * S below)
 
-__device__ __forceinline__ void sg_mfma(sg_f32x4& acc, const u32x4& a, const u32x4& b) {
+__device__ __forceinline__ void sg_mfma(sg_f32x4& acc, const u32x4& a, const u32x4& b, bf16_t*) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0,
                                                 0, 0);
 }
+__device__ __forceinline__ void sg_mfma(sg_f32x4& acc, const u32x4& a, const u32x4& b, f16_t*) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), acc, 0, 0,
+                                               0);
+}
 
 // TAPS = 27: the 3x3x3 conv; TAPS = 1: the 1x1 skip conv of a ResBlock (the
-// centre tap of the same halo image and weight buffer, packed with k = 1)
-template <int BX, int BY, int MODE, int TAPS>
+// centre tap of the same halo image and weight buffer, packed with k = 1).
+// T: the 16-bit storage type (bf16 or fp16; v_mfma_f32_16x16x32_{bf16,f16})
+template <typename T, int BX, int BY, int MODE, int TAPS>
 __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   static_assert(TAPS == 27 || TAPS == 1, "3x3x3 or 1x1");
   constexpr int PAD = TAPS == 27 ? 1 : 0;
@@ -224,12 +229,12 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-          for (int m = 0; m < 4; ++m) sg_mfma(acc[m], aw[g & 1][dy], av[g & 1][m * C::LPO + dy]);
+          for (int m = 0; m < 4; ++m) sg_mfma(acc[m], aw[g & 1][dy], av[g & 1][m * C::LPO + dy], (T*)nullptr);
         __builtin_amdgcn_sched_barrier(0);
       }
     } else {
 #pragma unroll
-      for (int m = 0; m < 4; ++m) sg_mfma(acc[m], aw[0][0], av[0][m * C::LPO]);
+      for (int m = 0; m < 4; ++m) sg_mfma(acc[m], aw[0][0], av[0][m * C::LPO], (T*)nullptr);
     }
     if (has_next) {
       // the next chunk's halo and weights have landed; every wave is past this
@@ -291,7 +296,7 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
       long long rvox = ((long long)b * p.D + oz) * HW + (long long)oy * p.W + ox;
       if (p.rmode == 1)
         rvox = (((long long)b * (p.D >> 1) + (oz >> 1)) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1);
-      rq[m] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.res) + rvox * p.cout + co);
+      rq[m] = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(p.res) + rvox * p.cout + co);
     }
   }
 #pragma unroll
@@ -302,8 +307,8 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = acc[m][i];
     if (p.rmode >= 0) {
-      v[0] += __uint_as_float(rq[m].x << 16); v[1] += __uint_as_float(rq[m].x & 0xffff0000u);
-      v[2] += __uint_as_float(rq[m].y << 16); v[3] += __uint_as_float(rq[m].y & 0xffff0000u);
+      v[0] += lo2f<T>(rq[m].x); v[1] += hi2f<T>(rq[m].x);
+      v[2] += lo2f<T>(rq[m].y); v[3] += hi2f<T>(rq[m].y);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -311,9 +316,9 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
       ssq[i] += v[i] * v[i];
     }
     uint2 sq;
-    sq.x = pack_bf16x2(v[0], v[1]);
-    sq.y = pack_bf16x2(v[2], v[3]);
-    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + vox * p.cout + co) = sq;
+    sq.x = pack2<T>(v[0], v[1]);
+    sq.y = pack2<T>(v[2], v[3]);
+    *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.out) + vox * p.cout + co) = sq;
   }
   if (p.stats) {
     // rows of 16 lanes hold 4 channels for 16 voxels: DPP row sums, then the 4
@@ -347,19 +352,25 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   }
 }
 
-template __global__ void conv3d_sg_kernel<16, 4, 0, 27>(SGParams);
-template __global__ void conv3d_sg_kernel<16, 4, 1, 27>(SGParams);
-template __global__ void conv3d_sg_kernel<16, 4, 0, 1>(SGParams);
-template __global__ void conv3d_sg_kernel<8, 8, 0, 27>(SGParams);
-template __global__ void conv3d_sg_kernel<8, 8, 1, 27>(SGParams);
-template __global__ void conv3d_sg_kernel<8, 8, 0, 1>(SGParams);
+template __global__ void conv3d_sg_kernel<bf16_t, 16, 4, 0, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<bf16_t, 16, 4, 1, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<bf16_t, 16, 4, 0, 1>(SGParams);
+template __global__ void conv3d_sg_kernel<bf16_t, 8, 8, 0, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<bf16_t, 8, 8, 1, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<bf16_t, 8, 8, 0, 1>(SGParams);
+template __global__ void conv3d_sg_kernel<f16_t, 16, 4, 0, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<f16_t, 16, 4, 1, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<f16_t, 16, 4, 0, 1>(SGParams);
+template __global__ void conv3d_sg_kernel<f16_t, 8, 8, 0, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<f16_t, 8, 8, 1, 27>(SGParams);
+template __global__ void conv3d_sg_kernel<f16_t, 8, 8, 0, 1>(SGParams);
 
 extern std::atomic<int> g_conv_path;
 
 namespace {
 bool sg_shape_ok(const cwdm_conv3d_desc* d) {
   if (g_conv_path.load(std::memory_order_relaxed) == 1) return false;
-  if (d->dtype != CWDM_BF16 || d->out_dtype != CWDM_BF16 || d->accumulate || d->out1 || d->cout % 64) return false;
+  if (!dtype_half(d->dtype) || d->out_dtype != d->dtype || d->accumulate || d->out1 || d->cout % 64) return false;
   return (d->W == 16 && d->H % 4 == 0 && d->D % 4 == 0) || (d->W == 8 && d->H % 8 == 0 && d->D % 4 == 0);
 }
 }  // namespace
@@ -428,21 +439,27 @@ int sg_counters(SGParams& q, void* own, hipStream_t s) {
   return CWDM_OK;
 }
 
-int sg_go(const SGParams& q, const cwdm_conv3d_desc* d, int taps, double flops, hipStream_t s) {
+template <typename T>
+void sg_go_t(const SGParams& q, const cwdm_conv3d_desc* d, int taps, hipStream_t s) {
   const dim3 grid((unsigned)(d->B * q.parts * q.ntile16 * q.ksplit));
-  prof_begin(s);
   if (d->W == 8 && taps == 1) {
-    hipLaunchKernelGGL((conv3d_sg_kernel<8, 8, 0, 1>), grid, dim3(256), 0, s, q);
+    hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 0, 1>), grid, dim3(256), 0, s, q);
   } else if (d->W == 8) {
-    if (q.v.amode == 1) hipLaunchKernelGGL((conv3d_sg_kernel<8, 8, 1, 27>), grid, dim3(256), 0, s, q);
-    else hipLaunchKernelGGL((conv3d_sg_kernel<8, 8, 0, 27>), grid, dim3(256), 0, s, q);
+    if (q.v.amode == 1) hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 1, 27>), grid, dim3(256), 0, s, q);
+    else hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 0, 27>), grid, dim3(256), 0, s, q);
   } else if (taps == 1) {
-    hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 0, 1>), grid, dim3(256), 0, s, q);
+    hipLaunchKernelGGL((conv3d_sg_kernel<T, 16, 4, 0, 1>), grid, dim3(256), 0, s, q);
   } else if (q.v.amode == 1) {
-    hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 1, 27>), grid, dim3(256), 0, s, q);
+    hipLaunchKernelGGL((conv3d_sg_kernel<T, 16, 4, 1, 27>), grid, dim3(256), 0, s, q);
   } else {
-    hipLaunchKernelGGL((conv3d_sg_kernel<16, 4, 0, 27>), grid, dim3(256), 0, s, q);
+    hipLaunchKernelGGL((conv3d_sg_kernel<T, 16, 4, 0, 27>), grid, dim3(256), 0, s, q);
   }
+}
+
+int sg_go(const SGParams& q, const cwdm_conv3d_desc* d, int taps, double flops, hipStream_t s) {
+  prof_begin(s);
+  if (d->dtype == CWDM_F16) sg_go_t<f16_t>(q, d, taps, s);
+  else sg_go_t<bf16_t>(q, d, taps, s);
   prof_end(s, flops);
   CWDM_LAUNCHED();
   return CWDM_OK;

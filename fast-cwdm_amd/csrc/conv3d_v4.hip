@@ -17,6 +17,12 @@ template __global__ void conv3d_v4_kernel<bf16_t, 1, true, true>(V4Params);
 template __global__ void conv3d_v4_kernel<bf16_t, 1, true>(V4Params);
 template __global__ void conv3d_v4_kernel<bf16_t, 0, false>(V4Params);
 template __global__ void conv3d_v4_kernel<bf16_t, 1, false>(V4Params);
+template __global__ void conv3d_v4_kernel<f16_t, 0, true>(V4Params);
+template __global__ void conv3d_v4_kernel<f16_t, 0, true, true>(V4Params);
+template __global__ void conv3d_v4_kernel<f16_t, 1, true, true>(V4Params);
+template __global__ void conv3d_v4_kernel<f16_t, 1, true>(V4Params);
+template __global__ void conv3d_v4_kernel<f16_t, 0, false>(V4Params);
+template __global__ void conv3d_v4_kernel<f16_t, 1, false>(V4Params);
 template __global__ void conv3d_v4_kernel<float, 0, false>(V4Params);
 template __global__ void conv3d_v4_kernel<float, 1, false>(V4Params);
 
@@ -53,7 +59,7 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x0,
     vs[k] = v;
     const T* src = xs + (size_t)v * xc;
     if constexpr (sizeof(T) == 2) {
-      unpack<bf16_t>(*reinterpret_cast<const u32x4*>(src), xv[k]);
+      unpack<T>(*reinterpret_cast<const u32x4*>(src), xv[k]);
     } else {
       unpack<float>(*reinterpret_cast<const u32x4*>(src), xv[k]);
       unpack<float>(*reinterpret_cast<const u32x4*>(src + 4), xv[k] + 4);
@@ -81,7 +87,7 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x0,
     T* dst = cm ? out + ((size_t)(b * (unsigned)(C / CK) + (unsigned)(c / CK)) * dvpb.d + (v - b * dvpb.d)) * CK + (c % CK)
                 : out + (size_t)v * C + c;
     if constexpr (sizeof(T) == 2) {
-      *reinterpret_cast<u32x4*>(dst) = pack<bf16_t>(y);
+      *reinterpret_cast<u32x4*>(dst) = pack<T>(y);
     } else {
       *reinterpret_cast<u32x4*>(dst) = pack<float>(y);
       *reinterpret_cast<u32x4*>(dst + 4) = pack<float>(y + 4);
@@ -131,7 +137,7 @@ int64_t v4_ksplit_target() {
 // level): enough K slices for ~512 work items, at least two chunks per slice
 int v4_ksplit(const cwdm_conv3d_desc* d) {
   if (sg_eligible(d)) return sg_ksplit(d);  // the small-grid kernel's own K split (8^3 level)
-  const int ck = d->dtype == CWDM_BF16 ? 16 : 8;
+  const int ck = 32 / dtype_size(d->dtype);
   const int nch = (d->a_c0 + d->a_c1) / ck;
   const int64_t nblk = v4_items(d);
   const int64_t target = v4_ksplit_target();
@@ -146,7 +152,7 @@ bool v4_eligible(const cwdm_conv3d_desc* d) {
   const int path = g_conv_path.load(std::memory_order_relaxed);
   if (path == 1) return false;
   if (sg_eligible(d)) return true;  // 16^3 / 8^3 levels: conv3d_sg.hip behind the same pre-passes
-  if (d->dtype != CWDM_BF16 && d->dtype != CWDM_F32) return false;
+  if (!dtype_compute(d->dtype)) return false;
   // W >= 32: the statistics partials follow cwdm_conv3d_parts' 32-wide x tiles (pick_brick)
   if (!d->a_w || d->W < 32 || d->H % 4 || d->D % 4 || d->cout % 64) return false;
   if (d->a_mode != 0 && d->a_mode != 1) return false;
@@ -154,7 +160,7 @@ bool v4_eligible(const cwdm_conv3d_desc* d) {
   if (d->out1 && d->out_c0 % 8) return false;
   const int64_t nblk = v4_items(d);
   if (nblk * v4_ksplit(d) < std::min<int64_t>(384, v4_ksplit_target()) && path != 2) return false;  // too few work items even K-split: the brick kernels
-  const int esz = d->dtype == CWDM_BF16 ? 2 : 4;
+  const int esz = dtype_size(d->dtype);
   const int64_t sv = src_voxels(d);
   // the DMA range check works on 32-bit byte offsets per batch
   const int64_t lim = 0xFFFFE000LL;
@@ -163,7 +169,7 @@ bool v4_eligible(const cwdm_conv3d_desc* d) {
 }
 
 int64_t v4_workspace_bytes(const cwdm_conv3d_desc* d) {
-  const int esz = d->dtype == CWDM_BF16 ? 2 : 4;
+  const int esz = dtype_size(d->dtype);
   int64_t ws = 0;
   if (d->a_gn) ws += align256(d->B * src_voxels(d) * (d->a_c0 + d->a_c1) * esz);
   if (d->b_w) ws += align256(d->B * d->D * d->H * d->W * d->cout * esz);
@@ -190,16 +196,14 @@ int gn_apply(const void* x0, int c0, const void* x1, int c1, const float* gn, in
   const int64_t nvox = B * vpb, nq = ceil_div(nvox, VPT);
   const dim3 grid((unsigned)ceil_div(nq * G8, 256));
   const FastDiv dvpb = make_fastdiv((unsigned)vpb), dg8 = make_fastdiv((unsigned)G8);
-  if (dtype == CWDM_BF16)
-    hipLaunchKernelGGL((gn_apply_kernel<bf16_t, VPT>), grid, dim3(256), 0, s, reinterpret_cast<const bf16_t*>(x0), c0,
-                       reinterpret_cast<const bf16_t*>(x1), c1, gn, dvpb, dg8, (unsigned)nvox, (unsigned)nq,
-                       reinterpret_cast<bf16_t*>(out), cm);
-  else
-    hipLaunchKernelGGL((gn_apply_kernel<float, VPT>), grid, dim3(256), 0, s, reinterpret_cast<const float*>(x0), c0,
-                       reinterpret_cast<const float*>(x1), c1, gn, dvpb, dg8, (unsigned)nvox, (unsigned)nq,
-                       reinterpret_cast<float*>(out), cm);
-  CWDM_LAUNCHED();
-  return CWDM_OK;
+  return dispatch_dtype(dtype, [&](auto tag) -> int {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((gn_apply_kernel<T, VPT>), grid, dim3(256), 0, s, reinterpret_cast<const T*>(x0), c0,
+                       reinterpret_cast<const T*>(x1), c1, gn, dvpb, dg8, (unsigned)nvox, (unsigned)nq,
+                       reinterpret_cast<T*>(out), cm);
+    CWDM_LAUNCHED();
+    return CWDM_OK;
+  });
 }
 
 // launch of the DMA-staged kernel on prepared sources: a0 (c0 channels,
@@ -207,8 +211,8 @@ int gn_apply(const void* x0, int c0, const void* x1, int c1, const float* gn, in
 // partial: fp32 scratch of v4_ksplit(d) output slices (unused without a K split)
 int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
               const void* res, int rmode, void* partial, hipStream_t s) {
-  const int esz = d->dtype == CWDM_BF16 ? 2 : 4;
-  const int ck = d->dtype == CWDM_BF16 ? 16 : 8;
+  const int esz = dtype_size(d->dtype);
+  const int ck = 32 / esz;
   const int64_t SV = src_voxels(d);
   V4Params p{};
   p.B = (int)d->B; p.D = (int)d->D; p.H = (int)d->H; p.W = (int)d->W;
@@ -243,7 +247,7 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   // fewer 64-channel tiles than CUs (the 32^3 level): 32-channel tiles, one
   // z-plane per wave (twice the work items; the statistics bricks are the same)
   static const bool ct32_on = [] { const char* e = std::getenv("CWDM_V4_CT32"); return !(e && e[0] == '0'); }();
-  const bool ct32 = ct32_on && d->dtype == CWDM_BF16 && S == 1 && !p.out_f32 && !p.accumulate && !p.out1 &&
+  const bool ct32 = ct32_on && dtype_half(d->dtype) && S == 1 && !p.out_f32 && !p.accumulate && !p.out1 &&
                     (long long)p.B * p.tx * p.ty * p.tz * p.nct < 256 &&
                     (long long)p.D * p.H * p.W * p.cout * 2 < 0xFFFFE000LL;
   if (ct32) p.nct = d->cout / 32;
@@ -268,17 +272,23 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   const bool fast = !p.out_f32 && !p.accumulate && !p.out1 &&
                     (long long)p.D * p.H * p.W * p.cout * 2 < 0xFFFFE000LL;
   prof_begin(s);
-  if (ct32) {
-    if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 1, true, true>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 0, true, true>), grid, dim3(256), 0, s, p);
-  } else if (d->dtype == CWDM_BF16) {
-    if (fast) {
-      if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 1, true>), grid, dim3(256), 0, s, p);
-      else hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 0, true>), grid, dim3(256), 0, s, p);
+  auto launch16 = [&](auto tag) {
+    using T = decltype(tag);
+    if (ct32) {
+      if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<T, 1, true, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((conv3d_v4_kernel<T, 0, true, true>), grid, dim3(256), 0, s, p);
+    } else if (fast) {
+      if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<T, 1, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((conv3d_v4_kernel<T, 0, true>), grid, dim3(256), 0, s, p);
     } else {
-      if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 1, false>), grid, dim3(256), 0, s, p);
-      else hipLaunchKernelGGL((conv3d_v4_kernel<bf16_t, 0, false>), grid, dim3(256), 0, s, p);
+      if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<T, 1, false>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((conv3d_v4_kernel<T, 0, false>), grid, dim3(256), 0, s, p);
     }
+  };
+  if (d->dtype == CWDM_BF16) {
+    launch16(bf16_t{});
+  } else if (d->dtype == CWDM_F16) {
+    launch16(f16_t{});
   } else {
     if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<float, 1, false>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((conv3d_v4_kernel<float, 0, false>), grid, dim3(256), 0, s, p);
@@ -304,15 +314,18 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
     q.ksplit = 1;
     q.partial = part;
     const dim3 rg((unsigned)v4_items(d));
-    if (d->dtype == CWDM_BF16) hipLaunchKernelGGL((conv3d_reduce_kernel<bf16_t, 32, 4, 4, 2>), rg, dim3(256), 0, s, q, 1);
-    else hipLaunchKernelGGL((conv3d_reduce_kernel<float, 32, 4, 4, 2>), rg, dim3(256), 0, s, q, 1);
+    dispatch_dtype(d->dtype, [&](auto tag) -> int {
+      using T = decltype(tag);
+      hipLaunchKernelGGL((conv3d_reduce_kernel<T, 32, 4, 4, 2>), rg, dim3(256), 0, s, q, 1);
+      return CWDM_OK;
+    });
     CWDM_LAUNCHED();
   }
   return CWDM_OK;
 }
 
 int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
-  const int esz = d->dtype == CWDM_BF16 ? 2 : 4;
+  const int esz = dtype_size(d->dtype);
   unsigned char* ws = reinterpret_cast<unsigned char*>(d->workspace);
   const int64_t SV = src_voxels(d);
   const void* a0 = d->a0;
@@ -464,8 +477,8 @@ __global__ void __launch_bounds__(256) gn_apply_skip_kernel(ApplySkipParams p) {
         T* o = reinterpret_cast<T*>(p.skip) + v * p.cout + f * 32 + 8 * j + 4 * hh;
         if constexpr (sizeof(T) == 2) {
           uint2 w;
-          w.x = pack_bf16x2(acc[f][4 * j], acc[f][4 * j + 1]);
-          w.y = pack_bf16x2(acc[f][4 * j + 2], acc[f][4 * j + 3]);
+          w.x = pack2<T>(acc[f][4 * j], acc[f][4 * j + 1]);
+          w.y = pack2<T>(acc[f][4 * j + 2], acc[f][4 * j + 3]);
           *reinterpret_cast<uint2*>(o) = w;
         } else {
           *reinterpret_cast<float4*>(o) = make_float4(acc[f][4 * j], acc[f][4 * j + 1], acc[f][4 * j + 2], acc[f][4 * j + 3]);
@@ -476,14 +489,14 @@ __global__ void __launch_bounds__(256) gn_apply_skip_kernel(ApplySkipParams p) {
 }
 
 int64_t apply_skip_lds_bytes(int dtype, int C, int cout, int64_t B) {
-  const int es = dtype == CWDM_BF16 ? 2 : 4;
+  const int es = dtype_size(dtype);
   return (int64_t)cout * C * es + ((B * C * 8 + 15) & ~15) + 128LL * (C * es + 16);
 }
 
 bool apply_skip_ok(int dtype, int C, int cout, int64_t B, int64_t vpb) {
-  const int ck = dtype == CWDM_BF16 ? 16 : 8;
-  const int qt = C * (dtype == CWDM_BF16 ? 2 : 4) / 32;   // prefetch registers per thread (kernel's QT)
-  return (dtype == CWDM_BF16 || dtype == CWDM_F32) && (cout == 64 || cout == 128) && vpb % 128 == 0 &&
+  const int ck = 32 / dtype_size(dtype);
+  const int qt = C * dtype_size(dtype) / 32;   // prefetch registers per thread (kernel's QT)
+  return dtype_compute(dtype) && (cout == 64 || cout == 128) && vpb % 128 == 0 &&
          C % ck == 0 && qt <= 16 && apply_skip_lds_bytes(dtype, C, cout, B) <= 160 * 1024;
 }
 
@@ -503,8 +516,10 @@ int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* g
     return CWDM_OK;
   };
   int rc;
-  if (dtype == CWDM_BF16) rc = cout == 64 ? go(gn_apply_skip_kernel<bf16_t, 2, 16>) : go(gn_apply_skip_kernel<bf16_t, 4, 16>);
-  else rc = cout == 64 ? go(gn_apply_skip_kernel<float, 2, 16>) : go(gn_apply_skip_kernel<float, 4, 16>);
+  rc = dispatch_dtype(dtype, [&](auto tag) -> int {
+    using T = decltype(tag);
+    return cout == 64 ? go(gn_apply_skip_kernel<T, 2, 16>) : go(gn_apply_skip_kernel<T, 4, 16>);
+  });
   if (rc) return rc;
   CWDM_LAUNCHED();
   return CWDM_OK;
@@ -519,7 +534,7 @@ extern "C" int cwdm_gn_apply(const void* x0, int c0, const void* x1, int c1, con
   CWDM_REQUIRE(x0 && gn && out && (c1 == 0 || x1), CWDM_E_INVALID, "cwdm_gn_apply: null pointer");
   CWDM_REQUIRE(c0 > 0 && c0 % 8 == 0 && c1 % 8 == 0 && B > 0 && voxels > 0, CWDM_E_SHAPE,
                "cwdm_gn_apply: channels must be multiples of 8");
-  CWDM_REQUIRE(dtype == CWDM_BF16 || dtype == CWDM_F32, CWDM_E_INVALID, "cwdm_gn_apply: bad dtype");
+  CWDM_REQUIRE(dtype_compute(dtype), CWDM_E_INVALID, "cwdm_gn_apply: bad dtype");
   return gn_apply(x0, c0, x1, c1, gn, B, voxels, dtype, out, (hipStream_t)stream);
 }
 

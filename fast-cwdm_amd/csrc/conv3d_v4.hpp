@@ -141,6 +141,7 @@ template <typename T, bool FAST, bool CT32 = false>
 __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][4], int b, int sl, int ct, int x0,
                                             int y0, int z0, int ks, int tid, int wv, unsigned char* smem) {
   constexpr int NPL = CT32 ? 1 : 2;
+  using T16 = std::conditional_t<sizeof(T) == 2, T, bf16_t>;   // the 16-bit storage type (bf16 / fp16)
   const int lane = tid & 63, lr = lane & 31, hh = lane >> 5;
   const int zb = CT32 ? wv : 2 * (wv >> 1);                    // the wave's first z-plane in the tile
   const int c0w = CT32 ? ct * 32 : ct * 64 + (wv & 1) * 32;    // the wave's first output channel
@@ -155,7 +156,7 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
   // voxel of (plane pl, line m) = vox0 + pl * HW + m * W
   const long long vox0 = (((long long)b * p.D + z0 + zb) * p.H + y0) * p.W + ox;
   if constexpr (FAST) {
-    // bf16 fast path: 16-byte residual loads and stores.  A lane pair (l, l+32)
+    // 16-bit fast path (bf16 / fp16): 16-byte residual loads and stores.  A lane pair (l, l+32)
     // holds channels 8j..8j+7 of one voxel split 4 / 4; v_permlane32_swap turns
     // two such groups (j, j+1) into 8 consecutive channels per lane.
     // Buffer loads / stores on per-batch resources: lanes past W get an
@@ -167,7 +168,7 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
     const int cl = c0w + 8 * hh;   // this lane's first channel (jj = 0)
     const long long V = (long long)p.D * HW;
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<bf16_t*>(p.out) + (long long)b * V * p.cout, (short)0, (int)(V * p.cout * 2), 0x00020000);
+        reinterpret_cast<T16*>(p.out) + (long long)b * V * p.cout, (short)0, (int)(V * p.cout * 2), 0x00020000);
     const unsigned vb0 = (unsigned)((((z0 + zb) * p.H) + y0) * p.W + ox);  // (plane 0, line 0) in the batch
     const unsigned rowb = (unsigned)p.W * (unsigned)p.cout * 2u, planeb = (unsigned)HW * (unsigned)p.cout * 2u;
     const unsigned obase = vb0 * (unsigned)p.cout * 2u + (unsigned)cl * 2u;
@@ -177,7 +178,7 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
       if constexpr (RES) {
         const long long rV = p.rmode == 1 ? V / 8 : V;
         const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(reinterpret_cast<const bf16_t*>(p.res) + (long long)b * rV * p.cout), (short)0,
+            (void*)(reinterpret_cast<const T16*>(p.res) + (long long)b * rV * p.cout), (short)0,
             (int)(rV * p.cout * 2), 0x00020000);
 #pragma unroll
         for (int pl = 0; pl < NPL; ++pl)
@@ -212,10 +213,10 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
               const auto s0 = __builtin_amdgcn_permlane32_swap(q[0], q[2], false, false);
               const auto s1 = __builtin_amdgcn_permlane32_swap(q[1], q[3], false, false);
               const unsigned g0 = s0[0], g1 = s1[0], h0 = s0[1], h1 = s1[1];
-              v[0] += __uint_as_float(g0 << 16); v[1] += __uint_as_float(g0 & 0xffff0000u);
-              v[2] += __uint_as_float(g1 << 16); v[3] += __uint_as_float(g1 & 0xffff0000u);
-              v[4] += __uint_as_float(h0 << 16); v[5] += __uint_as_float(h0 & 0xffff0000u);
-              v[6] += __uint_as_float(h1 << 16); v[7] += __uint_as_float(h1 & 0xffff0000u);
+              v[0] += lo2f<T16>(g0); v[1] += hi2f<T16>(g0);
+              v[2] += lo2f<T16>(g1); v[3] += hi2f<T16>(g1);
+              v[4] += lo2f<T16>(h0); v[5] += hi2f<T16>(h0);
+              v[6] += lo2f<T16>(h1); v[7] += hi2f<T16>(h1);
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
@@ -223,8 +224,8 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
               ssum[8 * jj + k] += vv;
               ssq[8 * jj + k] += vv * vv;
             }
-            const unsigned p0 = pack_bf16x2(v[0], v[1]), p1 = pack_bf16x2(v[2], v[3]);
-            const unsigned p2 = pack_bf16x2(v[4], v[5]), p3 = pack_bf16x2(v[6], v[7]);
+            const unsigned p0 = pack2<T16>(v[0], v[1]), p1 = pack2<T16>(v[2], v[3]);
+            const unsigned p2 = pack2<T16>(v[4], v[5]), p3 = pack2<T16>(v[6], v[7]);
             const auto t0 = __builtin_amdgcn_permlane32_swap(p0, p2, false, false);
             const auto t1 = __builtin_amdgcn_permlane32_swap(p1, p3, false, false);
             u32x4 w;
@@ -257,8 +258,8 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
             const T* r = reinterpret_cast<const T*>(p.res) + rvox * p.cout + co;
             if constexpr (sizeof(T) == 2) {
               const uint2 rq = *reinterpret_cast<const uint2*>(r);
-              v[0] += __uint_as_float(rq.x << 16); v[1] += __uint_as_float(rq.x & 0xffff0000u);
-              v[2] += __uint_as_float(rq.y << 16); v[3] += __uint_as_float(rq.y & 0xffff0000u);
+              v[0] += lo2f<T16>(rq.x); v[1] += hi2f<T16>(rq.x);
+              v[2] += lo2f<T16>(rq.y); v[3] += hi2f<T16>(rq.y);
             } else {
               const float4 rq = *reinterpret_cast<const float4*>(r);
               v[0] += rq.x; v[1] += rq.y; v[2] += rq.z; v[3] += rq.w;
@@ -278,15 +279,15 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
             }
             *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
           } else {
-            bf16_t* o = reinterpret_cast<bf16_t*>(obase) + vox * ostride + oc;
+            T16* o = reinterpret_cast<T16*>(obase) + vox * ostride + oc;
             if (p.accumulate) {
               const uint2 oq = *reinterpret_cast<const uint2*>(o);
-              v[0] += __uint_as_float(oq.x << 16); v[1] += __uint_as_float(oq.x & 0xffff0000u);
-              v[2] += __uint_as_float(oq.y << 16); v[3] += __uint_as_float(oq.y & 0xffff0000u);
+              v[0] += lo2f<T16>(oq.x); v[1] += hi2f<T16>(oq.x);
+              v[2] += lo2f<T16>(oq.y); v[3] += hi2f<T16>(oq.y);
             }
             uint2 sq;
-            sq.x = pack_bf16x2(v[0], v[1]);
-            sq.y = pack_bf16x2(v[2], v[3]);
+            sq.x = pack2<T16>(v[0], v[1]);
+            sq.y = pack2<T16>(v[2], v[3]);
             *reinterpret_cast<uint2*>(o) = sq;
           }
 #pragma unroll
@@ -434,7 +435,7 @@ __device__ __forceinline__ void v4_issue_halo(const V4Params& p, const V4Tile& t
 // weights and bias are prefetched under the current tile's last chunk.
 template <typename T, int MODE, bool FAST, bool CT32 = false>
 __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
-  static_assert(!FAST || sizeof(T) == 2, "the fast epilogue is bf16 only");
+  static_assert(!FAST || sizeof(T) == 2, "the fast epilogue is 16-bit (bf16 / fp16) only");
   using C = V4Cfg;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[C::SMEM];
 

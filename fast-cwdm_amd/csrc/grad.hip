@@ -29,6 +29,11 @@ template <> __device__ __forceinline__ void load8<bf16_t>(const bf16_t* p, float
 #pragma unroll
   for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(a[i] << 16); f[2 * i + 1] = __uint_as_float(a[i] & 0xffff0000u); }
 }
+template <> __device__ __forceinline__ void load8<f16_t>(const f16_t* p, float* f) {
+  const u4 a = *reinterpret_cast<const u4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { f[2 * i] = lo2f<f16_t>(a[i]); f[2 * i + 1] = hi2f<f16_t>(a[i]); }
+}
 template <typename T> __device__ __forceinline__ void store8(T* p, const float* f);
 template <> __device__ __forceinline__ void store8<float>(float* p, const float* f) {
   u4 a, b;
@@ -41,6 +46,12 @@ template <> __device__ __forceinline__ void store8<bf16_t>(bf16_t* p, const floa
   u4 a;
 #pragma unroll
   for (int i = 0; i < 4; ++i) a[i] = (unsigned)f2bf(f[2 * i]) | ((unsigned)f2bf(f[2 * i + 1]) << 16);
+  *reinterpret_cast<u4*>(p) = a;
+}
+template <> __device__ __forceinline__ void store8<f16_t>(f16_t* p, const float* f) {
+  u4 a;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[i] = pack2<f16_t>(f[2 * i], f[2 * i + 1]);
   *reinterpret_cast<u4*>(p) = a;
 }
 
@@ -238,7 +249,7 @@ __global__ void __launch_bounds__(512) gn_bwd_finalize_kernel(const float* __res
 }
 
 template <typename T> __device__ __forceinline__ float stored(float v) {
-  if constexpr (sizeof(T) == 2) return bf2f(f2bf(v));
+  if constexpr (sizeof(T) == 2) return Elem<T>::to_f(Elem<T>::from_f(v));
   else return v;
 }
 
@@ -599,7 +610,7 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
   CWDM_REQUIRE(du_mode >= 0 && du_mode <= 2, CWDM_E_INVALID, "cwdm_gn_silu_bwd: bad du_mode");
   CWDM_REQUIRE(du_mode != 2 || (d % 2 == 0 && h % 2 == 0 && w % 2 == 0), CWDM_E_SHAPE,
                "cwdm_gn_silu_bwd: pooled grid must be even");
-  CWDM_REQUIRE(dtype == CWDM_F32 || dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_gn_silu_bwd: bad dtype");
+  CWDM_REQUIRE(dtype_compute(dtype), CWDM_E_INVALID, "cwdm_gn_silu_bwd: bad dtype");
   CWDM_REQUIRE(B > 0 && B < 65536 && d > 0 && h > 0 && w > 0, CWDM_E_SHAPE, "cwdm_gn_silu_bwd: empty grid");
   CWDM_REQUIRE(ws_bytes >= cwdm_gn_silu_bwd_workspace_bytes(C, B, d, h, w), CWDM_E_WORKSPACE,
                "cwdm_gn_silu_bwd: workspace too small");
@@ -615,14 +626,13 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
   int rc;
   if ((rc = dispatch_mode(du_mode, [&](auto M) -> int {
          constexpr int MD = decltype(M)::value;
-         if (dtype == CWDM_BF16)
-           hipLaunchKernelGGL((gn_bwd_reduce_kernel<bf16_t, MD>), dim3((unsigned)nb, (unsigned)B), dim3(256), 0, s,
-                              (const bf16_t*)x0, c0, (const bf16_t*)x1, c1, (const bf16_t*)du, ss, mr, groups, (int)d,
+         dispatch_dtype(dtype, [&](auto tag) -> int {
+           using T = decltype(tag);
+           hipLaunchKernelGGL((gn_bwd_reduce_kernel<T, MD>), dim3((unsigned)nb, (unsigned)B), dim3(256), 0, s,
+                              (const T*)x0, c0, (const T*)x1, c1, (const T*)du, ss, mr, groups, (int)d,
                               (int)h, (int)w, vpb, part);
-         else
-           hipLaunchKernelGGL((gn_bwd_reduce_kernel<float, MD>), dim3((unsigned)nb, (unsigned)B), dim3(256), 0, s,
-                              (const float*)x0, c0, (const float*)x1, c1, (const float*)du, ss, mr, groups, (int)d,
-                              (int)h, (int)w, vpb, part);
+           return CWDM_OK;
+         });
          CWDM_LAUNCHED();
          return CWDM_OK;
        })))
@@ -642,14 +652,13 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
   float* cp = chs ? chs_part : nullptr;
   if ((rc = dispatch_mode(du_mode, [&](auto M) -> int {
          constexpr int MD = decltype(M)::value;
-         if (dtype == CWDM_BF16)
-           hipLaunchKernelGGL((gn_bwd_apply_kernel<bf16_t, MD>), grid, block, 0, s, (const bf16_t*)x0, c0,
-                              (const bf16_t*)x1, c1, (const bf16_t*)du, ss, coef, (int)d, (int)h, (int)w, (bf16_t*)dx0,
-                              acc0, (bf16_t*)dx1, acc1, cp, (long long)chs_stride);
-         else
-           hipLaunchKernelGGL((gn_bwd_apply_kernel<float, MD>), grid, block, 0, s, (const float*)x0, c0,
-                              (const float*)x1, c1, (const float*)du, ss, coef, (int)d, (int)h, (int)w, (float*)dx0,
-                              acc0, (float*)dx1, acc1, cp, (long long)chs_stride);
+         dispatch_dtype(dtype, [&](auto tag) -> int {
+           using T = decltype(tag);
+           hipLaunchKernelGGL((gn_bwd_apply_kernel<T, MD>), grid, block, 0, s, (const T*)x0, c0,
+                              (const T*)x1, c1, (const T*)du, ss, coef, (int)d, (int)h, (int)w, (T*)dx0,
+                              acc0, (T*)dx1, acc1, cp, (long long)chs_stride);
+           return CWDM_OK;
+         });
          CWDM_LAUNCHED();
          return CWDM_OK;
        })))
@@ -673,6 +682,7 @@ extern "C" int cwdm_gn_silu_bwd(const void* x0, int c0, const void* x1, int c1, 
 extern "C" int cwdm_resample_add(void* dst, const void* src, int C, int64_t B, int64_t d, int64_t h, int64_t w,
                                  int mode, int accumulate, int dtype, cwdm_stream_t stream) {
   CWDM_REQUIRE(dst && src, CWDM_E_INVALID, "cwdm_resample_add: null pointer");
+  CWDM_REQUIRE(dtype_compute(dtype), CWDM_E_INVALID, "cwdm_resample_add: bad dtype");
   CWDM_REQUIRE(C > 0 && C % 8 == 0, CWDM_E_UNSUPPORTED, "cwdm_resample_add: channels must be a multiple of 8");
   CWDM_REQUIRE(mode >= 0 && mode <= 2, CWDM_E_INVALID, "cwdm_resample_add: bad mode");
   CWDM_REQUIRE(mode != 2 || (d % 2 == 0 && h % 2 == 0 && w % 2 == 0), CWDM_E_SHAPE, "cwdm_resample_add: odd grid");
@@ -685,12 +695,12 @@ extern "C" int cwdm_resample_add(void* dst, const void* src, int C, int64_t B, i
   hipStream_t s = (hipStream_t)stream;
   return dispatch_mode(mode, [&](auto M) -> int {
     constexpr int MD = decltype(M)::value;
-    if (dtype == CWDM_BF16)
-      hipLaunchKernelGGL((resample_add_kernel<bf16_t, MD>), grid, dim3(256), 0, s, (bf16_t*)dst, (const bf16_t*)src, C,
+    dispatch_dtype(dtype, [&](auto tag) -> int {
+      using T = decltype(tag);
+      hipLaunchKernelGGL((resample_add_kernel<T, MD>), grid, dim3(256), 0, s, (T*)dst, (const T*)src, C,
                          (int)d, (int)h, (int)w, accumulate, dncg);
-    else
-      hipLaunchKernelGGL((resample_add_kernel<float, MD>), grid, dim3(256), 0, s, (float*)dst, (const float*)src, C,
-                         (int)d, (int)h, (int)w, accumulate, dncg);
+      return CWDM_OK;
+    });
     CWDM_LAUNCHED();
     return CWDM_OK;
   });
@@ -712,6 +722,7 @@ extern "C" int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V
                                 int64_t bc_stride, float* out_c, float* out_c2, void* workspace, int64_t ws_bytes,
                                 cwdm_stream_t stream) {
   CWDM_REQUIRE(src, CWDM_E_INVALID, "cwdm_channel_sum: null pointer");
+  CWDM_REQUIRE(dtype_compute(dtype), CWDM_E_INVALID, "cwdm_channel_sum: bad dtype");
   CWDM_REQUIRE(C > 0 && cs >= ((C + 7) / 8) * 8 && cs % 8 == 0 && cs <= 2048, CWDM_E_UNSUPPORTED,
                "cwdm_channel_sum: stride must be a multiple of 8 covering C (<= 2048)");
   CWDM_REQUIRE(B > 0 && B < 65536 && V > 0, CWDM_E_SHAPE, "cwdm_channel_sum: empty input");
@@ -722,12 +733,12 @@ extern "C" int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V
   dim3 grid((unsigned)nb, (unsigned)B);
   hipStream_t s = (hipStream_t)stream;
   float* part = reinterpret_cast<float*>(workspace);
-  if (dtype == CWDM_BF16)
-    hipLaunchKernelGGL(channel_sum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)src, (long long)V, C, cs, vpb,
+  dispatch_dtype(dtype, [&](auto tag) -> int {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(channel_sum_kernel<T>, grid, dim3(256), 0, s, (const T*)src, (long long)V, C, cs, vpb,
                        out_bc, (long long)bc_stride, out_c, out_c2, part);
-  else
-    hipLaunchKernelGGL(channel_sum_kernel<float>, grid, dim3(256), 0, s, (const float*)src, (long long)V, C, cs, vpb,
-                       out_bc, (long long)bc_stride, out_c, out_c2, part);
+    return CWDM_OK;
+  });
   CWDM_LAUNCHED();
   if (part) {
     hipLaunchKernelGGL(chs_reduce_kernel, dim3((unsigned)ceil_div(C, 256)), dim3(256), 0, s, part, (int)nb, C, out_bc,

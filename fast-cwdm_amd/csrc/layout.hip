@@ -56,6 +56,9 @@ int launch_dst(const void* src, const int64_t* s, void* dst, int ddt, const int6
   else if (ddt == CWDM_BF16)
     hipLaunchKernelGGL((copy3_kernel<SrcT, bf16_t>), grid, dim3(256), 0, st, src, s[0], s[1], s[2], dst, d[0], d[1],
                        d[2], C, V);
+  else if (ddt == CWDM_F16)
+    hipLaunchKernelGGL((copy3_kernel<SrcT, f16_t>), grid, dim3(256), 0, st, src, s[0], s[1], s[2], dst, d[0], d[1],
+                       d[2], C, V);
   else
     return fail(CWDM_E_INVALID, "cwdm_copy3: bad dst dtype");
   CWDM_LAUNCHED();
@@ -74,5 +77,6 @@ extern "C" int cwdm_copy3(const void* src, int sdt, const int64_t* s, void* dst,
   CWDM_REQUIRE(B < 65536 && ceil_div(C, TC) < 65536, CWDM_E_UNSUPPORTED, "cwdm_copy3: grid too large");
   if (sdt == CWDM_F32) return launch_dst<float>(src, s, dst, ddt, d, B, C, V, (hipStream_t)stream);
   if (sdt == CWDM_BF16) return launch_dst<bf16_t>(src, s, dst, ddt, d, B, C, V, (hipStream_t)stream);
+  if (sdt == CWDM_F16) return launch_dst<f16_t>(src, s, dst, ddt, d, B, C, V, (hipStream_t)stream);
   return fail(CWDM_E_INVALID, "cwdm_copy3: bad src dtype");
 }

@@ -133,6 +133,12 @@ template <> __device__ __forceinline__ void pool_load8<bf16_t>(const bf16_t* p, 
 #pragma unroll
   for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(u[i] << 16); f[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u); }
 }
+template <> __device__ __forceinline__ void pool_load8<f16_t>(const f16_t* p, float* f) {
+  const uint4 a = *reinterpret_cast<const uint4*>(p);
+  const unsigned u[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { f[2 * i] = lo2f<f16_t>(u[i]); f[2 * i + 1] = hi2f<f16_t>(u[i]); }
+}
 template <typename T> __device__ __forceinline__ void pool_store8(T* p, const float* f);
 template <> __device__ __forceinline__ void pool_store8<float>(float* p, const float* f) {
   *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
@@ -144,6 +150,14 @@ template <> __device__ __forceinline__ void pool_store8<bf16_t>(bf16_t* p, const
   a.y = (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16);
   a.z = (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16);
   a.w = (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16);
+  *reinterpret_cast<uint4*>(p) = a;
+}
+template <> __device__ __forceinline__ void pool_store8<f16_t>(f16_t* p, const float* f) {
+  uint4 a;
+  a.x = pack2<f16_t>(f[0], f[1]);
+  a.y = pack2<f16_t>(f[2], f[3]);
+  a.z = pack2<f16_t>(f[4], f[5]);
+  a.w = pack2<f16_t>(f[6], f[7]);
   *reinterpret_cast<uint4*>(p) = a;
 }
 
@@ -213,6 +227,10 @@ extern "C" int cwdm_gn_silu_pool(const void* x, int C, const float* gn, int64_t 
     hipLaunchKernelGGL(gn_silu_pool_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream,
                        reinterpret_cast<const bf16_t*>(x), C, gn, (unsigned)n, dg8, dw, dh, dd,
                        reinterpret_cast<bf16_t*>(out_h), reinterpret_cast<bf16_t*>(out_x));
+  else if (dtype == CWDM_F16)
+    hipLaunchKernelGGL(gn_silu_pool_kernel<f16_t>, grid, dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const f16_t*>(x), C, gn, (unsigned)n, dg8, dw, dh, dd,
+                       reinterpret_cast<f16_t*>(out_h), reinterpret_cast<f16_t*>(out_x));
   else if (dtype == CWDM_F32)
     hipLaunchKernelGGL(gn_silu_pool_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream,
                        reinterpret_cast<const float*>(x), C, gn, (unsigned)n, dg8, dw, dh, dd,

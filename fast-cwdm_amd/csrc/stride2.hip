@@ -15,7 +15,7 @@
 namespace cwdm {
 namespace {
 
-// 16-byte (8 bf16 / 4 fp32 channels) copies; C * esize % 16 == 0
+// 16-byte (8 bf16 / fp16 or 4 fp32 channels) copies; C * esize % 16 == 0
 template <bool TO_DEPTH, bool ACC, typename T>
 __global__ void __launch_bounds__(256) s2d_kernel(const unsigned char* __restrict__ src, unsigned char* __restrict__ dst,
                                                  int C, int64_t B, int64_t d, int64_t h, int64_t w) {
@@ -42,11 +42,8 @@ __global__ void __launch_bounds__(256) s2d_kernel(const unsigned char* __restric
       unsigned* pv = reinterpret_cast<unsigned*>(&v);
       const unsigned* pa = reinterpret_cast<const unsigned*>(&a);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float lo = __uint_as_float(pv[k] << 16) + __uint_as_float(pa[k] << 16);
-        const float hi = __uint_as_float(pv[k] & 0xffff0000u) + __uint_as_float(pa[k] & 0xffff0000u);
-        pv[k] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
-      }
+      for (int k = 0; k < 4; ++k)
+        pv[k] = pack2<T>(lo2f<T>(pv[k]) + lo2f<T>(pa[k]), hi2f<T>(pv[k]) + hi2f<T>(pa[k]));
     } else {
       float* pv = reinterpret_cast<float*>(&v);
       const float* pa = reinterpret_cast<const float*>(&a);
@@ -86,8 +83,8 @@ using namespace cwdm;
 extern "C" int cwdm_space_to_depth(const void* x, int C, int64_t B, int64_t d, int64_t h, int64_t w, int dtype,
                                    void* out, int to_depth, int accumulate, cwdm_stream_t stream) {
   CWDM_REQUIRE(x && out, CWDM_E_INVALID, "cwdm_space_to_depth: null pointer");
-  CWDM_REQUIRE(dtype == CWDM_F32 || dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_space_to_depth: bad dtype");
-  const int es = dtype == CWDM_BF16 ? 2 : 4;
+  CWDM_REQUIRE(dtype_compute(dtype), CWDM_E_INVALID, "cwdm_space_to_depth: bad dtype");
+  const int es = dtype_size(dtype);
   CWDM_REQUIRE(C > 0 && (C * es) % 16 == 0 && B > 0 && d > 0 && h > 0 && w > 0, CWDM_E_SHAPE,
                "cwdm_space_to_depth: channels must fill 16-byte rows");
   const int64_t n = B * d * h * w * 8 * (C * es / 16);
@@ -97,6 +94,7 @@ extern "C" int cwdm_space_to_depth(const void* x, int C, int64_t B, int64_t d, i
   hipStream_t s = (hipStream_t)stream;
 #define S2D(TD, AC)                                                                                         \
   if (dtype == CWDM_BF16) hipLaunchKernelGGL((s2d_kernel<TD, AC, bf16_t>), grid, dim3(256), 0, s, src, dst, C, B, d, h, w); \
+  else if (dtype == CWDM_F16) hipLaunchKernelGGL((s2d_kernel<TD, AC, f16_t>), grid, dim3(256), 0, s, src, dst, C, B, d, h, w); \
   else hipLaunchKernelGGL((s2d_kernel<TD, AC, float>), grid, dim3(256), 0, s, src, dst, C, B, d, h, w);
   if (to_depth) {
     if (accumulate) { S2D(true, true) } else { S2D(true, false) }

@@ -154,7 +154,7 @@ struct cwdm_unet {
 
 namespace {
 
-int esize(int dtype) { return dtype == CWDM_BF16 ? 2 : 4; }
+int esize(int dtype) { return dtype_size(dtype); }
 
 void build(cwdm_unet* u) {
   const auto& c = u->cfg;
@@ -537,7 +537,7 @@ void build(cwdm_unet* u) {
   for (const auto& pr : u->params) { u->goff.push_back(go); go += pr.numel(); }
   u->grad_numel = go;
   // packed dgrad weights (every conv but conv_in, whose input needs no gradient)
-  const int ck = c.dtype == CWDM_BF16 ? 16 : 8;
+  const int ck = 32 / esize(c.dtype);
   int64_t bo = 0;
   auto takeb = [&](int64_t bytes) { int64_t o = bo; bo = align_up(bo + bytes); return o; };
   for (size_t i = 0; i < u->convs.size(); ++i) {
@@ -681,9 +681,9 @@ extern "C" int cwdm_unet_create(const cwdm_unet_config* cfg, cwdm_unet** plan) {
   CWDM_REQUIRE(cfg->num_levels >= 1 && cfg->num_levels <= 8, CWDM_E_INVALID, "cwdm_unet_create: 1..8 levels");
   CWDM_REQUIRE(cfg->model_channels > 0 && cfg->in_channels > 0 && cfg->out_channels > 0 && cfg->num_res_blocks >= 1,
                CWDM_E_INVALID, "cwdm_unet_create: bad channel config");
-  CWDM_REQUIRE(cfg->dtype == CWDM_F32 || cfg->dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_unet_create: bad dtype");
+  CWDM_REQUIRE(dtype_compute(cfg->dtype), CWDM_E_INVALID, "cwdm_unet_create: bad dtype");
   CWDM_REQUIRE(cfg->num_groups > 0, CWDM_E_INVALID, "cwdm_unet_create: bad num_groups");
-  const int ck = cfg->dtype == CWDM_BF16 ? 16 : 8;
+  const int ck = 32 / dtype_size(cfg->dtype);
   CWDM_REQUIRE(cfg->in_channels % ck == 0, CWDM_E_UNSUPPORTED,
                "cwdm_unet_create: in_channels must be a multiple of " + std::to_string(ck));
   for (int l = 0; l < cfg->num_levels; ++l) {
@@ -1021,7 +1021,7 @@ struct GLayout {
 };
 
 int ckpad(const cwdm_unet* u, int c) {
-  const int ck = u->cfg.dtype == CWDM_BF16 ? 16 : 8;
+  const int ck = 32 / esize(u->cfg.dtype);
   return (c + ck - 1) / ck * ck;
 }
 

@@ -180,7 +180,7 @@ inline S3 s3(const int64_t* p) { return p ? S3{p[0], p[1], p[2]} : S3{0, 0, 0}; 
 // Fused a3 + a7 + a9: one subband voxel (8 channels) per thread.
 // vec bit 0: model_out holds a voxel's 8 channels in 32 contiguous aligned bytes
 // (the U-Net's NDHWC fp32 output); bit 1: the same for the mirror (16 B bf16 /
-// 32 B fp32) -- one wide access instead of 8 strided scalars.
+// fp16, 32 B fp32) -- one wide access instead of 8 strided scalars.
 template <typename MirT>
 __global__ void __launch_bounds__(256) sampler_kernel(cwdm_sampler_args a, S3 mo, S3 xt, S3 xp, S3 nz, S3 px,
                                                      S3 mr_, int vec) {
@@ -254,10 +254,10 @@ __global__ void __launch_bounds__(256) sampler_kernel(cwdm_sampler_args a, S3 mo
   if (vec & 2) {
     if constexpr (sizeof(MirT) == 2) {
       uint4 q;
-      q.x = (unsigned)f2bf(r[0]) | ((unsigned)f2bf(r[1]) << 16);
-      q.y = (unsigned)f2bf(r[2]) | ((unsigned)f2bf(r[3]) << 16);
-      q.z = (unsigned)f2bf(r[4]) | ((unsigned)f2bf(r[5]) << 16);
-      q.w = (unsigned)f2bf(r[6]) | ((unsigned)f2bf(r[7]) << 16);
+      q.x = pack2<MirT>(r[0], r[1]);
+      q.y = pack2<MirT>(r[2], r[3]);
+      q.z = pack2<MirT>(r[4], r[5]);
+      q.w = pack2<MirT>(r[6], r[7]);
       *reinterpret_cast<uint4*>(reinterpret_cast<MirT*>(a.mirror) + b * mr_.b + v * mr_.v) = q;
     } else {
       float4* o = reinterpret_cast<float4*>(reinterpret_cast<MirT*>(a.mirror) + b * mr_.b + v * mr_.v);
@@ -293,6 +293,9 @@ extern "C" int cwdm_haar_dwt3d(const float* x, int64_t B, int64_t C, int64_t D, 
   else if (out_dtype == CWDM_BF16)
     hipLaunchKernelGGL(dwt3d_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, x, B * C, D / 2, H / 2,
                        W / 2, out, s, (int)C, lll_div3);
+  else if (out_dtype == CWDM_F16)
+    hipLaunchKernelGGL(dwt3d_kernel<f16_t>, grid, dim3(256), 0, (hipStream_t)stream, x, B * C, D / 2, H / 2,
+                       W / 2, out, s, (int)C, lll_div3);
   else
     return fail(CWDM_E_INVALID, "cwdm_haar_dwt3d: bad dtype");
   CWDM_LAUNCHED();
@@ -313,6 +316,9 @@ extern "C" int cwdm_haar_idwt3d(const void* bands, int in_dtype, const int64_t* 
                        h, w, x, lll_mul3, clamp01);
   else if (in_dtype == CWDM_BF16)
     hipLaunchKernelGGL(idwt3d_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, bands, s, B * C, (int)C, d,
+                       h, w, x, lll_mul3, clamp01);
+  else if (in_dtype == CWDM_F16)
+    hipLaunchKernelGGL(idwt3d_kernel<f16_t>, grid, dim3(256), 0, (hipStream_t)stream, bands, s, B * C, (int)C, d,
                        h, w, x, lll_mul3, clamp01);
   else
     return fail(CWDM_E_INVALID, "cwdm_haar_idwt3d: bad dtype");
@@ -336,6 +342,9 @@ extern "C" int cwdm_haar_idwt3d_planes(const void* const* bands, int in_dtype, c
                        h, w, x);
   else if (in_dtype == CWDM_BF16)
     hipLaunchKernelGGL(idwt3d_planes_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, pl, s, B * C, (int)C, d,
+                       h, w, x);
+  else if (in_dtype == CWDM_F16)
+    hipLaunchKernelGGL(idwt3d_planes_kernel<f16_t>, grid, dim3(256), 0, (hipStream_t)stream, pl, s, B * C, (int)C, d,
                        h, w, x);
   else
     return fail(CWDM_E_INVALID, "cwdm_haar_idwt3d_planes: bad dtype");
@@ -425,12 +434,14 @@ extern "C" int cwdm_sampler_step(const cwdm_sampler_args* a, cwdm_stream_t strea
   auto aligned = [](const void* p, int64_t bs, int64_t vs, int esz, int al) {
     return ((uintptr_t)p % al) == 0 && (bs * esz) % al == 0 && (vs * esz) % al == 0;
   };
-  const int mesz = a->mirror_dtype == CWDM_BF16 ? 2 : 4;
+  const int mesz = dtype_size(a->mirror_dtype);
   int vec = 0;
   if (mo.c == 1 && aligned(a->model_out, mo.b, mo.v, 4, 16)) vec |= 1;
   if (a->mirror && mi.c == 1 && aligned(a->mirror, mi.b, mi.v, mesz, 16)) vec |= 2;
   if (a->mirror && a->mirror_dtype == CWDM_BF16)
     hipLaunchKernelGGL(sampler_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, *a, mo, xt, xp, nz, px, mi, vec);
+  else if (a->mirror && a->mirror_dtype == CWDM_F16)
+    hipLaunchKernelGGL(sampler_kernel<f16_t>, grid, dim3(256), 0, (hipStream_t)stream, *a, mo, xt, xp, nz, px, mi, vec);
   else if (!a->mirror || a->mirror_dtype == CWDM_F32)
     hipLaunchKernelGGL(sampler_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *a, mo, xt, xp, nz, px, mi, vec);
   else

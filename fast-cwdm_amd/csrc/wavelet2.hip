@@ -10,6 +10,8 @@
 // register transforms (haar8.hpp, products rounded before adds like the
 // single-level kernels: bit-exact against the oracle).
 #include "common.hpp"
+#include <type_traits>
+
 #include "haar8.hpp"
 
 namespace cwdm {
@@ -249,9 +251,10 @@ __global__ void __launch_bounds__(256) sampler2_kernel(cwdm_sampler_args a, S3w 
     if (a.mirror) {
       MirT* o = reinterpret_cast<MirT*>(a.mirror) + b * mi.b + v * mi.v;
       if ((vec & 32) && sizeof(MirT) == 2) {
+        using M16 = std::conditional_t<sizeof(MirT) == 2, MirT, bf16_t>;
         uint2 q2;
-        q2.x = (unsigned)f2bf(r[0]) | ((unsigned)f2bf(r[1]) << 16);
-        q2.y = (unsigned)f2bf(r[2]) | ((unsigned)f2bf(r[3]) << 16);
+        q2.x = pack2<M16>(r[0], r[1]);
+        q2.y = pack2<M16>(r[2], r[3]);
         *reinterpret_cast<uint2*>(o + 4 * g) = q2;
       } else {
 #pragma unroll
@@ -270,7 +273,7 @@ int sampler2_launch(const cwdm_sampler_args* a, hipStream_t s) {
   auto ok = [](const void* p, S3w st, int esz) {
     return p && st.c == 1 && ((uintptr_t)p % 16) == 0 && (st.b * esz) % 16 == 0 && (st.v * esz) % 16 == 0;
   };
-  const int mesz = a->mirror_dtype == CWDM_BF16 ? 2 : 4;
+  const int mesz = dtype_size(a->mirror_dtype);
   int vec = 0;
   if (ok(a->model_out, mo, 4)) vec |= 1;
   if (ok(a->x_t, xt, 4)) vec |= 2;
@@ -282,6 +285,8 @@ int sampler2_launch(const cwdm_sampler_args* a, hipStream_t s) {
   const dim3 grid((unsigned)ceil_div(a->B * a->d * a->h * a->w, 256));
   if (a->mirror && a->mirror_dtype == CWDM_BF16)
     hipLaunchKernelGGL(sampler2_kernel<bf16_t>, grid, dim3(256), 0, s, *a, mo, xt, xp, nz, px, mi, vec);
+  else if (a->mirror && a->mirror_dtype == CWDM_F16)
+    hipLaunchKernelGGL(sampler2_kernel<f16_t>, grid, dim3(256), 0, s, *a, mo, xt, xp, nz, px, mi, vec);
   else if (!a->mirror || a->mirror_dtype == CWDM_F32)
     hipLaunchKernelGGL(sampler2_kernel<float>, grid, dim3(256), 0, s, *a, mo, xt, xp, nz, px, mi, vec);
   else
@@ -307,6 +312,9 @@ extern "C" int cwdm_wavelet2_analysis(const float* x, int64_t B, int64_t D, int6
   if (out_dtype == CWDM_BF16)
     hipLaunchKernelGGL(wav2_analysis_kernel<bf16_t>, grid, dim3(256), 0, s, x, B, d, h, w,
                        reinterpret_cast<bf16_t*>(out), out_bs, out_vs, out_c0);
+  else if (out_dtype == CWDM_F16)
+    hipLaunchKernelGGL(wav2_analysis_kernel<f16_t>, grid, dim3(256), 0, s, x, B, d, h, w,
+                       reinterpret_cast<f16_t*>(out), out_bs, out_vs, out_c0);
   else if (out_dtype == CWDM_F32)
     hipLaunchKernelGGL(wav2_analysis_kernel<float>, grid, dim3(256), 0, s, x, B, d, h, w,
                        reinterpret_cast<float*>(out), out_bs, out_vs, out_c0);

@@ -23,8 +23,8 @@ __device__ __forceinline__ void load8(const T* p, float* f) {
     const unsigned u[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      f[2 * i] = __uint_as_float(u[i] << 16);
-      f[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+      f[2 * i] = lo2f<T>(u[i]);
+      f[2 * i + 1] = hi2f<T>(u[i]);
     }
   } else {
     const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
@@ -36,10 +36,10 @@ template <typename T>
 __device__ __forceinline__ void store8(T* p, const float* f) {
   if constexpr (sizeof(T) == 2) {
     uint4 q;
-    q.x = (unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16);
-    q.y = (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16);
-    q.z = (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16);
-    q.w = (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16);
+    q.x = pack2<T>(f[0], f[1]);
+    q.y = pack2<T>(f[2], f[3]);
+    q.z = pack2<T>(f[4], f[5]);
+    q.w = pack2<T>(f[6], f[7]);
     *reinterpret_cast<uint4*>(p) = q;
   } else {
     *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
@@ -155,7 +155,7 @@ extern "C" int64_t cwdm_haar_nd_parts(int64_t d, int64_t h, int64_t w) { return 
 
 extern "C" int cwdm_haar_nd(const cwdm_haar_nd_desc* a, cwdm_stream_t stream) {
   CWDM_REQUIRE(a && a->src && a->out, CWDM_E_INVALID, "cwdm_haar_nd: null pointer");
-  CWDM_REQUIRE(a->dtype == CWDM_F32 || a->dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_haar_nd: bad dtype");
+  CWDM_REQUIRE(dtype_compute(a->dtype), CWDM_E_INVALID, "cwdm_haar_nd: bad dtype");
   CWDM_REQUIRE(a->B > 0 && a->d > 0 && a->h > 0 && a->w > 0, CWDM_E_SHAPE, "cwdm_haar_nd: empty grid");
   CWDM_REQUIRE(a->C > 0 && a->C % 8 == 0 && a->C <= 2048, CWDM_E_UNSUPPORTED,
                "cwdm_haar_nd: channels must be a multiple of 8, at most 2048");
@@ -165,13 +165,12 @@ extern "C" int cwdm_haar_nd(const cwdm_haar_nd_desc* a, cwdm_stream_t stream) {
   const int parts = (int)cwdm_haar_nd_parts(a->d, a->h, a->w);
   const dim3 grid((unsigned)(a->B * parts));
   hipStream_t s = (hipStream_t)stream;
-  if (a->dtype == CWDM_BF16) {
-    if (a->inverse) hipLaunchKernelGGL((haar_nd_kernel<bf16_t, true>), grid, dim3(256), 0, s, *a, parts);
-    else hipLaunchKernelGGL((haar_nd_kernel<bf16_t, false>), grid, dim3(256), 0, s, *a, parts);
-  } else {
-    if (a->inverse) hipLaunchKernelGGL((haar_nd_kernel<float, true>), grid, dim3(256), 0, s, *a, parts);
-    else hipLaunchKernelGGL((haar_nd_kernel<float, false>), grid, dim3(256), 0, s, *a, parts);
-  }
+  dispatch_dtype(a->dtype, [&](auto tag) -> int {
+    using T = decltype(tag);
+    if (a->inverse) hipLaunchKernelGGL((haar_nd_kernel<T, true>), grid, dim3(256), 0, s, *a, parts);
+    else hipLaunchKernelGGL((haar_nd_kernel<T, false>), grid, dim3(256), 0, s, *a, parts);
+    return CWDM_OK;
+  });
   CWDM_LAUNCHED();
   return CWDM_OK;
 }

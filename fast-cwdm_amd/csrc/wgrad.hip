@@ -19,7 +19,7 @@
 //     each, 32-B rows) and the brick's dY rows [voxel][co] are committed from
 //     registers that were loaded while the previous brick's MFMAs ran.
 //   * both MFMA operands need K (voxels) along the lane's 8 elements while
-//     LDS rows hold channels: bf16 reads them with the gfx950 transposed LDS
+//     LDS rows hold channels: bf16 / fp16 read them with the gfx950 transposed LDS
 //     read ds_read_b64_tr_b16 (4 voxel rows x 16 channels per 16-lane group),
 //     so no transposed copy is ever written.
 //   * 3x3x3: wave w owns taps {w, w+4, ..., <27}; the dY fragments of a
@@ -62,14 +62,13 @@ __device__ __forceinline__ v4s tr_read(const unsigned char* lds) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(lds));
 }
 
-// two transposed 64-bit reads -> one 8 x bf16 operand, as whole dwords (an
-// element-wise shuffle of the 16-bit lanes made the compiler repack every
-// dword with v_lshrrev + v_perm: 48 VALU per K-step)
-__device__ __forceinline__ bf16x8 join(v4s a, v4s b) {
+// two transposed 64-bit reads -> one 8 x 16-bit operand (bf16 or fp16), as
+// whole dwords (an element-wise shuffle of the 16-bit lanes made the compiler
+// repack every dword with v_lshrrev + v_perm: 48 VALU per K-step)
+__device__ __forceinline__ u32x4 join(v4s a, v4s b) {
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   const u32x2 lo = __builtin_bit_cast(u32x2, a), hi = __builtin_bit_cast(u32x2, b);
-  const u32x4 r = {lo.x, lo.y, hi.x, hi.y};
-  return __builtin_bit_cast(bf16x8, r);
+  return u32x4{lo.x, lo.y, hi.x, hi.y};
 }
 
 // dY quad swizzle (bf16, 128-B rows): rows 2,3 of every 4 use the other half
@@ -92,7 +91,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradParams p) {
   constexpr int CK = C::CK, NCH = C::NCH;
   constexpr int QPV = C::DYP / 16;          // dY quads per voxel row
   constexpr int EPQ = 16 / (int)sizeof(T);
-  constexpr bool PF = sizeof(T) == 2;       // register prefetch of the next brick (bf16)
+  constexpr bool PF = sizeof(T) == 2;       // register prefetch of the next brick (16-bit types)
   constexpr int NT = TAPS == 27 ? 7 : 1;    // taps per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* halo = smem;
@@ -180,7 +179,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradParams p) {
       constexpr int NS = TAPS == 27 ? 16 : 4;   // K-steps of this wave
       const int s0 = TAPS == 27 ? 0 : 4 * wv;
       // fragments of K-step s: dY (A) for every co sub-tile, U (B) for every tap
-      auto load_frags = [&](int s, bf16x8* a, bf16x8* bfr) {
+      auto load_frags = [&](int s, u32x4* a, u32x4* bfr) {
         const int y = s & 3, z = s >> 2;
 #pragma unroll
         for (int m = 0; m < MC; ++m) {
@@ -201,14 +200,13 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradParams p) {
         }
       };
       // software pipeline: K-step s+1's LDS reads are in flight during K-step s's MFMAs
-      bf16x8 fa0[MC], fb0[NT], fa1[MC], fb1[NT];
-      auto mfmas = [&](const bf16x8* a, const bf16x8* bfr) {
+      u32x4 fa0[MC], fb0[NT], fa1[MC], fb1[NT];
+      auto mfmas = [&](const u32x4* a, const u32x4* bfr) {
 #pragma unroll
         for (int k = 0; k < NT; ++k) {
           if (k + 1 < NT || k < ntap) {
 #pragma unroll
-            for (int m = 0; m < MC; ++m)
-              acc[k][m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m], bfr[k], acc[k][m], 0, 0, 0);
+            for (int m = 0; m < MC; ++m) mfma_acc(acc[k][m], a[m], bfr[k], (T*)nullptr);
           }
         }
       };
@@ -317,12 +315,12 @@ using namespace cwdm;
 extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream) {
   CWDM_REQUIRE(d, CWDM_E_INVALID, "cwdm_conv3d_wgrad: null desc");
   CWDM_REQUIRE(d->u0 && d->dy && d->dw, CWDM_E_INVALID, "cwdm_conv3d_wgrad: null pointer");
-  CWDM_REQUIRE(d->dtype == CWDM_F32 || d->dtype == CWDM_BF16, CWDM_E_INVALID, "cwdm_conv3d_wgrad: bad dtype");
+  CWDM_REQUIRE(dtype_compute(d->dtype), CWDM_E_INVALID, "cwdm_conv3d_wgrad: bad dtype");
   CWDM_REQUIRE(d->ksize == 1 || d->ksize == 3, CWDM_E_UNSUPPORTED, "cwdm_conv3d_wgrad: ksize must be 1 or 3");
   CWDM_REQUIRE(d->B > 0 && d->D > 0 && d->H > 0 && d->W > 0, CWDM_E_SHAPE, "cwdm_conv3d_wgrad: empty grid");
   CWDM_REQUIRE(d->u_c1 == 0 || d->u1, CWDM_E_INVALID, "cwdm_conv3d_wgrad: second source missing");
   const int cin = d->u_c0 + d->u_c1;
-  const int epq = d->dtype == CWDM_BF16 ? 8 : 4;
+  const int epq = 16 / dtype_size(d->dtype);
   CWDM_REQUIRE(cin > 0 && cin % 32 == 0 && d->u_c0 % epq == 0, CWDM_E_UNSUPPORTED,
                "cwdm_conv3d_wgrad: input channels must be a multiple of 32 (split on a quad)");
   CWDM_REQUIRE(d->cout > 0 && d->dy_cs >= d->cout && d->dy_cs % epq == 0, CWDM_E_SHAPE,
@@ -361,10 +359,10 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
   const long long nw = (long long)d->cout * cin * p.taps;
   CWDM_HIP(hipMemsetAsync(d->workspace, 0, nw * 4, s));
   int rc;
-  if (d->dtype == CWDM_BF16)
-    rc = mc == 2 ? dispatch_wg<bf16_t, 2>(p, d->u_mode, gn, grid, s) : dispatch_wg<bf16_t, 1>(p, d->u_mode, gn, grid, s);
-  else
-    rc = mc == 2 ? dispatch_wg<float, 2>(p, d->u_mode, gn, grid, s) : dispatch_wg<float, 1>(p, d->u_mode, gn, grid, s);
+  rc = dispatch_dtype(d->dtype, [&](auto tag) -> int {
+    using T = decltype(tag);
+    return mc == 2 ? dispatch_wg<T, 2>(p, d->u_mode, gn, grid, s) : dispatch_wg<T, 1>(p, d->u_mode, gn, grid, s);
+  });
   if (rc) return rc;
   hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)ceil_div(nw, 256)), dim3(256), 0, s,
                      reinterpret_cast<const float*>(d->workspace), d->dw, d->cout, cin, p.taps);

@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("CWDM_LIB", os.path.join(_HERE, "..", "lib", "libcwdm.
 CWDM_F32 = 0
 CWDM_BF16 = 1
 CWDM_F64 = 2
+CWDM_F16 = 3
 
 E_INVALID, E_SHAPE, E_HIP, E_WORKSPACE, E_INDEX, E_UNSUPPORTED = -1, -2, -3, -4, -5, -6
 

@@ -10,9 +10,9 @@ import math
 import torch
 
 from . import _lib
-from ._lib import CWDM_BF16, CWDM_F32, CWDM_F64, check, lib, strides
+from ._lib import CWDM_BF16, CWDM_F16, CWDM_F32, CWDM_F64, check, lib, strides
 
-DT = {torch.float32: CWDM_F32, torch.bfloat16: CWDM_BF16}
+DT = {torch.float32: CWDM_F32, torch.bfloat16: CWDM_BF16, torch.float16: CWDM_F16}
 
 
 def _stream():

@@ -9,18 +9,19 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import CWDM_BF16, CWDM_F32, check, lib
+from ._lib import CWDM_BF16, CWDM_F16, CWDM_F32, check, lib
 from .ops import _need_cuda, _stream
 
-_DTYPES = {"fp32": CWDM_F32, "float32": CWDM_F32, "bf16": CWDM_BF16, "bfloat16": CWDM_BF16}
-TORCH_DT = {CWDM_F32: torch.float32, CWDM_BF16: torch.bfloat16}
+_DTYPES = {"fp32": CWDM_F32, "float32": CWDM_F32, "bf16": CWDM_BF16, "bfloat16": CWDM_BF16,
+           "fp16": CWDM_F16, "float16": CWDM_F16}
+TORCH_DT = {CWDM_F32: torch.float32, CWDM_BF16: torch.bfloat16, CWDM_F16: torch.float16}
 
 
 def parse_dtype(d):
     if isinstance(d, torch.dtype):
-        d = {torch.float32: "fp32", torch.bfloat16: "bf16"}.get(d, str(d))
+        d = {torch.float32: "fp32", torch.bfloat16: "bf16", torch.float16: "fp16"}.get(d, str(d))
     if d not in _DTYPES:
-        raise ValueError(f"compute dtype must be fp32 or bf16, got {d!r}")
+        raise ValueError(f"compute dtype must be fp32, bf16 or fp16, got {d!r}")
     return _DTYPES[d]
 
 
@@ -178,7 +179,7 @@ class UNetPlan:
         out = []
         n = lib().cwdm_unet_trace_count(self._h)
         off, ch, lv = ctypes.c_int64(), ctypes.c_int(), ctypes.c_int()
-        es = 2 if self.dtype == CWDM_BF16 else 4
+        es = 4 if self.dtype == CWDM_F32 else 2
         for i in range(n):
             check(lib().cwdm_unet_trace_info(self._h, i, B, D, H, W, ctypes.byref(off), ctypes.byref(ch),
                                              ctypes.byref(lv)))

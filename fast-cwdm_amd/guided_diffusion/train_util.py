@@ -53,7 +53,15 @@ class TrainLoop:
         self.log_interval = log_interval
         self.save_interval = save_interval
         self.resume_checkpoint = resume_checkpoint
-        self.use_fp16 = use_fp16       # a no-op in the reference too
+        # use_fp16 enables dynamic loss scaling like the reference (amp.GradScaler,
+        # train_util.py:84-87, :367-389, :457-458; there it scales an fp32 model).
+        # A native model computing in fp16 (compute_dtype="fp16") needs it: the
+        # MSE gradient of a 128^3 x 8 output is ~1e-7 per element, below fp16's
+        # normal range, so it is scaled before the backward and unscaled (with
+        # the non-finite check that skips the step) before AdamW
+        self.use_fp16 = use_fp16
+        fp16_compute = getattr(model, "compute_dtype", None) in ("fp16", "float16")
+        self.grad_scaler = th.amp.GradScaler("cuda", enabled=bool(use_fp16 or fp16_compute) and th.cuda.is_available())
         self.schedule_sampler = schedule_sampler or UniformSampler(diffusion)
         self.weight_decay = weight_decay
         self.lr_anneal_steps = lr_anneal_steps
@@ -162,6 +170,8 @@ class TrainLoop:
     def run_step(self, batch, cond, label=None, info=None):
         info = {} if info is None else info
         lossmse, sample, sample_idwt = self.forward_backward(batch, cond, label)
+        if self.grad_scaler.is_enabled():
+            self.grad_scaler.unscale_(self.opt)
         with th.no_grad():
             if self.native:
                 info["norm/param_max"] = self.model.flat_params.abs().max()
@@ -170,7 +180,12 @@ class TrainLoop:
                 info["norm/param_max"] = max(p.abs().max() for p in self.model.parameters())
                 info["norm/grad_max"] = max(p.grad.abs().max() for p in self.model.parameters() if p.grad is not None)
         self._check_finite(lossmse)
-        self.opt.step()
+        if self.grad_scaler.is_enabled():
+            self.grad_scaler.step(self.opt)     # skipped when the unscaled gradients are not finite
+            self.grad_scaler.update()
+            info["scale"] = self.grad_scaler.get_scale()
+        else:
+            self.opt.step()
         self._anneal_lr()
         self.log_step()
         self.last_info = info
@@ -220,7 +235,10 @@ class TrainLoop:
         lossmse = loss.detach()
         for key, values in losses.items():
             logger.logkv_mean(key, values.mean().detach())
-        loss.backward()
+        if self.grad_scaler.is_enabled():
+            self.grad_scaler.scale(loss).backward()
+        else:
+            loss.backward()
         return lossmse, sample, sample_idwt
 
     def _anneal_lr(self):

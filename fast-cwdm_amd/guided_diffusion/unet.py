@@ -6,8 +6,9 @@ runs as one call into libcwdm (``cwdm_unet_forward``): time embedding, 35
 ResBlocks and the output head become ~160 fused launches (GroupNorm-finalize +
 implicit-GEMM Conv3d on MFMA with GN/SiLU/pool/upsample/concat/skip/bias/
 residual folded in).  Activations are channels-last NDHWC in the
-compute dtype (``compute_dtype`` = "fp32" for reference numerics, "bf16" for
-throughput); parameters stay fp32 masters and are re-packed when they change.
+compute dtype (``compute_dtype`` = "fp32" for reference numerics, "bf16" or
+"fp16" for throughput -- the same MFMA rate on gfx950, fp16 with 3 more mantissa
+bits); parameters stay fp32 masters and are re-packed when they change.
 
 Supported configuration family: the one run.sh uses (dims=3, no attention,
 use_scale_shift_norm=False, additive_skips=False, resample_2d=False), with
@@ -300,7 +301,7 @@ class UNetModel(nn.Module):
         plan.check_grid(D, H, W)
         V = D * H * W
         xin = th.empty((B, D, H, W, C), dtype=plan.torch_dtype, device=x.device)
-        ops.copy3(x.detach().contiguous().float() if x.dtype not in (th.float32, th.bfloat16) else
+        ops.copy3(x.detach().contiguous().float() if x.dtype not in (th.float32, th.bfloat16, th.float16) else
                   x.detach().contiguous(), (C * V, V, 1), xin, (V * C, 1, C), B, C, V)
         t = timesteps.to(device=x.device, dtype=th.float32).contiguous()
         return xin, t

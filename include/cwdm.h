@@ -28,7 +28,12 @@ extern "C" {
 
 typedef struct ihipStream_t* cwdm_stream_t; /* == hipStream_t; NULL = default stream */
 
-enum { CWDM_F32 = 0, CWDM_BF16 = 1, CWDM_F64 = 2 /* volume front end input only */ };
+enum {
+  CWDM_F32 = 0,
+  CWDM_BF16 = 1,
+  CWDM_F64 = 2, /* volume front end input only */
+  CWDM_F16 = 3  /* IEEE binary16: activations / weights like CWDM_BF16 (fp32 accumulation and statistics) */
+};
 
 enum {
   CWDM_OK = 0,

@@ -46,7 +46,7 @@ CFGS = [
 
 
 @pytest.mark.parametrize("cfg", CFGS)
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 def test_plan_param_contract_matches_oracle(cfg, dtype):
     from cwdm_hip.unet_runtime import UNetPlan
     plan = UNetPlan(cfg["in_channels"], cfg["model_channels"], cfg["out_channels"], cfg["num_res_blocks"],
@@ -83,6 +83,25 @@ def test_conv_pack_sizes():
     assert L.cwdm_conv3d_packed_bytes(64, 64, 3, _lib.CWDM_BF16) == 27 * 64 * 64 * 2
     assert L.cwdm_conv3d_packed_bytes(8, 64, 3, _lib.CWDM_F32) == 27 * 32 * 64 * 4   # cout padded to 32
     assert L.cwdm_conv3d_packed_bytes(64, 24, 3, _lib.CWDM_BF16) == -1              # 24 % 16 != 0
+    # fp16: the bf16 layout (16-channel K chunks, 2 bytes per element)
+    for co, ci, k in ((64, 64, 3), (8, 64, 3), (256, 512, 1)):
+        assert L.cwdm_conv3d_packed_bytes(co, ci, k, _lib.CWDM_F16) == L.cwdm_conv3d_packed_bytes(co, ci, k,
+                                                                                               _lib.CWDM_BF16)
+    assert L.cwdm_conv3d_packed_bytes(64, 64, 3, 7) == -1                            # unknown dtype
+
+
+def test_fp16_plan_matches_bf16_layout():
+    """compute_dtype="fp16": the same topology, packed-weight size and
+    workspace as bf16 (both 16-bit), and the torch dtype is float16."""
+    from cwdm_hip.unet_runtime import UNetPlan
+    a = UNetPlan(32, 64, 8, 2, (1, 2, 2, 4, 4), 32, "bf16")
+    b = UNetPlan(32, 64, 8, 2, (1, 2, 2, 4, 4), 32, "fp16")
+    assert a.param_specs == b.param_specs
+    assert a.packed_bytes == b.packed_bytes
+    assert a.workspace_bytes(1, 64, 64, 64) == b.workspace_bytes(1, 64, 64, 64)
+    assert b.torch_dtype == torch.float16
+    with pytest.raises(ValueError):
+        UNetPlan(32, 64, 8, 2, (1, 2, 2, 4, 4), 32, "fp8")
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])

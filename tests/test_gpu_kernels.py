@@ -13,6 +13,21 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+def _dtn():
+    from cwdm_hip import _lib
+    return {"fp32": (_lib.CWDM_F32, torch.float32), "bf16": (_lib.CWDM_BF16, torch.bfloat16),
+            "fp16": (_lib.CWDM_F16, torch.float16)}
+
+
+class _LazyDTN(dict):
+    def __missing__(self, k):
+        self.update(_dtn())
+        return dict.__getitem__(self, k)
+
+
+_DTN = _LazyDTN()   # dtype name -> (CWDM_*, torch dtype)
+
+
 def rel_err(a, b):
     a, b = a.double().cpu(), b.double().cpu()
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
@@ -35,7 +50,7 @@ def test_dwt_idwt_bitexact_vs_oracle(shape):
     assert (rec - x).abs().max() < 1e-5
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_idwt_from_separate_planes_bitexact(dtype):
     """IDWT_3D's eight arguments go to the kernel as eight pointers (no stack
     copy): bit-exact vs the oracle on the same (dtype-rounded) bands."""
@@ -98,6 +113,9 @@ def test_dwt_bf16_and_strided_output_into_channel_slice():
     ops.dwt3d(x.to(DEV), out=out, out_strides=(2 * V, V, V, 1))
     refb = torch.stack(haar.dwt3d(x), 0).to(torch.bfloat16)
     assert torch.equal(out.cpu(), refb)
+    outh = torch.empty(8, 2, 1, 8, 8, 8, device=DEV, dtype=torch.float16)
+    ops.dwt3d(x.to(DEV), out=outh, out_strides=(2 * V, V, V, 1))
+    assert torch.equal(outh.cpu(), torch.stack(haar.dwt3d(x), 0).to(torch.float16))
 
 
 # --------------------------------------------------------------------------- sampler
@@ -159,7 +177,7 @@ def _conv_call(dtype, out_grid, a0, a1, amode, gn, w, bias, bvec_bstride=0, b0=N
     from cwdm_hip._lib import check, lib
     B, D, H, W = out_grid
     cout = w.shape[0]
-    tdt = torch.float32 if dtype == _lib.CWDM_F32 else torch.bfloat16
+    tdt = {_lib.CWDM_F32: torch.float32, _lib.CWDM_BF16: torch.bfloat16, _lib.CWDM_F16: torch.float16}[dtype]
     L = lib()
 
     def pack(wt, k):
@@ -221,7 +239,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("split", [True, False], ids=["splitk", "nosplit"])
-@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 def test_conv3d_fused_vs_torch(case, dtype_name, split):
     _run_conv_case(case, dtype_name, split)
@@ -254,7 +272,7 @@ def _random_conv_cases(n, seed):
 RANDOM_CASES = _random_conv_cases(24, 20261016)
 
 
-@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("case", RANDOM_CASES, ids=[c[0] for c in RANDOM_CASES])
 def test_conv3d_random_shapes_vs_torch(case, dtype_name):
     _run_conv_case(case, dtype_name, True)
@@ -263,8 +281,7 @@ def test_conv3d_random_shapes_vs_torch(case, dtype_name):
 def _run_conv_case(case, dtype_name, split):
     from cwdm_hip import _lib
     name, B, grid, c0, c1, cout, amode, use_gn, skip, rmode = case
-    dtype = _lib.CWDM_F32 if dtype_name == "fp32" else _lib.CWDM_BF16
-    tdt = torch.float32 if dtype_name == "fp32" else torch.bfloat16
+    dtype, tdt = _DTN[dtype_name]
     g = torch.Generator().manual_seed(7)
     D, H, W = grid
     sD, sH, sW = {0: (D, H, W), 1: (D // 2, H // 2, W // 2), 2: (2 * D, 2 * H, 2 * W)}[amode]
@@ -290,8 +307,8 @@ def _run_conv_case(case, dtype_name, split):
         h = F.avg_pool3d(h, 2)
     elif amode == 1:
         h = F.interpolate(h, scale_factor=2, mode="nearest")
-    if dtype_name == "bf16":
-        h = h.to(tdt).float()   # the kernel stages the transformed halo in bf16
+    if dtype_name != "fp32":
+        h = h.to(tdt).float()   # the kernel stages the transformed halo in bf16 / fp16
     ref = F.conv3d(h, wq, bias, padding=1)
     wb = b0 = b1 = None
     if skip:
@@ -311,7 +328,7 @@ def _run_conv_case(case, dtype_name, split):
         wb=wb.to(tdt).float().to(DEV) if skip else None, res=_nd(res).to(DEV, tdt) if res is not None else None,
         rmode=rmode, out_f32=(cout == 8), split=split)
     got = _nc(out.float().cpu())
-    tol = 2e-5 if dtype_name == "fp32" else 2e-2
+    tol = {"fp32": 2e-5, "bf16": 2e-2, "fp16": 3e-3}[dtype_name]   # output rounding: 2^-8 / 2^-11
     assert rel_err(got, ref) < tol, name
     # per-channel statistics of the stored (pre-rounding) output
     s = st.sum(1).cpu()
@@ -335,7 +352,7 @@ V4_CASES = [
 ]
 
 
-@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("case", V4_CASES, ids=[c[0] for c in V4_CASES])
 def test_conv3d_dma_kernel_vs_torch(case, dtype_name):
     """The DMA-staged wide-grid kernel (conv3d_v4.hpp), forced on small shapes,
@@ -363,33 +380,35 @@ SG_CASES = [
 ]
 
 
+@pytest.mark.parametrize("dtype_name", ["bf16", "fp16"])
 @pytest.mark.parametrize("case", SG_CASES, ids=[c[0] for c in SG_CASES])
-def test_conv3d_small_grid_kernel_vs_torch(case):
+def test_conv3d_small_grid_kernel_vs_torch(case, dtype_name):
     """The small-grid kernel (16^3 / 8^3 levels: one statistics brick x 16 output
     channels per workgroup, whole K, 16x16x32 MFMA) against F.conv3d, with the
     per-brick GroupNorm partials."""
-    _run_conv_case(case, "bf16", True)
+    _run_conv_case(case, dtype_name, True)
 
 
+@pytest.mark.parametrize("dtype_name", ["bf16", "fp16"])
 @pytest.mark.parametrize("grid,B,cin", [((4, 4, 32), 1, 64), ((8, 8, 64), 2, 64), ((4, 8, 32), 1, 32)])
-def test_output_head_kernel_vs_torch(grid, B, cin):
+def test_output_head_kernel_vs_torch(grid, B, cin, dtype_name):
     """The narrow-output head kernel (conv3d_head.hip: GN+SiLU fused, 16x16x32
-    MFMA, 8 of 16 output lanes real): bf16 operands, fp32 output, vs F.conv3d."""
-    from cwdm_hip import _lib
+    MFMA, 8 of 16 output lanes real): bf16 / fp16 operands, fp32 output, vs F.conv3d."""
+    dtype, tdt = _DTN[dtype_name]
     g = torch.Generator().manual_seed(11)
     D, H, W = grid
     cout = 8
-    x = torch.randn(B, cin, D, H, W, generator=g).to(torch.bfloat16).float()
-    w = (torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)).to(torch.bfloat16).float()
+    x = torch.randn(B, cin, D, H, W, generator=g).to(tdt).float()
+    w = (torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)).to(tdt).float()
     bias = torch.randn(cout, generator=g) * 0.1
     scale = 1 + 0.2 * torch.randn(B, cin, generator=g)
     shift = 0.2 * torch.randn(B, cin, generator=g)
     gn = torch.stack([scale, shift], -1).contiguous()
-    h = F.silu(x * scale[:, :, None, None, None] + shift[:, :, None, None, None]).to(torch.bfloat16).float()
+    h = F.silu(x * scale[:, :, None, None, None] + shift[:, :, None, None, None]).to(tdt).float()
     ref = F.conv3d(h, w, bias, padding=1)
-    out, _ = _conv_call(_lib.CWDM_BF16, (B, D, H, W), _nd(x).to(DEV, torch.bfloat16), None, 0, gn.to(DEV),
+    out, _ = _conv_call(dtype, (B, D, H, W), _nd(x).to(DEV, tdt), None, 0, gn.to(DEV),
                         w.to(DEV), bias.to(DEV), out_f32=True, stats=False)
-    assert rel_err(_nc(out.float().cpu()), ref) < 1e-2
+    assert rel_err(_nc(out.float().cpu()), ref) < (1e-2 if dtype_name == "bf16" else 1e-3)
 
 
 def test_gn_apply_matches_torch():
@@ -448,11 +467,11 @@ def test_copy3_layouts():
     assert torch.equal(back.cpu(), x.to(torch.bfloat16).float().cpu())
 
 
-@pytest.mark.parametrize("dtype_name", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype_name", ["fp32", "bf16", "fp16"])
 def test_gn_silu_pool(dtype_name):
     from cwdm_hip import _lib
     from cwdm_hip._lib import check, lib
-    tdt = torch.float32 if dtype_name == "fp32" else torch.bfloat16
+    dt, tdt = _DTN[dtype_name]
     g = torch.Generator().manual_seed(9)
     B, C, d = 2, 64, 4
     x = torch.randn(B, C, 2 * d, 2 * d, 2 * d, generator=g).to(tdt).float()
@@ -462,11 +481,10 @@ def test_gn_silu_pool(dtype_name):
     xd = _nd(x).to(DEV, tdt)
     oh = torch.empty(B, d, d, d, C, device=DEV, dtype=tdt)
     ox = torch.empty_like(oh)
-    dt = _lib.CWDM_F32 if dtype_name == "fp32" else _lib.CWDM_BF16
     check(lib().cwdm_gn_silu_pool(ctypes.c_void_p(xd.data_ptr()), C, ctypes.c_void_p(gn.data_ptr()), B, d, d, d, dt,
                                   ctypes.c_void_p(oh.data_ptr()), ctypes.c_void_p(ox.data_ptr()), None))
     h = F.avg_pool3d(F.silu(x * scale[:, :, None, None, None] + shift[:, :, None, None, None]), 2)
-    tol = 1e-5 if dtype_name == "fp32" else 1e-2
+    tol = {"fp32": 1e-5, "bf16": 1e-2, "fp16": 2e-3}[dtype_name]
     assert rel_err(_nc(oh.float().cpu()), h) < tol
     assert rel_err(_nc(ox.float().cpu()), F.avg_pool3d(x, 2)) < tol
 
@@ -530,7 +548,7 @@ def _haar_nd(src, C, d, h, w, inverse=0, high_in=None, lll=1.0, high=1.0, all8=0
     from cwdm_hip.ops import _stream
     L = _lib.lib()
     B = src.shape[0]
-    dt = _lib.CWDM_BF16 if src.dtype == torch.bfloat16 else _lib.CWDM_F32
+    dt = {torch.bfloat16: _lib.CWDM_BF16, torch.float16: _lib.CWDM_F16}.get(src.dtype, _lib.CWDM_F32)
     shape = (B, 2 * d, 2 * h, 2 * w, C) if inverse else ((B, d, h, w, 8, C) if all8 else (B, d, h, w, C))
     out = torch.empty(shape, dtype=src.dtype, device=DEV)
     ho = torch.empty((B, d, h, w, 7, C), dtype=src.dtype, device=DEV) if want_high else None
@@ -558,7 +576,7 @@ def _cl(x):  # NCDHW -> NDHWC
 
 @pytest.mark.parametrize("C", [32, 96])
 @pytest.mark.parametrize("grid", [(3, 5, 4), (8, 8, 6)])
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_haar_nd_analysis_vs_oracle(C, grid, dtype):
     """Downsample(use_freq) of a ResBlock (wunet.py:120-128, :239-252): LLL x 1/3
     + emb bias and the 7 high bands, bit-exact vs the oracle DWT on the same
@@ -593,7 +611,7 @@ def test_haar_nd_all_bands_pyramid_vs_oracle():
 
 
 @pytest.mark.parametrize("C", [64, 40])
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_haar_nd_synthesis_vs_oracle(C, dtype):
     """Upsample(use_freq) of a ResBlock (wunet.py:62-80, :236-252): IDWT(3 h,
     skip bands) + emb bias, bit-exact vs the oracle IDWT; statistics vs float64."""

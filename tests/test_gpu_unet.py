@@ -28,7 +28,7 @@ def _product_model(cfg, groups, params, dtype):
     return m.to(DEV)
 
 
-@pytest.mark.parametrize("dtype,tol", [("fp32", 1e-3), ("bf16", 6e-2)])
+@pytest.mark.parametrize("dtype,tol", [("fp32", 1e-3), ("bf16", 6e-2), ("fp16", 1e-2)])
 def test_tiny_unet_forward_and_trace(dtype, tol):
     cfg, G = cases.C1_CFG, cases.C1_GROUPS
     P = ou.random_params(seed=1, **cfg)
@@ -84,21 +84,23 @@ def test_production_unet_forward_dma_kernel(grid):
             # the oracle at every grid, including 32x32x64 (R0 and R1 on the DMA kernel, the
             # 16^3-class levels on the small-grid kernel)
             assert rel_err(out, ou.unet_forward(P, x, t)) < 1e-3
-            m16 = _product_model(cfg, 32, P, "bf16")
-            assert rel_err(m16(x.to(DEV), t.to(DEV)), out) < 6e-2
+            for half, tol in (("bf16", 6e-2), ("fp16", 1e-2)):
+                m16 = _product_model(cfg, 32, P, half)
+                assert rel_err(m16(x.to(DEV), t.to(DEV)), out) < tol, half
     finally:
         lib().cwdm_conv3d_set_path(prev)
 
 
-def test_production_unet_bf16_close_to_fp32():
+@pytest.mark.parametrize("half,tol", [("bf16", 6e-2), ("fp16", 1e-2)])
+def test_production_unet_half_close_to_fp32(half, tol):
     P = ou.random_params(seed=12)
     cfg = dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4))
     m32 = _product_model(cfg, 32, P, "fp32")
-    m16 = _product_model(cfg, 32, P, "bf16")
+    m16 = _product_model(cfg, 32, P, half)
     x = torch.randn(1, 32, 32, 32, 32, device=DEV)
     t = torch.tensor([250], device=DEV)
     a, b = m32(x, t), m16(x, t)
-    assert rel_err(b, a) < 6e-2
+    assert rel_err(b, a) < tol
 
 
 def _c1_product(dtype):
@@ -245,7 +247,7 @@ def test_graph_loop_leaves_caller_noise_unchanged():
     assert out.data_ptr() != x_dev.data_ptr() and torch.isfinite(out).all()
 
 
-@pytest.mark.parametrize("respacing,dtype", [("", "fp32"), ("ddim10", "bf16")])
+@pytest.mark.parametrize("respacing,dtype", [("", "fp32"), ("ddim10", "bf16"), ("ddim10", "fp16")])
 def test_hip_graph_loop_equals_eager_loop(respacing, dtype):
     """The graph-captured sampling step (one capture, replayed per timestep,
     noise from torch's graph-safe generator) reproduces the eager loop with
@@ -306,7 +308,7 @@ S2_CFGS = [(dict(in_channels=32, model_channels=32, out_channels=8, num_res_bloc
 
 
 @pytest.mark.parametrize("k", [0, 1], ids=["tiny", "runsh"])
-@pytest.mark.parametrize("dtype,tol", [("fp32", 1e-3), ("bf16", 6e-2)])
+@pytest.mark.parametrize("dtype,tol", [("fp32", 1e-3), ("bf16", 6e-2), ("fp16", 1e-2)])
 def test_unet_resblock_updown_false_forward_vs_oracle(k, dtype, tol):
     """resblock_updown=False: Downsample(use_conv=True) = stride-2 Conv3d (run as
     a stride-1 conv over the space-to-depth input) and Upsample(use_conv=True) =
@@ -400,7 +402,7 @@ def _wavunet(k, dtype, seed=21):
 
 
 @pytest.mark.parametrize("k,dtype,tol", [("tiny", "fp32", 1e-3), ("three", "fp32", 1e-3), ("prod", "fp32", 1e-3),
-                                         ("tiny", "bf16", 6e-2)])
+                                         ("tiny", "bf16", 6e-2), ("tiny", "fp16", 1e-2)])
 def test_wavunet_forward_vs_oracle(k, dtype, tol):
     """WavUNetModel (use_freq=True, wunet.py:754-795) forward on the native plan:
     DWT/IDWT ResBlocks, wavelet input pyramid, the reused decoder ResBlock

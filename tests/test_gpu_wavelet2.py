@@ -133,14 +133,16 @@ def test_config5_fats_loop_vs_oracle(sampler):
     assert torch.allclose(img.cpu(), w2.synthesis2(ref), atol=1e-3 * float(ref.abs().max()) * 8)
 
 
-def test_config5_graph_loop_bf16_runs_at_224():
-    """The config-5 sizes themselves: 224^3 -> 56^3 x 64 channels, bf16 graph
-    loop, 3 steps; finite, and the eager loop agrees with the graph replay."""
+@pytest.mark.parametrize("dtype", ["fp16", "bf16"])
+def test_config5_graph_loop_runs_at_224(dtype):
+    """The config-5 sizes themselves: 224^3 -> 56^3 x 64 channels, fp16 (the
+    config's dtype) and bf16 graph loops, 3 steps; finite, and the eager loop
+    agrees with the graph replay."""
     from guided_diffusion import script_util
     model = script_util.create_model(image_size=224, num_channels=64, num_res_blocks=2, channel_mult="1,2,2",
                                      attention_resolutions="", dims=3, num_groups=32, in_channels=256,
                                      out_channels=64, bottleneck_attention=False, resample_2d=False,
-                                     resblock_updown=True, compute_dtype="bf16").to(DEV)
+                                     resblock_updown=True, compute_dtype=dtype).to(DEV)
     diffusion = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
                                                       timestep_respacing="3", wavelet_levels=2)
     g = torch.Generator(device=DEV).manual_seed(1)
@@ -213,3 +215,81 @@ def test_config5_training_step_vs_oracle():
     for n, p in model.named_parameters():
         err = float((p.grad.double().cpu() - Pr[n].grad.double()).norm() / Pr[n].grad.double().norm().clamp_min(1e-30))
         assert err < 1e-3, (n, err)
+
+
+def test_config5_fp16_loop_close_to_oracle():
+    """Config 5 as specified, fp16 (BASELINE.json config 5): the reduced-size
+    FATS pipeline of test_config5_fats_loop_vs_oracle (32^3 images, 2-level
+    analysis, 3-level U-Net, 10 ddim10 DDPM steps) with the U-Net in fp16
+    against the fp32 oracle loop.  Measured bound."""
+    from cwdm_hip import ops
+    from guided_diffusion import script_util
+    shift = [-1.5, 0.2, 0.3, 0.5, 0.2, 0.4, 0.6, 1.0] + [0.8, 1.0, 1.2, 1.0, 1.2, 1.4, 1.8]
+    diffusion = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
+                                                      timestep_respacing="ddim10", band_log_snr_shift=shift,
+                                                      wavelet_levels=2)
+    P = ou.random_params(seed=2, **C5_CFG)
+    outs = {}
+    vols = cases.data.brats_batch(32, seed=9, batch=1)
+    cond = torch.cat([w2.analysis2(vols[k]) for k in ("t1c", "t2w", "t2f")], dim=1)
+    g = torch.Generator().manual_seed(12)
+    x_T = torch.randn(1, 64, 8, 8, 8, generator=g)
+    noises = [torch.randn(x_T.shape, generator=g) for _ in range(10)]
+    for dt in ("fp16", "bf16"):
+        model = _c5_model(dt)
+        model.load_state_dict(P)
+        model.to(DEV)
+        it = iter([z.to(DEV) for z in noises])
+        outs[dt] = diffusion.p_sample_loop(model, x_T.shape, noise=x_T.to(DEV), cond=cond.to(DEV).contiguous(),
+                                           progress=False, noise_fn=lambda x: next(it)).cpu()
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"), use_timesteps=od.space_timesteps(1000, "ddim10"),
+                    band_shift=w2.channel_shift(shift))
+    ref = od.p_sample_loop(tab, ou.OracleUNet(P, num_groups=8, **C5_CFG), x_T, cond, noises,
+                           process=w2.process_xstart2)
+    errs = {dt: float((o.double() - ref.double()).norm() / ref.double().norm()) for dt, o in outs.items()}
+    print("config-5 10-step loop vs fp32 oracle, rel L2:", errs)
+    assert errs["fp16"] < 1e-2, errs
+    assert errs["fp16"] < errs["bf16"], errs
+
+
+def test_config5_fp16_training_gradients_with_loss_scaling():
+    """Config-5 training in fp16: the MSE gradient of the 64-channel output is
+    far below fp16's normal range, so training scales the loss (amp.GradScaler,
+    the reference's use_fp16 path, train_util.py:84-87, :457-458) and unscales
+    the flat gradient before AdamW.  Scaled fp16 gradients vs the fp32 oracle's
+    autograd."""
+    from cwdm_hip.optim import FlatAdamW
+    from guided_diffusion import script_util
+    shift = [-1.5, 0.2, 0.3, 0.5, 0.2, 0.4, 0.6, 1.0] + [0.8, 1.0, 1.2, 1.0, 1.2, 1.4, 1.8]
+    diffusion = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
+                                                      band_log_snr_shift=shift, wavelet_levels=2)
+    P = ou.random_params(seed=21, **C5_CFG)
+    model = _c5_model("fp16")
+    model.load_state_dict(P)
+    model.to(DEV)
+    vols = {k: v.to(DEV) for k, v in cases.data.brats_batch(32, seed=5, batch=2).items()}
+    t = torch.tensor([11, 802], device=DEV)
+    noise = torch.randn(2, 1, 32, 32, 32, generator=torch.Generator().manual_seed(8)).to(DEV)
+    terms, out, _ = diffusion.training_losses(model, vols, t, mode="i2i", contr="t1n", noise=noise)
+    scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 16)
+    scaler.scale(terms["mse_wav"].mean()).backward()
+    opt = FlatAdamW(model, lr=1e-5, weight_decay=0.0)
+    scaler.unscale_(opt)
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"), band_shift=w2.channel_shift(shift))
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+
+    def om(x, tt, **kw):
+        return ou.unet_forward(Pr, x, tt, num_groups=8, **C5_CFG)
+    rterms, rout, _ = od.training_losses(tab, om, {k: v.cpu() for k, v in vols.items()}, t.cpu(), noise.cpu(),
+                                         contr="t1n", levels=2)
+    rterms["mse_wav"].mean().backward()
+    assert rel_err(out.detach(), rout.detach()) < 1e-2
+    worst = {n: float((p.grad.double().cpu() - Pr[n].grad.double()).norm() / Pr[n].grad.double().norm().clamp_min(1e-30))
+             for n, p in model.named_parameters()}
+    top = sorted(worst.items(), key=lambda kv: -kv[1])[:5]
+    print("fp16 + loss scaling, worst gradients vs fp32 oracle:", top)
+    assert top[0][1] < 3e-2, top
+    before = model.flat_params.clone()
+    scaler.step(opt)
+    scaler.update()
+    assert not torch.equal(before, model.flat_params)    # finite gradients: the step was taken
