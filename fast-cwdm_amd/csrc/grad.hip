@@ -166,7 +166,8 @@ __global__ void __launch_bounds__(512) gn_bwd_finalize_kernel(const float* __res
                                                              int B, const float* __restrict__ gamma,
                                                              const float* __restrict__ mr, int groups,
                                                              long long V, float* __restrict__ coef,
-                                                             float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                             float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                             int acc_affine) {
   __shared__ double sA[1024], sB[1024], s1[256], s2[256], rA[512], rB[512];
   const int cpg = C / groups;
   // C <= 512: `sub` threads per channel split the partial blocks; C > 512: 2 channels per thread
@@ -241,9 +242,9 @@ __global__ void __launch_bounds__(512) gn_bwd_finalize_kernel(const float* __res
   }
   for (int k = 0; k < 2; ++k) {
     const int c = threadIdx.x + 512 * k;
-    if (c < C) {
-      dgamma[c] = (float)dg[k];
-      dbeta[c] = (float)db[k];
+    if (c < C) {   // acc_affine: a GroupNorm whose parameters serve two calls (WavUNetModel's reused blocks)
+      dgamma[c] = acc_affine ? dgamma[c] + (float)dg[k] : (float)dg[k];
+      dbeta[c] = acc_affine ? dbeta[c] + (float)db[k] : (float)db[k];
     }
   }
 }
@@ -438,7 +439,7 @@ __device__ __forceinline__ float dsilu_ref(float z) {
 __global__ void __launch_bounds__(256) emb_bwd_w_kernel(const float* __restrict__ dEb, int R, int n, int B,
                                                        const float* __restrict__ temb, int E,
                                                        float* __restrict__ dw, float* __restrict__ db,
-                                                       float* __restrict__ dcb) {
+                                                       float* __restrict__ dcb, int acc) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long long)n * E) return;
   const int r = (int)(i / E), e = (int)(i % E);
@@ -448,10 +449,10 @@ __global__ void __launch_bounds__(256) emb_bwd_w_kernel(const float* __restrict_
     s += g * silu_ref(temb[(long long)b * E + e]);
     sb += g;
   }
-  dw[i] = s;
+  dw[i] = acc ? dw[i] + s : s;
   if (e == 0) {
-    db[r] = sb;
-    if (dcb) dcb[r] = sb;
+    db[r] = acc ? db[r] + sb : sb;
+    if (dcb) dcb[r] = acc ? dcb[r] + sb : sb;
   }
 }
 
@@ -552,9 +553,9 @@ long long gn_bwd_blocks(int C, long long V) {
 }  // namespace
 
 int launch_emb_bwd(const float* dEb, int R, int n, int B, const float* temb, int E, const float* W, float* dw,
-                   float* db, float* dcb, float* dsil, hipStream_t s) {
+                   float* db, float* dcb, float* dsil, hipStream_t s, int acc) {
   hipLaunchKernelGGL(emb_bwd_w_kernel, dim3((unsigned)ceil_div((long long)n * E, 256)), dim3(256), 0, s, dEb, R, n,
-                     B, temb, E, dw, db, dcb);
+                     B, temb, E, dw, db, dcb, acc);
   CWDM_LAUNCHED();
   hipLaunchKernelGGL(emb_bwd_x_kernel, dim3((unsigned)ceil_div(E, 64), B, (unsigned)ceil_div(n, 32)), dim3(256), 0, s,
                      dEb, R, n, W, E, dsil);
@@ -577,7 +578,7 @@ int launch_temb_bwd(const float* t, int B, int mc, const float* w1, const float*
 int gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode, const float* ss,
                      const float* mr, const float* gamma, int groups, int64_t B, int64_t d, int64_t h, int64_t w,
                      int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma, float* dbeta, void* ws,
-                     int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream);
+                     int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream, int acc_affine);
 }  // namespace cwdm
 
 using namespace cwdm;
@@ -597,7 +598,7 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
                            const float* ss, const float* mr, const float* gamma, int groups, int64_t B, int64_t d,
                            int64_t h, int64_t w, int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma,
                            float* dbeta, void* ws, int64_t ws_bytes, float* chs, int64_t chs_stride,
-                           cwdm_stream_t stream) {
+                           cwdm_stream_t stream, int acc_affine) {
   CWDM_REQUIRE(!chs || (c1 == 0 && chs_stride >= c0), CWDM_E_UNSUPPORTED,
                "gn_silu_bwd: fused channel sums need one source");
   CWDM_REQUIRE(x0 && du && ss && mr && gamma && dx0 && dgamma && dbeta && ws, CWDM_E_INVALID,
@@ -638,7 +639,7 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
        })))
     return rc;
   hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(512), 0, s, part, (int)nb, C, (int)B, gamma, mr, groups, V,
-                     coef, dgamma, dbeta);
+                     coef, dgamma, dbeta, acc_affine);
   CWDM_LAUNCHED();
   // workgroups of (256 / ncg) voxels x ncg channel groups; two voxels per
   // thread (the kernel's UNR; du_mode 1 loops twice instead); with channel
@@ -676,7 +677,7 @@ extern "C" int cwdm_gn_silu_bwd(const void* x0, int c0, const void* x1, int c1, 
                                 int64_t d, int64_t h, int64_t w, int dtype, void* dx0, int acc0, void* dx1, int acc1,
                                 float* dgamma, float* dbeta, void* ws, int64_t ws_bytes, cwdm_stream_t stream) {
   return gn_silu_bwd_impl(x0, c0, x1, c1, du, du_mode, ss, mr, gamma, groups, B, d, h, w, dtype, dx0, acc0, dx1, acc1,
-                          dgamma, dbeta, ws, ws_bytes, nullptr, 0, stream);
+                          dgamma, dbeta, ws, ws_bytes, nullptr, 0, stream, 0);
 }
 
 extern "C" int cwdm_resample_add(void* dst, const void* src, int C, int64_t B, int64_t d, int64_t h, int64_t w,

@@ -21,14 +21,18 @@ int launch_emb_proj(const float* temb, int B, int E, const float* W, const float
                     hipStream_t s);
 int launch_vec_add(const float* a, const float* b, float* out, int64_t n, hipStream_t s);
 int launch_emb_bwd(const float* dEb, int R, int n, int B, const float* temb, int E, const float* W, float* dw,
-                   float* db, float* dcb, float* dsil, hipStream_t s);
+                   float* db, float* dcb, float* dsil, hipStream_t s, int acc);
 int launch_temb_bwd(const float* t, int B, int mc, const float* w1, const float* b1, const float* w2,
                     const float* temb, const float* dsil, float* dw1, float* db1, float* dw2, float* db2,
                     hipStream_t s);
 int gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode, const float* ss,
                      const float* mr, const float* gamma, int groups, int64_t B, int64_t d, int64_t h, int64_t w,
                      int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma, float* dbeta, void* ws,
-                     int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream);
+                     int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream, int acc_affine);
+int haar_nd_synth_add(int dtype, int64_t B, int64_t d, int64_t h, int64_t w, int C, const void* L, int64_t l_vs,
+                      float lll, const void* H, int64_t h_vs, float high, void* fine, int acc, hipStream_t s);
+int haar_nd_anal_add(int dtype, int64_t B, int64_t d, int64_t h, int64_t w, int C, const void* fine, void* L,
+                     int64_t l_vs, float lll, int accL, void* H, int64_t h_vs, float high, int accH, hipStream_t s);
 }  // namespace cwdm
 
 using namespace cwdm;
@@ -101,9 +105,11 @@ struct Block {
   int x0, x1;                 // input tensors (x1 = -1 unless decoder concat)
   int updown;                 // 0 none, 1 up, 2 down; layers without a ResBlock (resblock_updown=False):
                               // 3 Downsample stride-2 conv (c1, pool = its S2dStep), 4 Upsample nearest + conv (c1);
-                              // WavUNetModel ResBlocks: 5 down (DWT), 6 up (IDWT)
+                              // WavUNetModel ResBlocks: 5 down (DWT), 6 up (IDWT); 7 WaveletDownsample of the input
+                              // pyramid (pool = its HaarStep, c1 = its conv, x0 = the pyramid level it transforms)
   int p_begin, p_end;         // parameter index range
   int emb_k;                  // index into emb_rows_*
+  int hh = -1, hx = -1;       // WavUNetModel down / up blocks: HaarSteps of h (+ emb) and of x (x_upd)
 };
 
 }  // namespace
@@ -276,12 +282,14 @@ void build(cwdm_unet* u) {
       }
       hh.emb_row = row; hh.stats = true; hh.level = down ? lout : lin;
       haar_step(hh);
+      blk.hh = (int)u->haars.size() - 1;
       if (skip_out) *skip_out = hh.high_out;
       // x: the same resampling, LLL only / with the same skip bands (x_upd)
       HaarStep hx = hh;
       hx.src = x0; hx.out = new_tensor(lout, cin); hx.high_out = -1; hx.emb_row = -1; hx.stats = false;
       u->tensors[hx.out].stats_kind = -1;
       haar_step(hx);
+      blk.hx = (int)u->haars.size() - 1;
       const int g2 = gn_step(p + ".out_layers.0", hh.out, -1, lout);
       blk.g2 = g2;
       ConvStep c2{};
@@ -410,6 +418,10 @@ void build(cwdm_unet* u) {
       hp.out = new_tensor(level, 8 * cp);
       u->tensors[hp.out].stats_kind = -1;
       haar_step(hp);
+      Block pb{};   // the WaveletDownsample as a backward segment of its own
+      pb.updown = 7; pb.pool = (int)u->haars.size() - 1; pb.x0 = pyr; pb.x1 = -1;
+      pb.g1 = pb.g2 = pb.c2 = -1; pb.emb_k = -1;
+      pb.p_begin = (int)u->params.size();
       ConvStep cs{};
       conv_params("input_blocks." + std::to_string(idx + 1) + ".0.conv", ch, 8 * cp, 3, &cs.w_p, &cs.b_p);
       cs.a0 = hp.out; cs.a1 = -1; cs.amode = 0; cs.gn = -1; cs.cin_a = 8 * cp;
@@ -418,6 +430,9 @@ void build(cwdm_unet* u) {
       h = pyr = cs.out = new_tensor(level, ch);
       u->convs.push_back(cs);
       u->steps.push_back({1, (int)u->convs.size() - 1});
+      pb.c1 = (int)u->convs.size() - 1;
+      pb.p_end = (int)u->params.size();
+      u->blocks.push_back(pb);
       u->trace.push_back(h); u->trace_level.push_back(level);
       idx += 2;
     }
@@ -1096,7 +1111,6 @@ extern "C" int64_t cwdm_unet_packed_bwd_bytes(const cwdm_unet* u) { return u ? u
 
 extern "C" int cwdm_unet_pack_bwd(const cwdm_unet* u, const float* const* P, void* packed_bwd, cwdm_stream_t stream) {
   CWDM_REQUIRE(u && P && packed_bwd, CWDM_E_INVALID, "cwdm_unet_pack_bwd: null pointer");
-  CWDM_REQUIRE(!u->cfg.use_freq, CWDM_E_UNSUPPORTED, "cwdm_unet_pack_bwd: the WavUNetModel plan is forward-only");
   auto* base = reinterpret_cast<unsigned char*>(packed_bwd);
   int rc;
   for (size_t i = 0; i < u->convs.size(); ++i) {
@@ -1115,7 +1129,7 @@ extern "C" int cwdm_unet_pack_bwd(const cwdm_unet* u, const float* const* P, voi
 }
 
 extern "C" int64_t cwdm_unet_grad_workspace_bytes(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
-  if (!u || u->cfg.use_freq || B <= 0 || D <= 0 || H <= 0 || W <= 0) return -1;
+  if (!u || B <= 0 || D <= 0 || H <= 0 || W <= 0) return -1;
   return glayout(u, B, D, H, W).total;
 }
 
@@ -1153,13 +1167,11 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
                                   int seg_begin, int seg_end, cwdm_stream_t stream) {
   CWDM_REQUIRE(u && packed && packed_bwd && x && t && dout && grads && ws && gws, CWDM_E_INVALID,
                "cwdm_unet_backward: null pointer");
-  CWDM_REQUIRE(!u->cfg.use_freq, CWDM_E_UNSUPPORTED,
-               "cwdm_unet_backward: the WavUNetModel plan is forward-only (sampling); train with UNetModel");
   const int nseg = (int)u->blocks.size() + 2;
   CWDM_REQUIRE(0 <= seg_begin && seg_begin <= seg_end && seg_end <= nseg, CWDM_E_INVALID,
                "cwdm_unet_backward: bad segment range");
   CWDM_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0, CWDM_E_SHAPE, "cwdm_unet_backward: empty grid");
-  const int64_t div = int64_t(1) << (u->cfg.num_levels - 1);
+  const int64_t div = int64_t(1) << (u->cfg.num_levels - (u->cfg.use_freq ? 0 : 1));
   CWDM_REQUIRE(D % div == 0 && H % div == 0 && W % div == 0, CWDM_E_SHAPE,
                "cwdm_unet_backward: every subband edge must be divisible by " + std::to_string(div));
   Layout L = layout(u, B, D, H, W);
@@ -1227,9 +1239,10 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
     const int lv = g.level;
     const int c0 = u->tensors[x0].channels, c1 = x1 >= 0 ? u->tensors[x1].channels : 0;
     const int a0 = take_acc(x0), a1 = take_acc(x1);
-    return cwdm_gn_silu_bwd(act(x0), c0, act(x1), c1, tmp, du_mode, ss_of(gi), mr_of(gi), P(g.gamma_off),
+    // affine gradients accumulate (zeroed at segment 0): a reused WavUNetModel block adds its second use
+    return gn_silu_bwd_impl(act(x0), c0, act(x1), c1, tmp, du_mode, ss_of(gi), mr_of(gi), P(g.gamma_off),
                             u->cfg.num_groups, B, D >> lv, H >> lv, W >> lv, dt, grd(x0), a0, grd(x1), a1,
-                            GR(g.gamma_p), GR(g.beta_p), gb + G.gnws, G.gnws_bytes, stream);
+                            GR(g.gamma_p), GR(g.beta_p), gb + G.gnws, G.gnws_bytes, nullptr, 0, stream, 1);
   };
 
   for (int seg = seg_begin; seg < seg_end; ++seg) {
@@ -1255,6 +1268,100 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
         return rc;
       if ((rc = dgrad(u->head_c, d16))) return rc;
       if ((rc = gn_bwd(u->head_g, hg.src0, -1, 0))) return rc;
+      continue;
+    }
+    if (seg <= nb && u->blocks[nb - seg].updown == 7) {
+      // WavUNetModel WaveletDownsample (wunet.py:131-145): out = conv(cat(DWT(pyr)) / 3) + h
+      const Block& bk = u->blocks[nb - seg];
+      const auto& cs = u->convs[bk.c1];
+      const auto& hp = u->haars[bk.pool];
+      const int o = cs.out;
+      if ((rc = cwdm_channel_sum(grd(o), dt, B, vox(cs.level), cs.cout, cs.cout, nullptr, 0, GR(cs.b_p), nullptr,
+                                 gb + G.chs, G.chs_bytes, stream)))
+        return rc;
+      if ((rc = wgrad(cs.level, 3, act(hp.out), cs.cin_a, nullptr, 0, 0, nullptr, grd(o), cs.cout, cs.cout,
+                      GR(cs.w_p))))
+        return rc;
+      const int lv = cs.level;
+      if ((rc = cwdm_resample_add(grd(cs.res), grd(o), cs.cout, B, D >> lv, H >> lv, W >> lv, 0, take_acc(cs.res), dt,
+                                  stream)))
+        return rc;
+      if (hp.src != u->input_tensor) {   // the level-0 pyramid is the model input: no gradient
+        if ((rc = dgrad(bk.c1, grd(o)))) return rc;
+        const int cp = u->tensors[hp.src].channels;
+        if ((rc = haar_nd_synth_add(dt, B, D >> lv, H >> lv, W >> lv, cp, tmp, 8LL * cp, hp.lll_scale,
+                                    reinterpret_cast<unsigned char*>(tmp) + (int64_t)cp * es, 8LL * cp, hp.high_scale,
+                                    grd(hp.src), take_acc(hp.src), s)))
+          return rc;
+      }
+      continue;
+    }
+    if (seg <= nb && (u->blocks[nb - seg].updown == 5 || u->blocks[nb - seg].updown == 6)) {
+      // WavUNetModel ResBlock that resamples by DWT / IDWT after its first conv (wunet.py:210-269)
+      const Block& bk = u->blocks[nb - seg];
+      const bool down = bk.updown == 5;
+      const auto& c1 = u->convs[bk.c1];
+      const auto& c2 = u->convs[bk.c2];
+      const auto& hh = u->haars[bk.hh];
+      const auto& hx = u->haars[bk.hx];
+      const int lout = c2.level, lin = c1.level;
+      const int64_t Vo = vox(lout);
+      const int o = c2.out, h1 = c1.out, cout = c2.cout, cin = u->tensors[bk.x0].channels;
+      // ---- conv2 + the residual x_upd
+      if ((rc = cwdm_channel_sum(grd(o), dt, B, Vo, cout, cout, nullptr, 0, GR(c2.b_p), nullptr, gb + G.chs,
+                                 G.chs_bytes, stream)))
+        return rc;
+      if ((rc = wgrad(lout, 3, act(hh.out), cout, nullptr, 0, 0, ss_of(bk.g2), grd(o), cout, cout, GR(c2.w_p))))
+        return rc;
+      if ((rc = cwdm_resample_add(grd(hx.out), grd(o), cout, B, D >> lout, H >> lout, W >> lout, 0, take_acc(hx.out),
+                                  dt, stream)))
+        return rc;
+      if ((rc = dgrad(bk.c2, grd(o)))) return rc;
+      // ---- GN2 -> d(h + emb), with its channel sums = the emb projection's gradient
+      const int k = bk.emb_k;
+      const int roff = u->emb_rows_off[k], rn = u->emb_rows_n[k];
+      {
+        const auto& g = u->gns[bk.g2];
+        if ((rc = gn_silu_bwd_impl(act(hh.out), cout, nullptr, 0, tmp, 0, ss_of(bk.g2), mr_of(bk.g2), P(g.gamma_off),
+                                   u->cfg.num_groups, B, D >> lout, H >> lout, W >> lout, dt, grd(hh.out),
+                                   take_acc(hh.out), nullptr, 0, GR(g.gamma_p), GR(g.beta_p), gb + G.gnws,
+                                   G.gnws_bytes, deb + roff, u->R, stream, 1)))
+          return rc;
+      }
+      if ((rc = launch_emb_bwd(deb + roff, u->R, rn, (int)B, temb, u->E, P(u->off_emb_w) + (int64_t)roff * u->E,
+                               GR(u->emb_rows_w[k]), GR(u->emb_rows_b[k]), nullptr, dsil, s, 1)))
+        return rc;
+      // ---- the resampling adjoints (orthonormal Haar: analysis <-> synthesis)
+      const int lc = down ? lout : lin;   // the coarse grid of this block's DWT / IDWT
+      const int64_t dc = D >> lc, hc = H >> lc, wc = W >> lc;
+      if (down) {
+        // h = DWT(h1): LLL / 3 (+ emb) continues, the 7 high bands are the skip
+        const int sk = hh.high_out;
+        const void* dsk = u->ginit[sk] ? grd(sk) : nullptr;   // (no later user: zero)
+        if ((rc = haar_nd_synth_add(dt, B, dc, hc, wc, cout, grd(hh.out), cout, hh.lll_scale, dsk, 7LL * cout,
+                                    hh.high_scale, grd(h1), take_acc(h1), s)))
+          return rc;
+        if ((rc = haar_nd_synth_add(dt, B, dc, hc, wc, cin, grd(hx.out), cin, hx.lll_scale, nullptr, 0, 0.f,
+                                    grd(bk.x0), take_acc(bk.x0), s)))
+          return rc;
+      } else {
+        // h = IDWT(3 h1, skip) (+ emb), x_upd = IDWT(3 x, skip): both feed the skip bands' gradient
+        const int sk = hh.high_in;
+        if ((rc = haar_nd_anal_add(dt, B, dc, hc, wc, cout, grd(hh.out), grd(h1), cout, hh.lll_scale, take_acc(h1),
+                                   grd(sk), 7LL * cout, hh.high_scale, take_acc(sk), s)))
+          return rc;
+        if ((rc = haar_nd_anal_add(dt, B, dc, hc, wc, cin, grd(hx.out), grd(bk.x0), cin, hx.lll_scale,
+                                   take_acc(bk.x0), grd(sk), 7LL * cin, hx.high_scale, take_acc(sk), s)))
+          return rc;
+      }
+      // ---- conv1 (own bias; the emb is added after the resampling) and GN1
+      if ((rc = cwdm_channel_sum(grd(h1), dt, B, vox(lin), cout, cout, nullptr, 0, GR(c1.b_p), nullptr, gb + G.chs,
+                                 G.chs_bytes, stream)))
+        return rc;
+      if ((rc = wgrad(lin, 3, act(bk.x0), cin, nullptr, 0, 0, ss_of(bk.g1), grd(h1), cout, cout, GR(c1.w_p))))
+        return rc;
+      if ((rc = dgrad(bk.c1, grd(h1)))) return rc;
+      if ((rc = gn_bwd(bk.g1, bk.x0, -1, 0))) return rc;
       continue;
     }
     if (seg <= nb && u->blocks[nb - seg].updown >= 3) {
@@ -1342,7 +1449,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
         if ((rc = gn_silu_bwd_impl(act(h1), cout, nullptr, 0, tmp, 0, ss_of(bk.g2), mr_of(bk.g2), P(g.gamma_off),
                                    u->cfg.num_groups, B, D >> lout, H >> lout, W >> lout, dt, grd(h1), take_acc(h1),
                                    nullptr, 0, GR(g.gamma_p), GR(g.beta_p), gb + G.gnws, G.gnws_bytes, deb + roff, u->R,
-                                   stream)))
+                                   stream, 1)))
           return rc;
       } else {
         if ((rc = gn_bwd(bk.g2, h1, -1, 0))) return rc;
@@ -1352,7 +1459,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
       }
       // ---- conv1: emb projection, wgrad, dgrad
       if ((rc = launch_emb_bwd(deb + roff, u->R, rn, (int)B, temb, u->E, P(u->off_emb_w) + (int64_t)roff * u->E,
-                               GR(u->emb_rows_w[k]), GR(u->emb_rows_b[k]), GR(u->emb_rows_cb[k]), dsil, s)))
+                               GR(u->emb_rows_w[k]), GR(u->emb_rows_b[k]), GR(u->emb_rows_cb[k]), dsil, s, 1)))
         return rc;
       if (bk.updown == 2) {
         const auto& ps = u->pools[bk.pool];

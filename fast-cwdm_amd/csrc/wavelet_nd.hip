@@ -146,7 +146,141 @@ __global__ void __launch_bounds__(256) haar_nd_kernel(cwdm_haar_nd_desc a, int p
   }
 }
 
+// ---- adjoints for the backward (WavUNetModel training) ---------------------
+// One thread = one coarse voxel x 8 channels.  Haar is orthonormal, so the
+// adjoint of the analysis is the synthesis and vice versa; the scales of the
+// forward (LLL x lll, highs x high) carry over.  Band k (1..7) of a high-band
+// tensor sits at H + v * h_vs + (k - 1) * C (band-major channels, as
+// cwdm_haar_nd writes them); L / H voxel strides in elements (the pyramid's
+// all-band conv input is L = g, H = g + C with stride 8 C).
+template <typename T>
+__global__ void __launch_bounds__(256) haar_nd_synth_kernel(int64_t n, int C, int64_t d, int64_t h, int64_t w,
+                                                           const T* __restrict__ L, int64_t l_vs, float lll,
+                                                           const T* __restrict__ H, int64_t h_vs, float high,
+                                                           T* __restrict__ fine, int acc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int G = C / 8, g = (int)(i % G);
+  const int64_t cv = i / G, nv = d * h * w;
+  const int64_t b = cv / nv, v = cv - b * nv;
+  const int64_t x = v % w, y = (v / w) % h, z = v / (w * h);
+  float band[8][8];
+  load8(L + cv * l_vs + g * 8, band[0]);
+#pragma unroll
+  for (int k = 1; k < 8; ++k) {
+    if (H) load8(H + cv * h_vs + (k - 1) * C + g * 8, band[k]);
+    else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) band[k][e] = 0.f;
+    }
+  }
+  float blk[8][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float o[8], r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = band[k][e] * (k == 0 ? lll : high);
+    haar_inv8(o, r);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) blk[q][e] = r[q];
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int pa = q >> 2, pb = (q >> 1) & 1, pc = q & 1;
+    T* f = fine + (((b * 2 * d + 2 * z + pa) * 2 * h + 2 * y + pb) * 2 * w + 2 * x + pc) * C + g * 8;
+    if (acc) {
+      float o[8];
+      load8(f, o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) blk[q][e] += o[e];
+    }
+    store8(f, blk[q]);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) haar_nd_anal_kernel(int64_t n, int C, int64_t d, int64_t h, int64_t w,
+                                                          const T* __restrict__ fine, T* __restrict__ L, int64_t l_vs,
+                                                          float lll, int accL, T* __restrict__ H, int64_t h_vs,
+                                                          float high, int accH) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int G = C / 8, g = (int)(i % G);
+  const int64_t cv = i / G, nv = d * h * w;
+  const int64_t b = cv / nv, v = cv - b * nv;
+  const int64_t x = v % w, y = (v / w) % h, z = v / (w * h);
+  float blk[8][8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int pa = q >> 2, pb = (q >> 1) & 1, pc = q & 1;
+    load8(fine + (((b * 2 * d + 2 * z + pa) * 2 * h + 2 * y + pb) * 2 * w + 2 * x + pc) * C + g * 8, blk[q]);
+  }
+  float band[8][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float vin[8], o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) vin[q] = blk[q][e];
+    haar_fwd8(vin, o);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) band[k][e] = o[k] * (k == 0 ? lll : high);
+  }
+  if (L) {
+    T* p = L + cv * l_vs + g * 8;
+    if (accL) {
+      float o[8];
+      load8(p, o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) band[0][e] += o[e];
+    }
+    store8(p, band[0]);
+  }
+  if (H) {
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      T* p = H + cv * h_vs + (k - 1) * C + g * 8;
+      if (accH) {
+        float o[8];
+        load8(p, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) band[k][e] += o[e];
+      }
+      store8(p, band[k]);
+    }
+  }
+}
+
 }  // namespace
+
+int haar_nd_synth_add(int dtype, int64_t B, int64_t d, int64_t h, int64_t w, int C, const void* L, int64_t l_vs,
+                      float lll, const void* H, int64_t h_vs, float high, void* fine, int acc, hipStream_t s) {
+  CWDM_REQUIRE(L && fine && C % 8 == 0 && dtype_compute(dtype), CWDM_E_INVALID, "haar_nd_synth_add: bad argument");
+  const int64_t n = B * d * h * w * (C / 8);
+  return dispatch_dtype(dtype, [&](auto tag) -> int {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(haar_nd_synth_kernel<T>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, n, C, d, h, w,
+                       reinterpret_cast<const T*>(L), l_vs, lll, reinterpret_cast<const T*>(H), h_vs, high,
+                       reinterpret_cast<T*>(fine), acc);
+    CWDM_LAUNCHED();
+    return CWDM_OK;
+  });
+}
+
+int haar_nd_anal_add(int dtype, int64_t B, int64_t d, int64_t h, int64_t w, int C, const void* fine, void* L,
+                     int64_t l_vs, float lll, int accL, void* H, int64_t h_vs, float high, int accH, hipStream_t s) {
+  CWDM_REQUIRE(fine && (L || H) && C % 8 == 0 && dtype_compute(dtype), CWDM_E_INVALID,
+               "haar_nd_anal_add: bad argument");
+  const int64_t n = B * d * h * w * (C / 8);
+  return dispatch_dtype(dtype, [&](auto tag) -> int {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(haar_nd_anal_kernel<T>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, n, C, d, h, w,
+                       reinterpret_cast<const T*>(fine), reinterpret_cast<T*>(L), l_vs, lll, accL,
+                       reinterpret_cast<T*>(H), h_vs, high, accH);
+    CWDM_LAUNCHED();
+    return CWDM_OK;
+  });
+}
+
 }  // namespace cwdm
 
 using namespace cwdm;

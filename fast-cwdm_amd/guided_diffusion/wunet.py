@@ -12,9 +12,11 @@ names point at one Parameter) and the plan runs the block twice.
 Native path: the same plan as UNetModel (``cwdm_unet_*`` with
 ``use_freq=1``); the DWT/IDWT resampling, emb add and the GroupNorm
 statistics of their outputs run in one channels-last kernel
-(``cwdm_haar_nd``), convs on the MFMA kernels.  Forward only: training a
-WavUNetModel is outside the hot path (run.sh trains UNetModel); a forward with
-gradients enabled raises NotImplementedError instead of silently detaching.
+(``cwdm_haar_nd``), convs on the MFMA kernels.  Training: the plan's backward
+(``cwdm_unet_backward``) runs the adjoints -- the DWT's adjoint is the IDWT
+and vice versa (orthonormal Haar), the reused decoder blocks' gradients sum
+into the owner's parameters -- so ``model(x, t)`` under autograd and
+TrainLoop work as for UNetModel.
 """
 import torch as th
 
@@ -62,9 +64,3 @@ class WavUNetModel(UNetModel):
                            attention_resolutions, dropout, channel_mult, conv_resample, num_classes, use_checkpoint,
                            num_heads, num_groups, resblock_updown, bottleneck_attention, additive_skips,
                            decoder_device_thresh, compute_dtype)
-
-    def forward(self, x, timesteps, y=None):
-        if th.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("the native WavUNetModel is forward-only (sampling); run it under "
-                                      "torch.no_grad() or train UNetModel")
-        return super().forward(x, timesteps, y)

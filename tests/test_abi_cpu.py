@@ -161,7 +161,7 @@ def test_wavunet_state_dict_matches_oracle(cfg):
         assert sd[alias + ".in_layers.2.weight"] is sd[owner + ".in_layers.2.weight"]
     if cfg["model_channels"] == 64:
         assert sum(p.numel() for p in m.parameters()) == 90079304
-    with pytest.raises(NotImplementedError):   # forward-only: no silent detach under autograd
+    with pytest.raises(RuntimeError, match="ROCm device"):   # no CPU fallback, with or without autograd
         m(torch.zeros(1, 32, 32, 32, 32), torch.zeros(1))
 
 
@@ -177,5 +177,7 @@ def test_wavunet_plan_refusals():
     with pytest.raises(AssertionError):
         plan.check_grid(16, 16, 6)    # every level downsamples: edges divisible by 2^levels
     plan.check_grid(16, 16, 4)
-    with pytest.raises(AssertionError):  # forward-only plan: no gradient workspace
-        plan.grad_workspace_bytes(1, 8, 8, 8)
+    assert plan.grad_workspace_bytes(1, 8, 8, 8) > 0   # the plan trains (DWT/IDWT adjoints in the backward)
+    # backward segments tile the parameters (head, each block incl. the pyramid convs, conv_in)
+    tot = sum(plan.segment_range(s)[1] for s in range(plan.num_segments))
+    assert tot == plan.grad_numel
