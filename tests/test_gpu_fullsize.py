@@ -86,7 +86,8 @@ def test_fullsize_half_step_close_to_fp32():
     # bf16 / fp16 are the throughput modes (SURVEY.md §7 iii: judged on a looser,
     # documented bound): relative L2 over the 16.8 M outputs, and the max-norm
     # (a few outliers among 16.8 M values after 81 M 16-bit parameters)
-    bounds = {"bf16": (4e-2, 0.25), "fp16": (1e-2, 0.05)}
+    # measured (r03): pred_xstart rel L2 bf16 2.25e-2 / fp16 2.81e-3, rel max 0.145 / 0.0216
+    bounds = {"bf16": (4e-2, 0.25), "fp16": (5e-3, 0.04)}
     for dt, (l2_max, max_max) in bounds.items():
         for k in (0, 1):
             a, b = outs[dt][k].double(), outs["fp32"][k].double()
@@ -148,8 +149,11 @@ def test_fullsize_respaced50_volume_bf16_vs_fp32(sampler):
     # hold 1e-3 over a trajectory -- each bf16 layer adds ~1e-3 relative error,
     # 1.5e-2 at the U-Net output, and 50 steps accumulate it; fp32 is the
     # parity mode): ddpm 0.29 / ddim 0.22 image rel L2 measured
+    # measured (r03) image rel L2: ddpm bf16 0.293 / fp16 0.164 / fp32_xq 2.5e-3;
+    # ddim bf16 0.222 / fp16 0.074 / fp32_xq 0.095
     assert res["bf16"][0] < 0.4, res
-    assert res["fp16"][0] < 0.4, res
+    assert res["fp16"][0] < 0.25, res
+    assert res["fp16"][0] < 0.8 * res["bf16"][0], res
     assert res["fp32_xq"][0] < 0.15, res
 
 
@@ -182,8 +186,9 @@ def test_fullsize_half_error_by_layer():
     o = {dt: float((outs[dt].double() - outs["fp32"].double()).norm() / outs["fp32"].double().norm())
          for dt in ("bf16", "fp16")}
     print(f"model output rel L2: bf16 {o['bf16']:.3e}, fp16 {o['fp16']:.3e}")
+    # measured (r03): bf16 1.49e-2, fp16 1.86e-3 (fp16's 3 more mantissa bits: 8x, layer by layer)
     assert o["bf16"] < 5e-2
-    assert o["fp16"] < 1e-2
+    assert o["fp16"] < 5e-3
 
 
 def test_fullsize_wavunet_forward_fp32_vs_oracle():
