@@ -25,6 +25,7 @@ CASES = {
     "L0_128_128_up": (128, 128, 0, 128, 1, True, 0, -1),
     "L0_192_64_cat": (128, 128, 64, 64, 0, True, 0, -1),
     "L0_64_8_out": (128, 64, 0, 8, 0, True, 0, -1),
+    "L0_64_8_out_nogn": (128, 64, 0, 8, 0, False, 0, -1),
     "L1_256_128_cat": (64, 128, 128, 128, 0, True, 0, -1),
     "L0_64_64_nogn": (128, 64, 0, 64, 0, False, 0, -1),
     "L0_192_64_cat_nogn": (128, 128, 64, 64, 0, False, 0, -1),

@@ -1,5 +1,5 @@
 """Per-launch timeline of one denoising step from a rocprofv3 kernel trace of
-bench.py (the last complete step: between the last two sampler launches).
+bench.py (a complete step: from one time-embedding launch to the next).
 usage: python tools/trace_step.py gpurun_out/TAG/trace [--agg] [--last]"""
 import csv
 import glob
@@ -22,12 +22,15 @@ def short(n):
 
 def main():
     rows = load(sys.argv[1])
-    samp = [i for i, r in enumerate(rows) if "sampler_kernel" in r["Kernel_Name"]]
+    # steps start at the time-embedding MLP (the first launch of every U-Net
+    # forward; the sampler epilogue may live in the output head)
+    marks = [i for i, r in enumerate(rows) if "time_embed_kernel" in r["Kernel_Name"]]
     # the last step of the timed (graph-replayed) loop: bench.py ends with one
     # eager profiling step whose setup copies would otherwise land in it
-    k = -2 if "--last" not in sys.argv else -1
-    a, b = samp[k - 1] + 1, samp[k] + 1
-    step = rows[a:b]
+    if "--last" in sys.argv:
+        step = rows[marks[-1]:]
+    else:
+        step = rows[marks[-3]:marks[-2]]
     tot = 0.0
     agg = defaultdict(lambda: [0, 0.0])
     for i, r in enumerate(step):
