@@ -92,7 +92,7 @@ template <>
 __device__ __forceinline__ u32x4 pack<bf16_t>(const float* f) {
   u32x4 q;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) q[i] = (unsigned)f2bf(f[2 * i]) | ((unsigned)f2bf(f[2 * i + 1]) << 16);
+  for (int i = 0; i < 4; ++i) q[i] = pack2<bf16_t>(f[2 * i], f[2 * i + 1]);  // one v_cvt_pk_bf16_f32 per pair
   return q;
 }
 template <>

@@ -9,9 +9,22 @@ namespace cwdm {
 
 constexpr float kC = 0.70710677f;  // fp32(1/sqrt(2)) -- pywt rec_lo/rec_hi
 
-__device__ __forceinline__ float mr(float a, float b) { return __fmul_rn(a, b); }
-__device__ __forceinline__ float ad(float a, float b) { return __fadd_rn(a, b); }
-__device__ __forceinline__ float sb(float a, float b) { return __fsub_rn(a, b); }
+// Plain operators under contract(off) (HIP's __fmul_rn / __fadd_rn are plain
+// operators defined in a header with contraction allowed): no caller -- also
+// one compiled with contraction on, e.g. the fused output head -- can fuse a
+// product into the following add
+__device__ __forceinline__ float mr(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float ad(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+__device__ __forceinline__ float sb(float a, float b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
 
 // Analysis of a 2x2x2 block v[a][b][e] (a: D parity, b: H, e: W) into the 8
 // bands in reference order LLL, LLH, LHL, LHH, HLL, HLH, HHL, HHH.

@@ -830,9 +830,16 @@ extern "C" double cwdm_unet_flops(const cwdm_unet* u, int64_t B, int64_t D, int6
   return f;
 }
 
-extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x, const float* t, float* out,
-                                 int64_t B, int64_t D, int64_t H, int64_t W, void* ws, int64_t ws_bytes,
-                                 cwdm_stream_t stream) {
+namespace cwdm {
+bool head_sampler_eligible(const cwdm_conv3d_desc* d, const cwdm_sampler_args* a);  // conv3d_head.hip
+int head_sampler_forward(const cwdm_conv3d_desc* d, const cwdm_sampler_args* a, hipStream_t s);
+}
+
+// samp: run the sampling step on the output (cwdm_unet_forward_step); fused
+// into the output head when it qualifies (*fused = 1), else after the forward.
+static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, const float* t, float* out,
+                             int64_t B, int64_t D, int64_t H, int64_t W, void* ws, int64_t ws_bytes,
+                             cwdm_stream_t stream, const cwdm_sampler_args* samp, int* fused) {
   CWDM_REQUIRE(u && packed && x && t && out && ws, CWDM_E_INVALID, "cwdm_unet_forward: null pointer");
   CWDM_REQUIRE(B > 0 && D > 0 && H > 0 && W > 0, CWDM_E_SHAPE, "cwdm_unet_forward: empty grid");
   const int64_t div = int64_t(1) << (u->cfg.num_levels - (u->cfg.use_freq ? 0 : 1));
@@ -965,7 +972,12 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
         d.b0 = d.b1 = nullptr; d.b_c0 = d.b_c1 = 0; d.b_w = nullptr;
         d.res = wb + L.skipbuf; d.res_mode = 0;
       }
-      if ((rc = cwdm_conv3d_forward(&d, stream))) return rc;
+      if (samp && cs.out < 0 && cwdm::head_sampler_eligible(&d, samp)) {
+        if ((rc = cwdm::head_sampler_forward(&d, samp, s))) return rc;
+        if (fused) *fused = 1;
+      } else if ((rc = cwdm_conv3d_forward(&d, stream))) {
+        return rc;
+      }
     }
     if (u->profiling) {
       cwdm::g_prof = nullptr;
@@ -974,6 +986,27 @@ extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x
     ++conv_i;
   }
   return CWDM_OK;
+}
+
+extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x, const float* t, float* out,
+                                 int64_t B, int64_t D, int64_t H, int64_t W, void* ws, int64_t ws_bytes,
+                                 cwdm_stream_t stream) {
+  return unet_forward_impl(u, packed, x, t, out, B, D, H, W, ws, ws_bytes, stream, nullptr, nullptr);
+}
+
+extern "C" int cwdm_unet_forward_step(cwdm_unet* u, const void* packed, const void* x, const float* t_model,
+                                      const cwdm_sampler_args* step, int64_t B, int64_t D, int64_t H, int64_t W,
+                                      void* ws, int64_t ws_bytes, int* fused, cwdm_stream_t stream) {
+  CWDM_REQUIRE(step && step->model_out, CWDM_E_INVALID, "cwdm_unet_forward_step: null step / model_out");
+  CWDM_REQUIRE(u && step->d == D && step->h == H && step->w == W && step->B == B &&
+                   (step->levels == 2 || u->cfg.out_channels == 8),
+               CWDM_E_SHAPE, "cwdm_unet_forward_step: the step's grid must be the forward's");
+  int did = 0;
+  int rc = unet_forward_impl(u, packed, x, t_model, const_cast<float*>(step->model_out), B, D, H, W, ws, ws_bytes,
+                             stream, step, &did);
+  if (fused) *fused = did;
+  if (rc || did) return rc;
+  return cwdm_sampler_step(step, stream);
 }
 
 extern "C" int cwdm_unet_trace_count(const cwdm_unet* u) { return u ? (int)u->trace.size() : -1; }

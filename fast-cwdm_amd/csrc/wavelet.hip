@@ -4,6 +4,7 @@
 // so results match the oracle's elementwise restatement bit for bit.
 #include "common.hpp"
 #include "haar8.hpp"
+#include "sampler.hpp"
 
 // Rounding must follow the reference stage by stage: no FMA contraction here.
 #pragma clang fp contract(off)
@@ -205,46 +206,21 @@ __global__ void __launch_bounds__(256) sampler_kernel(cwdm_sampler_args a, S3 mo
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) xv[q] = a.x_t[b * xt.b + q * xt.c + v * xt.v];
-  if (a.mean_type == 1) {
-    // EPSILON: x0 = sqrt(1/acp) * x_t - sqrt(1/acp - 1) * eps (gaussian_diffusion.py:392-397)
+  float nzv[8];
+  bool has_noise = false;
+  if (a.update != 1 && t != 0) {
+    if (a.noise) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) m[q] = sb(mr(cf[q * bs + 3], xv[q]), mr(cf[q * bs + 4], m[q]));
-  }
-  float pred[8];
-  if (a.clip_denoised) {
-    m[0] = mr(m[0], 3.0f);
-    float blk[8];
-    haar_inv8(m, blk);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) blk[q] = fminf(fmaxf(blk[q], 0.0f), 1.0f);
-    haar_fwd8(blk, pred);
-    pred[0] = __fdiv_rn(pred[0], 3.0f);
-  } else {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) pred[q] = m[q];
-  }
-  float r[8];
-  if (a.update == 1) {
-    // DDIM (ddim_sample, gaussian_diffusion.py:753-784): eps from x_t and the
-    // projected x0 (_predict_eps_from_xstart, :407-415), then
-    // x0 * sqrt(acp_prev) + sqrt(1 - acp_prev - sigma^2) * eps, returned
-    // without noise like the reference (:784); cf[5], cf[6] hold the two roots
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float* c = cf + q * bs;
-      const float eps = __fdiv_rn(sb(mr(c[3], xv[q]), pred[q]), c[4]);
-      r[q] = ad(mr(pred[q], c[5]), mr(c[6], eps));
-    }
-  } else {
-    const bool noisy = (t != 0) && a.noise;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float* c = cf + q * bs;
-      float mean = ad(mr(c[0], pred[q]), mr(c[1], xv[q]));
-      r[q] = mean;
-      if (noisy) r[q] = ad(mean, mr(c[2], a.noise[b * nz.b + q * nz.c + v * nz.v]));
+      for (int q = 0; q < 8; ++q) nzv[q] = a.noise[b * nz.b + q * nz.c + v * nz.v];
+      has_noise = true;
+    } else if (a.noise_philox) {
+      philox_normal4(a.noise_seed, v, b, t, 0, nzv);
+      philox_normal4(a.noise_seed, v, b, t, 1, nzv + 4);
+      has_noise = true;
     }
   }
+  float pred[8], r[8];
+  sampler_voxel8(a, cf, bs, t, m, xv, has_noise, nzv, r, pred);
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     a.x_prev[b * xp.b + q * xp.c + v * xp.v] = r[q];

@@ -13,6 +13,7 @@
 #include <type_traits>
 
 #include "haar8.hpp"
+#include "sampler.hpp"
 
 namespace cwdm {
 namespace {
@@ -222,15 +223,17 @@ __global__ void __launch_bounds__(256) sampler2_kernel(cwdm_sampler_args a, S3w 
 #pragma unroll
     for (int q = 0; q < 64; ++q) pred[q] = m[q];
   }
-  const bool noisy = a.update != 1 && t != 0 && a.noise;
+  const bool noisy = a.update != 1 && t != 0 && (a.noise || a.noise_philox);
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
     const float4 u = ld4(a.x_t, xt, b, 4 * g, v, vec & 2);
     const float xq[4] = {u.x, u.y, u.z, u.w};
     float nq[4] = {0.f, 0.f, 0.f, 0.f};
-    if (noisy) {
+    if (noisy && a.noise) {
       const float4 n4 = ld4(a.noise, nz, b, 4 * g, v, vec & 8);
       nq[0] = n4.x; nq[1] = n4.y; nq[2] = n4.z; nq[3] = n4.w;
+    } else if (noisy) {
+      philox_normal4(a.noise_seed, v, b, t, g, nq);
     }
     float r[4];
 #pragma unroll

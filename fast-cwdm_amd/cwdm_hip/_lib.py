@@ -38,6 +38,9 @@ class SamplerArgs(ctypes.Structure):
         ("update", ctypes.c_int),
         ("per_band", ctypes.c_int),
         ("levels", ctypes.c_int),
+        ("noise_philox", ctypes.c_int),
+        ("reserved0", ctypes.c_int),
+        ("noise_seed", ctypes.c_uint64),
     ]
 
 
@@ -171,6 +174,8 @@ _PROTOS = {
     "cwdm_unet_pack": (ctypes.c_int, [vp, ctypes.POINTER(vp), vp, vp]),
     "cwdm_unet_workspace_bytes": (i64, [vp, i64, i64, i64, i64]),
     "cwdm_unet_forward": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, i64, vp]),
+    "cwdm_unet_forward_step": (ctypes.c_int, [vp, vp, vp, vp, ctypes.POINTER(SamplerArgs), i64, i64, i64, i64,
+                                              vp, i64, ctypes.POINTER(ctypes.c_int), vp]),
     "cwdm_unet_trace_count": (ctypes.c_int, [vp]),
     "cwdm_unet_trace_info": (ctypes.c_int, [vp, ctypes.c_int, i64, i64, i64, i64, ctypes.POINTER(i64),
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),

@@ -143,12 +143,12 @@ def ndhwc_strides(B, C, V, c_total=None):
     return (V * ct, 1, ct)
 
 
-def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t, T, B, d, h, w,
+def sampler_args(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t, T, B, d, h, w,
                  clip_denoised=True, pred_xstart=None, px_s=(0, 0, 0), mirror=None, mr_s=(0, 0, 0),
-                 mean_type=0, update=0, per_band=False, levels=1):
-    """Fused process_xstart + posterior mean + noise (cwdm_sampler_step);
-    update=1: the DDIM step instead of the posterior mean + noise; levels=2:
-    the 64-channel two-level block representation (config 5, wavelet2_*)."""
+                 mean_type=0, update=0, per_band=False, levels=1, noise_seed=None):
+    """The cwdm_sampler_args of one step.  noise_seed (with noise None): draw
+    the noise in the kernel (Philox, keyed by the seed, counter = voxel,
+    batch, device timestep, channel group)."""
     _need_cuda(model_out, x_t, x_prev, noise, coef, t, pred_xstart, mirror)
     a = _lib.SamplerArgs()
     a.model_out, a.mo_s = model_out.data_ptr(), _lib.I64x3(*mo_s)
@@ -168,6 +168,21 @@ def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t,
     a.update = int(update)
     a.per_band = 1 if per_band else 0
     a.levels = int(levels)
+    a.noise_philox = 1 if (noise is None and noise_seed is not None) else 0
+    a.noise_seed = int(noise_seed or 0) & ((1 << 64) - 1)
+    return a
+
+
+def sampler_step(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t, T, B, d, h, w,
+                 clip_denoised=True, pred_xstart=None, px_s=(0, 0, 0), mirror=None, mr_s=(0, 0, 0),
+                 mean_type=0, update=0, per_band=False, levels=1, noise_seed=None):
+    """Fused process_xstart + posterior mean + noise (cwdm_sampler_step);
+    update=1: the DDIM step instead of the posterior mean + noise; levels=2:
+    the 64-channel two-level block representation (config 5, wavelet2_*);
+    noise_seed: in-kernel Philox noise instead of a noise tensor."""
+    a = sampler_args(model_out, mo_s, x_t, xt_s, x_prev, xp_s, noise, nz_s, coef, t, T, B, d, h, w,
+                     clip_denoised, pred_xstart, px_s, mirror, mr_s, mean_type, update, per_band, levels,
+                     noise_seed)
     check(lib().cwdm_sampler_step(ctypes.byref(a), _stream()), "sampler_step")
 
 

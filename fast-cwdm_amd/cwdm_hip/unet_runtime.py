@@ -116,6 +116,22 @@ class UNetPlan:
               "UNetModel.forward")
         return out_ndhwc
 
+    def forward_step(self, packed, x_ndhwc, t_f32, step, B, D, H, W, ws=None):
+        """cwdm_unet_forward_step: the forward plus the sampling step ``step``
+        (an ops.sampler_args whose model_out is the NDHWC fp32 output buffer);
+        returns True when the step ran fused into the output head."""
+        _need_cuda(packed, x_ndhwc, t_f32)
+        self.check_grid(D, H, W)
+        if ws is None:
+            ws = self.workspace(B, D, H, W, x_ndhwc.device)
+        fused = ctypes.c_int(0)
+        check(lib().cwdm_unet_forward_step(self._h, ctypes.c_void_p(packed.data_ptr()),
+                                           ctypes.c_void_p(x_ndhwc.data_ptr()), ctypes.c_void_p(t_f32.data_ptr()),
+                                           ctypes.byref(step), B, D, H, W, ctypes.c_void_p(ws.data_ptr()),
+                                           ws.numel(), ctypes.byref(fused), _stream()),
+              "UNetModel.forward_step")
+        return bool(fused.value)
+
     def flops(self, B, D, H, W):
         return float(lib().cwdm_unet_flops(self._h, B, D, H, W))
 

@@ -12,8 +12,11 @@ Host-side float64 tables are the reference's (:143-205).  On device:
   ``th.cat([x, cond])`` and layout moves disappear;
 * DWTs of the training path write the wavelet channels straight into the
   model-input buffer.
-Noise is drawn with ``th.randn_like`` exactly where the reference draws it, so
-a seeded run consumes the same RNG stream.
+Noise: p_sample / the generic loop draw ``th.randn_like`` where the reference
+draws it (:565).  The native loop draws it inside the sampler kernel instead
+(``native_noise = "philox"``: Philox4x32-10 keyed by one 64-bit seed taken from
+torch's CPU generator when the loop starts, so ``th.manual_seed`` still fixes
+a run); ``native_noise = "torch"`` or a ``noise_fn`` restores a noise tensor.
 
 Deliberate differences (DESIGN.md "reference quirks"): ``p_sample_loop``
 runs ``num_timesteps`` steps (the reference hard-codes 1000, which only works
@@ -164,6 +167,9 @@ class GaussianDiffusion:
 
     # capture the native sampling step in a HIP graph (see _native_loop)
     use_hip_graph = True
+    # the native loop's noise: "philox" (drawn in the sampler kernel / fused
+    # output head) or "torch" (a th.randn_like tensor per step)
+    native_noise = "philox"
 
     # ---- tables -------------------------------------------------------------
     def _fixed_variance(self):
@@ -397,11 +403,15 @@ class GaussianDiffusion:
                      need_pred=True, update=0, eta=0.0):
         """Channels-last resident loop for the native UNetModel.
 
-        graph: capture one denoising step (U-Net launch list + noise draw +
-        fused sampler epilogue) in a HIP graph and replay it for every later
-        step (default: ``self.use_hip_graph``; only with the default noise
-        source, whose draw torch's graph-safe generator replays).  The timestep
-        is the only per-step input: two 8-byte device fills before each replay.
+        graph: capture one denoising step (U-Net launch list + fused sampler
+        epilogue) in a HIP graph and replay it for every later step (default:
+        ``self.use_hip_graph``; not with a ``noise_fn``).  The timestep is the
+        only per-step input: two 8-byte device fills before each replay.  Each
+        step is cwdm_unet_forward_step: with a 16-bit single-level model the
+        sampler epilogue runs inside the output head's conv kernel and the
+        noise is generated there (Philox, counter includes the device
+        timestep, so replays draw fresh noise); otherwise the forward and
+        cwdm_sampler_step run back to back.
         fresh_outputs=False lets the yielded tensors be the graph's static
         buffers (overwritten by the next step; p_sample_loop only keeps the last).
         need_pred=False skips the pred_xstart store (p_sample_loop never reads
@@ -437,18 +447,22 @@ class GaussianDiffusion:
         t_model = th.empty((B,), dtype=th.float32, device=dev)
         ddim = update == 1
 
+        philox = noise_fn is None and self.native_noise == "philox"
+        seed = int(th.randint(0, 2 ** 62, (1,)).item()) if (philox and not ddim) else None
+
         def step(src, dst, pred, noise):
-            unet.forward_ndhwc(xin, t_model, out_nd)
-            if ddim:
+            if ddim or philox:
                 noise = None
             elif noise is None:
                 noise = (noise_fn or th.randn_like)(src)
             else:
                 noise.normal_()
-            ops.sampler_step(out_nd, (V * C, 1, C), src, s, dst, s, noise, s if noise is not None else (0, 0, 0),
-                             coef, t, self.num_timesteps, B, d, h, w, clip_denoised=clip_denoised,
-                             pred_xstart=pred, px_s=s, mirror=xin, mr_s=(V * cin, 1, cin), mean_type=mean_type,
-                             update=update, per_band=self.per_band, levels=self.wavelet_levels)
+            a = ops.sampler_args(out_nd, (V * C, 1, C), src, s, dst, s, noise, s if noise is not None else (0, 0, 0),
+                                 coef, t, self.num_timesteps, B, d, h, w, clip_denoised=clip_denoised,
+                                 pred_xstart=pred, px_s=s, mirror=xin, mr_s=(V * cin, 1, cin), mean_type=mean_type,
+                                 update=update, per_band=self.per_band, levels=self.wavelet_levels,
+                                 noise_seed=seed)
+            unet.forward_step_ndhwc(xin, t_model, a)
 
         def fresh(x):
             return x.clone() if (fresh_outputs and x is not None) else x
@@ -469,7 +483,7 @@ class GaussianDiffusion:
             # and reads the caller's tensor, which no graph ever writes
             bufs = [th.empty_like(img), th.empty_like(img)]
             pred = th.empty_like(img) if need_pred else None
-            noise = None if ddim else th.empty_like(img)
+            noise = None if (ddim or philox) else th.empty_like(img)
             i0 = indices[0]
             t.fill_(i0)
             t_model.fill_(self._model_timestep(i0))

@@ -279,6 +279,14 @@ class UNetModel(nn.Module):
         assert C == self.in_channels
         return self.plan.forward(self.packed_weights(), x_ndhwc, t_f32, out_ndhwc, B, D, H, W)
 
+    def forward_step_ndhwc(self, x_ndhwc, t_f32, step):
+        """forward_ndhwc followed by the sampling step ``step`` (ops.sampler_args,
+        model_out = the (B, D, H, W, out) fp32 buffer), fused into the output
+        head when it qualifies; returns whether it was fused."""
+        B, D, H, W, C = x_ndhwc.shape
+        assert C == self.in_channels
+        return self.plan.forward_step(self.packed_weights(), x_ndhwc, t_f32, step, B, D, H, W)
+
     def forward(self, x, timesteps, y=None):
         assert (y is not None) == (self.num_classes is not None), \
             "must specify y if and only if the model is class-conditional"

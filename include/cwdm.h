@@ -184,8 +184,16 @@ typedef struct {
   int per_band;         /* coef is [T][C][8]: one schedule per subband channel (FATS, guided_diffusion/fats.py) */
   int levels;           /* 0 / 1: 8 single-level subbands; 2: the 64-channel 2-level block representation of
                            config 5 (cwdm_wavelet2_*), process_xstart = 2-level inverse -> clamp -> forward */
+  int noise_philox;     /* noise == NULL and nonzero: draw the N(0,1) noise in the kernel -- Philox4x32-10, key
+                           noise_seed, counter (voxel lo, voxel hi, t[b], b << 8 | channel / 4), Box-Muller on
+                           24-bit uniforms (csrc/sampler.hpp).  The counter holds the device timestep, so a
+                           replayed graph draws fresh noise each step with no host-side state. */
+  int reserved0;
+  uint64_t noise_seed;
 } cwdm_sampler_args;
 int cwdm_sampler_step(const cwdm_sampler_args* args, cwdm_stream_t stream);
+/* Reference: p_sample (gaussian_diffusion.py:529-575) draws th.randn_like(x)
+ * at :565; noise_philox replaces that draw, the rest is unchanged. */
 
 /* Config 5 (BASELINE.json: 2-level DWT + FATS, 224^3; no reference code --
  * the specification is oracle/wavelet2.py).  Per modality 64 channels on the
@@ -461,6 +469,18 @@ int64_t cwdm_unet_workspace_bytes(const cwdm_unet* plan, int64_t B, int64_t D, i
 int cwdm_unet_forward(cwdm_unet* plan, const void* packed, const void* x, const float* t,
                       float* out, int64_t B, int64_t D, int64_t H, int64_t W,
                       void* workspace, int64_t ws_bytes, cwdm_stream_t stream);
+/* One denoising step: the forward, then cwdm_sampler_step(step) on its output.
+ * step->model_out / mo_s name the forward's output (NDHWC fp32 as for
+ * cwdm_unet_forward, mo_s = {V*C, 1, C}).  When the output head qualifies
+ * (16-bit plan, out_channels 8, single-level sampler on the forward's grid,
+ * mirror in the plan dtype or fp32) the head conv runs the sampler epilogue
+ * on its accumulators (*fused = 1): model_out is not written and the bits of
+ * x_prev / pred_xstart / mirror are those of the unfused step.  step->mirror may
+ * alias x (the next step's input).  Replaces the model call + p_sample tail of
+ * p_sample_loop_progressive (gaussian_diffusion.py:668-719, :529-575). */
+int cwdm_unet_forward_step(cwdm_unet* plan, const void* packed, const void* x, const float* t_model,
+                           const cwdm_sampler_args* step, int64_t B, int64_t D, int64_t H, int64_t W,
+                           void* workspace, int64_t ws_bytes, int* fused, cwdm_stream_t stream);
 /* Block outputs kept in the workspace after a forward (one per entry of the
  * topology), for layer-level parity tests. */
 int cwdm_unet_trace_count(const cwdm_unet* plan);

@@ -76,15 +76,11 @@ static void exercise(const cwdm_unet_config& c, int64_t n) {
       CHECK(off < ws && ch > 0 && lv >= 0 && lv <= c.num_levels);
     }
     const int64_t gws = cwdm_unet_grad_workspace_bytes(u, b, n, n, 2 * n);
-    if (c.use_freq) {
-      CHECK(gws < 0);
-    } else {
-      CHECK(gws > 0);
-      CHECK(cwdm_unet_backward_flops(u, b, n, n, 2 * n) > 0);
-    }
+    CHECK(gws > 0);   // WavUNetModel trains too (Haar adjoint backward)
+    CHECK(cwdm_unet_backward_flops(u, b, n, n, 2 * n) > 0);
   }
   CHECK(cwdm_unet_workspace_bytes(u, 0, n, n, n) < 0);
-  if (!c.use_freq) {
+  {
     const int ns = cwdm_unet_backward_segments(u);
     CHECK(ns > 2);
     int64_t total = 0;

@@ -247,12 +247,14 @@ def test_graph_loop_leaves_caller_noise_unchanged():
     assert out.data_ptr() != x_dev.data_ptr() and torch.isfinite(out).all()
 
 
-@pytest.mark.parametrize("respacing,dtype", [("", "fp32"), ("ddim10", "bf16"), ("ddim10", "fp16")])
-def test_hip_graph_loop_equals_eager_loop(respacing, dtype):
+@pytest.mark.parametrize("respacing,dtype,noise_src", [("", "fp32", "philox"), ("ddim10", "bf16", "philox"),
+                                                        ("ddim10", "fp16", "torch")])
+def test_hip_graph_loop_equals_eager_loop(respacing, dtype, noise_src):
     """The graph-captured sampling step (one capture, replayed per timestep,
-    noise from torch's graph-safe generator) reproduces the eager loop with
-    the same seed, for the full and a respaced schedule (a 50-step direct
-    schedule: beta_T = 0.4, every table column finite)."""
+    noise drawn in the sampler kernel by Philox with the device timestep in
+    its counter, or from torch's graph-safe generator) reproduces the eager
+    loop with the same seed, for the full and a respaced schedule (a 50-step
+    direct schedule: beta_T = 0.4, every table column finite)."""
     from guided_diffusion import script_util
     args = script_util.run_sh_model_args(num_channels=32, channel_mult="1,2", num_res_blocks=1, num_groups=8,
                                          diffusion_steps=50, sample_schedule="direct",
@@ -264,6 +266,8 @@ def test_hip_graph_loop_equals_eager_loop(respacing, dtype):
     g = torch.Generator().manual_seed(5)
     cond = torch.rand(1, 24, 16, 16, 16, generator=g).to(DEV)
     x_T = torch.randn(1, 8, 16, 16, 16, generator=g).to(DEV)
+
+    diffusion.native_noise = noise_src
 
     def run(graph):
         diffusion.use_hip_graph = graph
