@@ -139,4 +139,16 @@ inline FastDiv make_fastdiv(unsigned d) {
 }
 __device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.s; }
 
+
+// one conv weight pack of a batched launch (conv3d.hip pack_batch_run; the
+// U-Net plan collects its packs through g_pack_batch).  No implicit padding:
+// tables are compared bytewise to skip re-uploads.
+struct PackJob {
+  const float* w;
+  void* out;
+  long long total;
+  int cout, cin, ntaps, NT, transpose, cin_real, s2_ci0, pad;
+  long long blk0;
+};
+static_assert(sizeof(PackJob) == 64, "PackJob layout");
 }  // namespace cwdm

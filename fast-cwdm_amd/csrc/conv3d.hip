@@ -3,6 +3,8 @@
 #include <algorithm>
 
 #include <cstdlib>
+#include <cstring>
+#include <vector>
 
 #include "conv3d_kernels.hpp"
 
@@ -42,15 +44,12 @@ __device__ __forceinline__ float s2_weight(const float* w, int ci0, int co, int 
   return w[((long long)co * ci0 + ci) * 27 + (kz * 3 + ky) * 3 + kx];
 }
 
+// element i of a packed weight image (output-indexed)
 template <typename T>
-__global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, int cout, int cin, int ntaps, int NT,
-                                                   int nct, T* __restrict__ out, int transpose, int cin_real,
-                                                   int s2_ci0) {
+__device__ __forceinline__ void pack_elem(const float* __restrict__ w, int cout, int cin, int ntaps, int NT,
+                                          T* __restrict__ out, int transpose, int cin_real, int s2_ci0, long long i) {
   constexpr int CK = ConvTr<T>::CK, EPQ = ConvTr<T>::EPQ;
   const int nch = cin / CK;
-  const long long total = (long long)nct * nch * ntaps * NT * CK;
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
   const int e = i % EPQ;
   long long r = i / EPQ;
   const int qp = r % 2;
@@ -72,6 +71,38 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, 
     else v = w[((long long)co * cin + ci) * ntaps + tap];
   }
   out[i] = Elem<T>::from_f(v);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, int cout, int cin, int ntaps, int NT,
+                                                   int nct, T* __restrict__ out, int transpose, int cin_real,
+                                                   int s2_ci0) {
+  constexpr int CK = ConvTr<T>::CK;
+  const long long total = (long long)nct * (cin / CK) * ntaps * NT * CK;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < total) pack_elem<T>(w, cout, cin, ntaps, NT, out, transpose, cin_real, s2_ci0, i);
+}
+
+// every conv of a U-Net pack in one launch: block -> job by a binary search
+// over the jobs' first blocks (uniform per block), 1024 elements per block
+template <typename T>
+__global__ void __launch_bounds__(256) pack_batch_kernel(const PackJob* __restrict__ jobs, int njobs) {
+  const long long bid = blockIdx.x;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].blk0 <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const PackJob j = jobs[lo];
+  const long long base = (bid - j.blk0) * 1024;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // 4 independent gathers in flight per thread
+    const long long i = base + k * 256 + threadIdx.x;
+    if (i < j.total)
+      pack_elem<T>(j.w, j.cout, j.cin, j.ntaps, j.NT, reinterpret_cast<T*>(j.out), j.transpose, j.cin_real,
+                   j.s2_ci0, i);
+  }
 }
 
 template <typename T, int NF>
@@ -113,6 +144,9 @@ extern "C" int64_t cwdm_conv3d_packed_bytes(int cout, int cin, int ksize, int dt
 
 static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, void* packed, int transpose,
                      cwdm_stream_t stream, int s2_ci0 = 0);
+namespace cwdm {
+extern thread_local std::vector<PackJob>* g_pack_batch;
+}
 
 extern "C" int cwdm_conv3d_pack(const float* w, int cout, int cin, int ksize, int dtype, void* packed,
                                 cwdm_stream_t stream) {
@@ -148,6 +182,10 @@ static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, vo
   const int nct = (int)ceil_div(cout, NT);
   const int ntaps = ksize * ksize * ksize;
   const long long total = (long long)nct * (cin / ck) * ntaps * NT * ck;
+  if (g_pack_batch) {  // the U-Net plan collects its packs and launches them together (pack_batch_run)
+    g_pack_batch->push_back(PackJob{w, packed, total, cout, cin, ntaps, NT, transpose, cin_real, s2_ci0, 0, 0});
+    return CWDM_OK;
+  }
   dim3 grid((unsigned)ceil_div(total, 256));
   return dispatch_dtype(dtype, [&](auto tag) -> int {
     using T = decltype(tag);
@@ -157,6 +195,34 @@ static int pack_impl(const float* w, int cout, int cin, int ksize, int dtype, vo
     return CWDM_OK;
   });
 }
+
+namespace cwdm {
+thread_local std::vector<PackJob>* g_pack_batch = nullptr;
+
+// one launch for the collected packs; the job table goes to `table` (device,
+// >= jobs.size() entries), uploaded only when it differs from `cache`
+int pack_batch_run(std::vector<PackJob>& jobs, int dtype, PackJob* table, std::vector<PackJob>& cache,
+                   hipStream_t s) {
+  if (jobs.empty()) return CWDM_OK;
+  long long blk = 0;
+  for (auto& j : jobs) {
+    j.blk0 = blk;
+    blk += ceil_div(j.total, 1024);
+  }
+  CWDM_REQUIRE(blk < (1LL << 31), CWDM_E_UNSUPPORTED, "pack batch: too many blocks");
+  if (cache.size() != jobs.size() || std::memcmp(cache.data(), jobs.data(), jobs.size() * sizeof(PackJob))) {
+    CWDM_HIP(hipMemcpyAsync(table, jobs.data(), jobs.size() * sizeof(PackJob), hipMemcpyHostToDevice, s));
+    CWDM_HIP(hipStreamSynchronize(s));  // (pageable source; only when the layout changed)
+    cache = jobs;
+  }
+  return dispatch_dtype(dtype, [&](auto tag) -> int {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(pack_batch_kernel<T>, dim3((unsigned)blk), dim3(256), 0, s, table, (int)jobs.size());
+    CWDM_LAUNCHED();
+    return CWDM_OK;
+  });
+}
+}  // namespace cwdm
 
 namespace {
 struct Plan1 { Brick br; int nf, nct, S; long long nblk; int64_t ws; };

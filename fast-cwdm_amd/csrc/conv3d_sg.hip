@@ -63,7 +63,8 @@ struct SGCfg {
 struct SGParams {
   V4Params v;   // shape / sources / weights / epilogue as for the wide kernel (ct counts 64-row tiles)
   int ntile16;  // output channel tiles of 16
-  int parts;    // statistics bricks per batch
+  int parts;    // statistics bricks per batch (tx * ty * tz; the last brick of an axis may be partial)
+  int tx, ty;   // bricks along x and y
   // K split (the 8^3 level: 32 tiles): slice ks runs chunks [ks kper, +kper); it
   // stores its fp32 accumulators at part + (tile S + ks) 4096, and the slice
   // that arrives last at the tile's counter sums all S in slice order (the
@@ -112,7 +113,7 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   const int ks = (blockIdx.x / q.ntile16) % q.ksplit;
   const int st = blockIdx.x / (q.ntile16 * q.ksplit);
   const int b = st / q.parts, brick = st - b * q.parts;
-  const int tx = p.W / BX, ty = p.H / BY;
+  const int tx = q.tx, ty = q.ty;
   const int x0 = (brick % tx) * BX, y0 = ((brick / tx) % ty) * BY, z0 = (brick / (tx * ty)) * 4;
   const int SH = MODE == 1 ? p.H >> 1 : p.H, SW = MODE == 1 ? p.W >> 1 : p.W;
   const int nch = p.nch / 2;  // 32-channel chunks
@@ -284,10 +285,15 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
 
   // epilogue: lane (l16, kq) of operand m holds channels t16 16 + 4 kq + i of
   // voxel (x0 + xl, y0 + m LPO + yl, z0 + wv)
+  // (a partial brick at the grid's edge: voxels outside D x H x W computed
+  // zero-padded and dropped here -- no store, no residual load, no statistics)
   const int ox = x0 + xl, oz = z0 + wv;
   const long long HW = (long long)p.H * p.W;
   float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
   const int co = t16 * 16 + 4 * kq;
+  bool inb[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) inb[m] = ox < p.W && (y0 + m * C::LPO + yl) < p.H && oz < p.D;
   uint2 rq[4];
   if (p.rmode >= 0) {
 #pragma unroll
@@ -296,7 +302,8 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
       long long rvox = ((long long)b * p.D + oz) * HW + (long long)oy * p.W + ox;
       if (p.rmode == 1)
         rvox = (((long long)b * (p.D >> 1) + (oz >> 1)) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1);
-      rq[m] = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(p.res) + rvox * p.cout + co);
+      rq[m] = uint2{0u, 0u};
+      if (inb[m]) rq[m] = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(p.res) + rvox * p.cout + co);
     }
   }
 #pragma unroll
@@ -310,15 +317,17 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
       v[0] += lo2f<T>(rq[m].x); v[1] += hi2f<T>(rq[m].x);
       v[2] += lo2f<T>(rq[m].y); v[3] += hi2f<T>(rq[m].y);
     }
+    if (inb[m]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ssum[i] += v[i];
-      ssq[i] += v[i] * v[i];
+      for (int i = 0; i < 4; ++i) {
+        ssum[i] += v[i];
+        ssq[i] += v[i] * v[i];
+      }
+      uint2 sq;
+      sq.x = pack2<T>(v[0], v[1]);
+      sq.y = pack2<T>(v[2], v[3]);
+      *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.out) + vox * p.cout + co) = sq;
     }
-    uint2 sq;
-    sq.x = pack2<T>(v[0], v[1]);
-    sq.y = pack2<T>(v[2], v[3]);
-    *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.out) + vox * p.cout + co) = sq;
   }
   if (p.stats) {
     // rows of 16 lanes hold 4 channels for 16 voxels: DPP row sums, then the 4
@@ -371,7 +380,16 @@ namespace {
 bool sg_shape_ok(const cwdm_conv3d_desc* d) {
   if (g_conv_path.load(std::memory_order_relaxed) == 1) return false;
   if (!dtype_half(d->dtype) || d->out_dtype != d->dtype || d->accumulate || d->out1 || d->cout % 64) return false;
-  return (d->W == 16 && d->H % 4 == 0 && d->D % 4 == 0) || (d->W == 8 && d->H % 8 == 0 && d->D % 4 == 0);
+  // W < 32 (the wide kernels take W >= 32): 16 x 4 x 4 bricks for W >= 16, 8 x 8 x 4
+  // below (pick_brick's statistics bricks), the last brick of an axis partial
+  return d->W >= 1 && d->W < 32 && d->H >= 1 && d->D >= 1;
+}
+
+// statistics bricks of a small grid: (bx, tx, ty, tz), parts = tx ty tz (== cwdm_conv3d_parts)
+struct SgGeom { int bx, tx, ty, tz; int64_t parts() const { return (int64_t)tx * ty * tz; } };
+SgGeom sg_geom(const cwdm_conv3d_desc* d) {
+  const int bx = d->W >= 16 ? 16 : 8, by = 64 / bx;
+  return SgGeom{bx, (int)ceil_div(d->W, bx), (int)ceil_div(d->H, by), (int)ceil_div(d->D, 4)};
 }
 }  // namespace
 
@@ -402,7 +420,7 @@ bool sg_skip_eligible(const cwdm_conv3d_desc* d) {
 // 32-channel chunk per slice (the 16^3 level has 256 tiles: no split)
 namespace {
 int sg_split_for(const cwdm_conv3d_desc* d, int cin) {
-  const int64_t parts = d->W == 16 ? (d->D / 4) * (d->H / 4) : (d->D / 4) * (d->H / 8);
+  const int64_t parts = sg_geom(d).parts();
   const int64_t tiles = d->B * parts * (d->cout / 16);
   const int nch = cin / 32;
   // work-item target (env CWDM_SG_TARGET, A/B knob)
@@ -416,6 +434,11 @@ int sg_split_for(const cwdm_conv3d_desc* d, int cin) {
 }  // namespace
 
 int sg_ksplit(const cwdm_conv3d_desc* d) { return sg_eligible(d) ? sg_split_for(d, d->a_c0 + d->a_c1) : 1; }
+// voxels per batch of one K-split slice: the small-grid kernel stores whole
+// (possibly partial) bricks of 256 voxels, the wide kernel the grid itself
+int64_t ksplit_slice_voxels(const cwdm_conv3d_desc* d) {
+  return sg_shape_ok(d) ? sg_geom(d).parts() * 256 : d->D * d->H * d->W;
+}
 int sg_skip_ksplit(const cwdm_conv3d_desc* d) { return sg_skip_eligible(d) ? sg_split_for(d, d->b_c0 + d->b_c1) : 1; }
 
 // bytes of the K-split counter block a lone launch keeps behind its slices (0 without a split)
@@ -442,9 +465,10 @@ int sg_counters(SGParams& q, void* own, hipStream_t s) {
 template <typename T>
 void sg_go_t(const SGParams& q, const cwdm_conv3d_desc* d, int taps, hipStream_t s) {
   const dim3 grid((unsigned)(d->B * q.parts * q.ntile16 * q.ksplit));
-  if (d->W == 8 && taps == 1) {
+  const bool w8 = sg_geom(d).bx == 8;
+  if (w8 && taps == 1) {
     hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 0, 1>), grid, dim3(256), 0, s, q);
-  } else if (d->W == 8) {
+  } else if (w8) {
     if (q.v.amode == 1) hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 1, 27>), grid, dim3(256), 0, s, q);
     else hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 0, 27>), grid, dim3(256), 0, s, q);
   } else if (taps == 1) {
@@ -472,14 +496,16 @@ int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, void* partial, hipSt
   SGParams q{};
   q.v = v;
   q.ntile16 = d->cout / 16;
-  q.parts = (int)(d->W == 16 ? (d->D / 4) * (d->H / 4) : (d->D / 4) * (d->H / 8));
+  const SgGeom gm = sg_geom(d);
+  q.parts = (int)gm.parts();
+  q.tx = gm.tx; q.ty = gm.ty;
   q.ksplit = sg_ksplit(d);
   q.kper = ((d->a_c0 + d->a_c1) / 32 + q.ksplit - 1) / q.ksplit;
   q.part = reinterpret_cast<float*>(partial);
   CWDM_REQUIRE(q.ksplit == 1 || partial, CWDM_E_INVALID, "conv3d (small grid): K-split scratch missing");
   int rc;
   if ((rc = sg_counters(q, q.ksplit > 1 ? reinterpret_cast<unsigned char*>(partial) +
-                                              (int64_t)q.ksplit * d->B * d->D * d->H * d->W * d->cout * 4
+                                              (int64_t)q.ksplit * d->B * ksplit_slice_voxels(d) * d->cout * 4
                                         : nullptr, s)))
     return rc;
   return sg_go(q, d, 27, 2.0 * d->B * d->D * d->H * d->W * (double)d->cout * 27.0 * (d->a_c0 + d->a_c1), s);
@@ -502,14 +528,16 @@ int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, void* partial, hipStrea
   p.bias = nullptr; p.res = nullptr; p.rmode = -1;
   p.out = out; p.stats = nullptr;
   q.ntile16 = d->cout / 16;
-  q.parts = (int)(d->W == 16 ? (d->D / 4) * (d->H / 4) : (d->D / 4) * (d->H / 8));
+  const SgGeom gm = sg_geom(d);
+  q.parts = (int)gm.parts();
+  q.tx = gm.tx; q.ty = gm.ty;
   q.ksplit = sg_skip_ksplit(d);
   q.kper = ((d->b_c0 + d->b_c1) / 32 + q.ksplit - 1) / q.ksplit;
   q.part = reinterpret_cast<float*>(partial);
   CWDM_REQUIRE(q.ksplit == 1 || partial, CWDM_E_INVALID, "conv3d (small grid): K-split scratch missing");
   int rc;
   if ((rc = sg_counters(q, q.ksplit > 1 ? reinterpret_cast<unsigned char*>(partial) +
-                                              (int64_t)q.ksplit * d->B * V * d->cout * 4
+                                              (int64_t)q.ksplit * d->B * ksplit_slice_voxels(d) * d->cout * 4
                                         : nullptr, s)))
     return rc;
   return sg_go(q, d, 1, 2.0 * d->B * V * (double)d->cout * (d->b_c0 + d->b_c1), s);

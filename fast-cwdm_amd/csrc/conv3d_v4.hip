@@ -115,6 +115,7 @@ std::atomic<unsigned long long*> g_stamps{nullptr};
 bool sg_eligible(const cwdm_conv3d_desc* d);
 bool sg_skip_eligible(const cwdm_conv3d_desc* d);
 int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, void* partial, hipStream_t s);
+int64_t ksplit_slice_voxels(const cwdm_conv3d_desc* d);
 int sg_ksplit(const cwdm_conv3d_desc* d);
 int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, void* partial, hipStream_t s);
 int sg_skip_ksplit(const cwdm_conv3d_desc* d);
@@ -151,6 +152,8 @@ int v4_ksplit(const cwdm_conv3d_desc* d) {
 bool v4_eligible(const cwdm_conv3d_desc* d) {
   const int path = g_conv_path.load(std::memory_order_relaxed);
   if (path == 1) return false;
+  // the 1x1 skip product is added through the residual slot: not both
+  if (d->b_w && d->res_mode >= 0) return false;
   if (sg_eligible(d)) return true;  // 16^3 / 8^3 levels: conv3d_sg.hip behind the same pre-passes
   if (!dtype_compute(d->dtype)) return false;
   // W >= 32: the statistics partials follow cwdm_conv3d_parts' 32-wide x tiles (pick_brick)
@@ -181,7 +184,7 @@ int64_t v4_workspace_bytes(const cwdm_conv3d_desc* d) {
     S = std::max(S, sg_skip_ksplit(&e));
   }
   // (+ the small-grid kernel's K-split arrival counters behind the slices)
-  if (S > 1) ws += align256(S * d->B * d->D * d->H * d->W * d->cout * 4) + sg_sync_bytes(S);
+  if (S > 1) ws += align256(S * d->B * ksplit_slice_voxels(d) * d->cout * 4) + sg_sync_bytes(S);
   return ws;
 }
 
@@ -324,6 +327,9 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   return CWDM_OK;
 }
 
+thread_local void* g_act_keep = nullptr;  // set by the U-Net plan's training forward (ActKeepScope)
+thread_local int g_act_kept = 0;
+
 int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   const int esz = dtype_size(d->dtype);
   unsigned char* ws = reinterpret_cast<unsigned char*>(d->workspace);
@@ -334,8 +340,15 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   int a0_cm = 0;
   int rc;
   if (d->a_gn) {
+    // the activated input: in the workspace, or (training) where the plan keeps
+    // it for the backward's DMA-staged wgrad
     void* act = ws;
-    ws += align256(d->B * SV * (c0 + c1) * esz);
+    if (g_act_keep) {
+      act = g_act_keep;
+      g_act_kept = 1;
+    } else {
+      ws += align256(d->B * SV * (c0 + c1) * esz);
+    }
     if ((rc = gn_apply(a0, c0, a1, c1, d->a_gn, d->B, SV, d->dtype, act, s, 1))) return rc;
     a0 = act; c0 = c0 + c1; a1 = nullptr; c1 = 0;
     a0_cm = 1;

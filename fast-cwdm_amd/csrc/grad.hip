@@ -335,21 +335,49 @@ __global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__
 
 // out[b * stride + c] += sum_k part[b][k][c], k in order (fixed-order finish of
 // per-workgroup channel sums: the result does not depend on arrival order)
-__global__ void __launch_bounds__(256) chs_reduce_kernel(const float* __restrict__ part, int nk, int C,
-                                                        float* __restrict__ out_bc, long long bc_stride,
-                                                        float* __restrict__ out_c, float* __restrict__ out_c2, int B) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+// Fixed-order finish of [B][nk][C] partial rows: a 1024-thread block per 64
+// channels; thread (channel cl, row r) sums rows r, r + 16, ... with 8
+// interleaved accumulators (loads in flight, not a serial chain), then the 16
+// row sums are added in row order -- deterministic for a given nk.  (One
+// thread per channel walking all nk rows took ~90 us per call.)
+__global__ void __launch_bounds__(1024) chs_reduce_kernel(const float* __restrict__ part, int nk, int C,
+                                                         float* __restrict__ out_bc, long long bc_stride,
+                                                         float* __restrict__ out_c, float* __restrict__ out_c2,
+                                                         int B) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float tot = 0.f;
   for (int b = 0; b < B; ++b) {
-    const float* p = part + (long long)b * nk * C + c;
-    float s = 0.f;
-    for (int k = 0; k < nk; ++k) s += p[(long long)k * C];
-    if (out_bc) out_bc[(long long)b * bc_stride + c] += s;
-    tot += s;
+    float a[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = 0.f;
+    if (c < C) {
+      const float* p = part + (long long)b * nk * C + c;
+      int k = r;
+      for (; k + 16 * 7 < nk; k += 16 * 8) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += p[(long long)(k + 16 * e) * C];
+      }
+#pragma unroll
+      for (int e = 0; e < 7; ++e)
+        if (k + 16 * e < nk) a[e] += p[(long long)(k + 16 * e) * C];
+    }
+    red[r][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    __syncthreads();
+    if (r == 0 && c < C) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += red[q][cl];
+      if (out_bc) out_bc[(long long)b * bc_stride + c] += s;
+      tot += s;
+    }
+    __syncthreads();
   }
-  if (out_c) out_c[c] += tot;
-  if (out_c2) out_c2[c] += tot;
+  if (r == 0 && c < C) {
+    if (out_c) out_c[c] += tot;
+    if (out_c2) out_c2[c] += tot;
+  }
 }
 
 template <typename T, int MODE>
@@ -665,7 +693,7 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
        })))
     return rc;
   if (chs) {
-    hipLaunchKernelGGL(chs_reduce_kernel, dim3((unsigned)ceil_div(C, 256)), dim3(256), 0, s, chs_part, (int)nblk, C,
+    hipLaunchKernelGGL(chs_reduce_kernel, dim3((unsigned)ceil_div(C, 64)), dim3(1024), 0, s, chs_part, (int)nblk, C,
                        chs, (long long)chs_stride, nullptr, nullptr, (int)B);
     CWDM_LAUNCHED();
   }
@@ -742,7 +770,7 @@ extern "C" int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V
   });
   CWDM_LAUNCHED();
   if (part) {
-    hipLaunchKernelGGL(chs_reduce_kernel, dim3((unsigned)ceil_div(C, 256)), dim3(256), 0, s, part, (int)nb, C, out_bc,
+    hipLaunchKernelGGL(chs_reduce_kernel, dim3((unsigned)ceil_div(C, 64)), dim3(1024), 0, s, part, (int)nb, C, out_bc,
                        (long long)bc_stride, out_c, out_c2, (int)B);
     CWDM_LAUNCHED();
   }

@@ -114,8 +114,22 @@ struct Block {
 
 }  // namespace
 
+struct CopyJob {  // dst[0:n] = a[0:n] (+ b[0:n]): the fp32 parameter copies of a pack, one launch
+  float* dst;
+  const float* a;
+  const float* b;
+  long long n, blk0;
+};
+
 struct cwdm_unet {
   cwdm_unet_config cfg;
+  // device job tables of the batched packs (uploaded when the job list changes)
+  cwdm::PackJob* pack_tab = nullptr;
+  cwdm::PackJob* bwd_tab = nullptr;
+  CopyJob* copy_tab = nullptr;
+  size_t pack_cap = 0, bwd_cap = 0, copy_cap = 0;
+  std::vector<cwdm::PackJob> pack_cache, bwd_cache;
+  std::vector<CopyJob> copy_cache;
   int E = 0;                      // time embed dim
   std::vector<Param> params;
   std::vector<Tensor> tensors;
@@ -574,6 +588,20 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
               const void* res, int rmode, void* partial, hipStream_t s);
 extern thread_local unsigned* g_sg_sync;
 int64_t sg_sync_bytes(int ksplit);
+bool head_eligible(const cwdm_conv3d_desc* d);
+extern thread_local int g_wgrad_ws_zeroed;  // wgrad.hip
+extern thread_local std::vector<PackJob>* g_pack_batch;  // conv3d.hip
+int pack_batch_run(std::vector<PackJob>& jobs, int dtype, PackJob* table, std::vector<PackJob>& cache, hipStream_t s);
+// conv3d_v4.hip: where conv3d_v4_forward's GroupNorm pre-pass writes the
+// activated input (null: its own workspace), and whether it did
+extern thread_local void* g_act_keep;
+extern thread_local int g_act_kept;
+struct ActKeepScope {
+  void* ptr;
+  explicit ActKeepScope(void* p) : ptr(p) { g_act_keep = p; g_act_kept = 0; }
+  ~ActKeepScope() { g_act_keep = nullptr; }
+  bool used() const { return g_act_kept != 0; }
+};
 }  // namespace cwdm
 namespace {
 // the small-grid conv's K-split arrival counters for one launch list: one block
@@ -594,6 +622,11 @@ struct Layout {
   std::vector<int64_t> t_off, s_off, s_parts;
   std::vector<int64_t> ss_off, mr_off;
   int64_t total;
+  // training: the activated input (GroupNorm+SiLU, chunk-major) of every conv
+  // whose forward pre-pass writes one, kept past the inference total for the
+  // DMA-staged wgrad (cwdm_unet_train_workspace_bytes); -1 = not kept
+  std::vector<int64_t> keep_off;
+  int64_t train_total;
 };
 
 // shape-only descriptor of one conv step (pointers filled in by the forward)
@@ -672,6 +705,19 @@ Layout layout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
   }
   L.skipbuf = take(skipb);
   L.total = off;
+  L.keep_off.assign(u->convs.size(), -1);
+  for (size_t i = 0; i < u->convs.size(); ++i) {
+    const auto& cs = u->convs[i];
+    cwdm_conv3d_desc d = conv_shape(u, cs, B, D, H, W);
+    if (!dtype_half(u->cfg.dtype) || cs.gn < 0 || cs.amode > 1 || cs.s2 || cwdm::head_eligible(&d) ||
+        !cwdm::v4_eligible(&d))
+      continue;
+    const int64_t sv = cs.amode == 1 ? (d.D / 2) * (d.H / 2) * (d.W / 2) : d.D * d.H * d.W;
+    const int64_t cin = d.a_c0 + d.a_c1;
+    if (sv * cin * 2 >= (1LL << 31)) continue;  // the DMA wgrad's per-batch buffer range
+    L.keep_off[i] = take(B * sv * cin * es);
+  }
+  L.train_total = off;
   return L;
 }
 
@@ -679,6 +725,23 @@ Layout layout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
 
 namespace cwdm {
 namespace {
+__global__ void __launch_bounds__(256) copy_batch_kernel(const CopyJob* __restrict__ jobs, int njobs) {
+  const long long bid = blockIdx.x;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].blk0 <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const CopyJob j = jobs[lo];
+  const long long base = (bid - j.blk0) * 1024;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // 4 independent gathers in flight per thread
+    const long long i = base + k * 256 + threadIdx.x;
+    if (i < j.n) j.dst[i] = j.b ? j.a[i] + j.b[i] : j.a[i];
+  }
+}
+
 __global__ void vec_add_kernel(const float* a, const float* b, float* o, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) o[i] = a[i] + b[i];
@@ -734,6 +797,9 @@ extern "C" int cwdm_unet_create(const cwdm_unet_config* cfg, cwdm_unet** plan) {
 extern "C" void cwdm_unet_destroy(cwdm_unet* u) {
   if (!u) return;
   for (auto e : u->ev) (void)hipEventDestroy(e);
+  (void)hipFree(u->pack_tab);
+  (void)hipFree(u->bwd_tab);
+  (void)hipFree(u->copy_tab);
   delete u;
 }
 
@@ -767,57 +833,103 @@ extern "C" int cwdm_unet_alias_info(const cwdm_unet* u, int i, char* name, int c
 
 extern "C" int64_t cwdm_unet_packed_bytes(const cwdm_unet* u) { return u ? u->packed_bytes : -1; }
 
-extern "C" int cwdm_unet_pack(const cwdm_unet* u, const float* const* P, void* packed, cwdm_stream_t stream) {
-  CWDM_REQUIRE(u && P && packed, CWDM_E_INVALID, "cwdm_unet_pack: null pointer");
+// device table of n jobs (grown when needed)
+template <typename J>
+static int ensure_table(J*& tab, size_t& cap, size_t n) {
+  if (n <= cap) return CWDM_OK;
+  if (tab) CWDM_HIP(hipFree(tab));
+  tab = nullptr;
+  CWDM_HIP(hipMalloc(reinterpret_cast<void**>(&tab), n * sizeof(J)));
+  cap = n;
+  return CWDM_OK;
+}
+
+static int copy_batch_run(cwdm_unet* u, std::vector<CopyJob>& jobs, hipStream_t s) {
+  if (jobs.empty()) return CWDM_OK;
+  long long blk = 0;
+  for (auto& j : jobs) {
+    j.blk0 = blk;
+    blk += (j.n + 1023) / 1024;
+  }
+  int rc;
+  if ((rc = ensure_table(u->copy_tab, u->copy_cap, jobs.size()))) return rc;
+  if (u->copy_cache.size() != jobs.size() ||
+      std::memcmp(u->copy_cache.data(), jobs.data(), jobs.size() * sizeof(CopyJob))) {
+    CWDM_HIP(hipMemcpyAsync(u->copy_tab, jobs.data(), jobs.size() * sizeof(CopyJob), hipMemcpyHostToDevice, s));
+    CWDM_HIP(hipStreamSynchronize(s));
+    u->copy_cache = jobs;
+  }
+  hipLaunchKernelGGL(cwdm::copy_batch_kernel, dim3((unsigned)blk), dim3(256), 0, s, u->copy_tab, (int)jobs.size());
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+// collects every cwdm_conv3d_pack* of its scope into jobs (one launch later)
+struct PackBatchScope {
+  explicit PackBatchScope(std::vector<cwdm::PackJob>* v) { cwdm::g_pack_batch = v; }
+  ~PackBatchScope() { cwdm::g_pack_batch = nullptr; }
+};
+
+// (the packs and the fp32 parameter copies each go out as one batched launch;
+// one launch per parameter / conv cost ~2.5 ms per training step in copies,
+// vec-adds and pack kernels)
+extern "C" int cwdm_unet_pack(const cwdm_unet* uc, const float* const* P, void* packed, cwdm_stream_t stream) {
+  CWDM_REQUIRE(uc && P && packed, CWDM_E_INVALID, "cwdm_unet_pack: null pointer");
+  cwdm_unet* u = const_cast<cwdm_unet*>(uc);  // only the job-table cache changes
   hipStream_t s = (hipStream_t)stream;
   auto* base = reinterpret_cast<unsigned char*>(packed);
-  auto cp = [&](int pi, int64_t off) -> int {
-    CWDM_HIP(hipMemcpyAsync(base + off, P[pi], u->params[pi].numel() * 4, hipMemcpyDeviceToDevice, s));
-    return CWDM_OK;
+  std::vector<CopyJob> cj;
+  auto cp = [&](int pi, int64_t off) {
+    cj.push_back(CopyJob{reinterpret_cast<float*>(base + off), P[pi], nullptr, u->params[pi].numel(), 0});
   };
-  int rc;
-  if ((rc = cp(u->te_w1, u->off_te_w1)) || (rc = cp(u->te_b1, u->off_te_b1)) || (rc = cp(u->te_w2, u->off_te_w2)) ||
-      (rc = cp(u->te_b2, u->off_te_b2)))
-    return rc;
+  cp(u->te_w1, u->off_te_w1);
+  cp(u->te_b1, u->off_te_b1);
+  cp(u->te_w2, u->off_te_w2);
+  cp(u->te_b2, u->off_te_b2);
   float* ew = reinterpret_cast<float*>(base + u->off_emb_w);
   float* eb = reinterpret_cast<float*>(base + u->off_emb_b);
   for (size_t k = 0; k < u->emb_rows_w.size(); ++k) {
     const int64_t o = u->emb_rows_off[k], n = u->emb_rows_n[k];
-    CWDM_HIP(hipMemcpyAsync(ew + o * u->E, P[u->emb_rows_w[k]], n * u->E * 4, hipMemcpyDeviceToDevice, s));
-    if (u->emb_rows_cb[k] < 0) {
-      CWDM_HIP(hipMemcpyAsync(eb + o, P[u->emb_rows_b[k]], n * 4, hipMemcpyDeviceToDevice, s));
-    } else if ((rc = launch_vec_add(P[u->emb_rows_b[k]], P[u->emb_rows_cb[k]], eb + o, n, s))) {
-      return rc;
-    }
+    cj.push_back(CopyJob{ew + o * u->E, P[u->emb_rows_w[k]], nullptr, n * u->E, 0});
+    cj.push_back(CopyJob{eb + o, P[u->emb_rows_b[k]], u->emb_rows_cb[k] < 0 ? nullptr : P[u->emb_rows_cb[k]], n, 0});
   }
-  for (const auto& cs : u->convs) {
-    if (cs.s2) {
-      if ((rc = cwdm_conv3d_pack_s2(P[cs.w_p], cs.cout, cs.cin_a / 8, u->cfg.dtype, base + cs.w_off, 0, stream)))
-        return rc;
-    } else if ((rc = cwdm_conv3d_pack(P[cs.w_p], cs.cout, cs.cin_a, 3, u->cfg.dtype, base + cs.w_off, stream))) {
-      return rc;
-    }
-    if (cs.ws_p >= 0 &&
-        (rc = cwdm_conv3d_pack(P[cs.ws_p], cs.cout, cs.cin_b, 1, u->cfg.dtype, base + cs.wsk_off, stream)))
-      return rc;
-    if (cs.bias_kind == 0) {
-      float* bo = reinterpret_cast<float*>(base + cs.bias_off);
-      if (cs.wsb_p >= 0) {
-        if ((rc = launch_vec_add(P[cs.b_p], P[cs.wsb_p], bo, cs.cout, s))) return rc;
-      } else if ((rc = cp(cs.b_p, cs.bias_off))) {
+  std::vector<cwdm::PackJob> jobs;
+  int rc;
+  {
+    PackBatchScope scope(&jobs);
+    for (const auto& cs : u->convs) {
+      if (cs.s2) {
+        if ((rc = cwdm_conv3d_pack_s2(P[cs.w_p], cs.cout, cs.cin_a / 8, u->cfg.dtype, base + cs.w_off, 0, stream)))
+          return rc;
+      } else if ((rc = cwdm_conv3d_pack(P[cs.w_p], cs.cout, cs.cin_a, 3, u->cfg.dtype, base + cs.w_off, stream))) {
         return rc;
       }
+      if (cs.ws_p >= 0 &&
+          (rc = cwdm_conv3d_pack(P[cs.ws_p], cs.cout, cs.cin_b, 1, u->cfg.dtype, base + cs.wsk_off, stream)))
+        return rc;
+      if (cs.bias_kind == 0)
+        cj.push_back(CopyJob{reinterpret_cast<float*>(base + cs.bias_off), P[cs.b_p],
+                             cs.wsb_p >= 0 ? P[cs.wsb_p] : nullptr, cs.cout, 0});
     }
   }
   for (const auto& g : u->gns) {
-    if ((rc = cp(g.gamma_p, g.gamma_off)) || (rc = cp(g.beta_p, g.beta_off))) return rc;
+    cp(g.gamma_p, g.gamma_off);
+    cp(g.beta_p, g.beta_off);
   }
-  return CWDM_OK;
+  if ((rc = copy_batch_run(u, cj, s))) return rc;
+  if ((rc = ensure_table(u->pack_tab, u->pack_cap, jobs.size()))) return rc;
+  return cwdm::pack_batch_run(jobs, u->cfg.dtype, u->pack_tab, u->pack_cache, s);
 }
 
 extern "C" int64_t cwdm_unet_workspace_bytes(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
   if (!u || B <= 0 || D <= 0 || H <= 0 || W <= 0) return -1;
   return layout(u, B, D, H, W).total;
+}
+
+extern "C" int64_t cwdm_unet_train_workspace_bytes(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
+  const int64_t n = cwdm_unet_workspace_bytes(u, B, D, H, W);
+  if (n < 0) return n;
+  return layout(u, B, D, H, W).train_total;
 }
 
 extern "C" double cwdm_unet_flops(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
@@ -848,6 +960,8 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
   Layout L = layout(u, B, D, H, W);
   CWDM_REQUIRE(ws_bytes >= L.total, CWDM_E_WORKSPACE,
                "cwdm_unet_forward: workspace too small (need " + std::to_string(L.total) + " bytes)");
+  // a training-sized workspace keeps the convs' activated inputs for the backward
+  const bool keep = L.train_total > L.total && ws_bytes >= L.train_total;
   hipStream_t s = (hipStream_t)stream;
   auto* pk = reinterpret_cast<const unsigned char*>(packed);
   auto* wb = reinterpret_cast<unsigned char*>(ws);
@@ -960,7 +1074,7 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
       // conv1 of a skip block: SiLU(GN1(x)) for this conv and W_skip . x for conv2 in one pass
       const auto& c2 = u->convs[cs.skip_conv];
       const int64_t vpb = d.D * d.H * d.W;
-      void* act = wb + L.split;
+      void* act = keep && L.keep_off[st.idx] >= 0 ? wb + L.keep_off[st.idx] : wb + L.split;
       if ((rc = cwdm::gn_apply_skip(d.a0, d.a_c0, d.a1, d.a_c1, d.a_gn, B, vpb, u->cfg.dtype, pk + c2.wsk_off,
                                     c2.cout, act, wb + L.skipbuf, s)))
         return rc;
@@ -975,8 +1089,11 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
       if (samp && cs.out < 0 && cwdm::head_sampler_eligible(&d, samp)) {
         if ((rc = cwdm::head_sampler_forward(&d, samp, s))) return rc;
         if (fused) *fused = 1;
-      } else if ((rc = cwdm_conv3d_forward(&d, stream))) {
-        return rc;
+      } else {
+        cwdm::ActKeepScope ks(keep && L.keep_off[st.idx] >= 0 ? wb + L.keep_off[st.idx] : nullptr);
+        if ((rc = cwdm_conv3d_forward(&d, stream))) return rc;
+        CWDM_REQUIRE(!ks.ptr || ks.used(), CWDM_E_INVALID,
+                     "cwdm_unet_forward: conv " + std::to_string(st.idx) + " did not keep its activated input");
       }
     }
     if (u->profiling) {
@@ -1065,7 +1182,7 @@ namespace {
 
 struct GLayout {
   std::vector<int64_t> g_off;
-  int64_t sync, tmp, dout, deb, dsil, gnws, gnws_bytes, split, split_bytes, wgws, dwe, chs, chs_bytes, total;
+  int64_t sync, tmp, dout, deb, dsil, gnws, gnws_bytes, split, split_bytes, wgws, wgws_bytes, dwe, chs, chs_bytes, total;
 };
 
 int ckpad(const cwdm_unet* u, int c) {
@@ -1124,6 +1241,7 @@ GLayout glayout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) 
   G.split_bytes = split;
   G.split = take(split);
   G.wgws = take(wgws);
+  G.wgws_bytes = wgws;
   int64_t dwe = 0;   // expanded weight gradient of a stride-2 conv before folding
   for (const auto& cs : u->convs)
     if (cs.s2) dwe = std::max(dwe, (int64_t)cs.cout * cs.cin_a * 27 * 4);
@@ -1142,10 +1260,14 @@ GLayout glayout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) 
 
 extern "C" int64_t cwdm_unet_packed_bwd_bytes(const cwdm_unet* u) { return u ? u->packed_bwd_bytes : -1; }
 
-extern "C" int cwdm_unet_pack_bwd(const cwdm_unet* u, const float* const* P, void* packed_bwd, cwdm_stream_t stream) {
-  CWDM_REQUIRE(u && P && packed_bwd, CWDM_E_INVALID, "cwdm_unet_pack_bwd: null pointer");
+extern "C" int cwdm_unet_pack_bwd(const cwdm_unet* uc, const float* const* P, void* packed_bwd, cwdm_stream_t stream) {
+  CWDM_REQUIRE(uc && P && packed_bwd, CWDM_E_INVALID, "cwdm_unet_pack_bwd: null pointer");
+  cwdm_unet* u = const_cast<cwdm_unet*>(uc);  // only the job-table cache changes
   auto* base = reinterpret_cast<unsigned char*>(packed_bwd);
   int rc;
+  std::vector<cwdm::PackJob> jobs;
+  {
+  PackBatchScope scope(&jobs);
   for (size_t i = 0; i < u->convs.size(); ++i) {
     const auto& cs = u->convs[i];
     if (u->dg_off[i] >= 0 && cs.s2 &&
@@ -1158,7 +1280,9 @@ extern "C" int cwdm_unet_pack_bwd(const cwdm_unet* u, const float* const* P, voi
         (rc = cwdm_conv3d_pack_dgrad(P[cs.ws_p], cs.cout, cs.cin_b, 1, u->cfg.dtype, base + u->dgs_off[i], stream)))
       return rc;
   }
-  return CWDM_OK;
+  }
+  if ((rc = ensure_table(u->bwd_tab, u->bwd_cap, jobs.size()))) return rc;
+  return cwdm::pack_batch_run(jobs, u->cfg.dtype, u->bwd_tab, u->bwd_cache, (hipStream_t)stream);
 }
 
 extern "C" int64_t cwdm_unet_grad_workspace_bytes(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
@@ -1224,6 +1348,12 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
   // (every call: a caller may run segments on a fresh grad workspace)
   CWDM_HIP(hipMemsetAsync(gb + G.sync, 0, cwdm::sg_sync_bytes(2), s));
   SgSyncScope sync_scope(gb + G.sync);
+  // the wgrad scratch: zeroed once here, each wgrad's finishing pass leaves it zeroed
+  CWDM_HIP(hipMemsetAsync(gb + G.wgws, 0, G.wgws_bytes, s));
+  struct WgZeroScope {
+    WgZeroScope() { cwdm::g_wgrad_ws_zeroed = 1; }
+    ~WgZeroScope() { cwdm::g_wgrad_ws_zeroed = 0; }
+  } wg_zero_scope;
   auto P = [&](int64_t off) { return reinterpret_cast<const float*>(pk + off); };
   auto GR = [&](int pi) { return grads + u->goff[pi]; };
   auto act = [&](int id) -> const void* {
@@ -1254,6 +1384,19 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
     cwdm_wgrad_desc d{};
     d.dtype = dt; d.B = B; d.D = D >> level; d.H = H >> level; d.W = W >> level; d.ksize = ksize;
     d.u0 = u0; d.u_c0 = uc0; d.u1 = u1; d.u_c1 = uc1; d.u_mode = umode; d.u_gn = ugn;
+    d.dy = dy; d.dy_cs = dy_cs; d.cout = cout; d.dw = dw;
+    d.workspace = gb + G.wgws;
+    return cwdm_conv3d_wgrad(&d, stream);
+  };
+  // conv ci's wgrad from the activated input its forward kept (training
+  // workspace), else recomputed from the sources by the staging code
+  const bool kept = L.train_total > L.total && ws_bytes >= L.train_total;
+  auto wgrad_c = [&](int ci, int level, const void* u0, int uc0, const void* u1, int uc1, int umode,
+                     const float* ugn, const void* dy, int dy_cs, int cout, float* dw) -> int {
+    if (!kept || L.keep_off[ci] < 0) return wgrad(level, 3, u0, uc0, u1, uc1, umode, ugn, dy, dy_cs, cout, dw);
+    cwdm_wgrad_desc d{};
+    d.dtype = dt; d.B = B; d.D = D >> level; d.H = H >> level; d.W = W >> level; d.ksize = 3;
+    d.u0 = wb + L.keep_off[ci]; d.u_c0 = uc0 + uc1; d.u_mode = umode; d.u_cm = 1;
     d.dy = dy; d.dy_cs = dy_cs; d.cout = cout; d.dw = dw;
     d.workspace = gb + G.wgws;
     return cwdm_conv3d_wgrad(&d, stream);
@@ -1344,7 +1487,8 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
       if ((rc = cwdm_channel_sum(grd(o), dt, B, Vo, cout, cout, nullptr, 0, GR(c2.b_p), nullptr, gb + G.chs,
                                  G.chs_bytes, stream)))
         return rc;
-      if ((rc = wgrad(lout, 3, act(hh.out), cout, nullptr, 0, 0, ss_of(bk.g2), grd(o), cout, cout, GR(c2.w_p))))
+      if ((rc = wgrad_c(bk.c2, lout, act(hh.out), cout, nullptr, 0, 0, ss_of(bk.g2), grd(o), cout, cout,
+                        GR(c2.w_p))))
         return rc;
       if ((rc = cwdm_resample_add(grd(hx.out), grd(o), cout, B, D >> lout, H >> lout, W >> lout, 0, take_acc(hx.out),
                                   dt, stream)))
@@ -1391,7 +1535,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
       if ((rc = cwdm_channel_sum(grd(h1), dt, B, vox(lin), cout, cout, nullptr, 0, GR(c1.b_p), nullptr, gb + G.chs,
                                  G.chs_bytes, stream)))
         return rc;
-      if ((rc = wgrad(lin, 3, act(bk.x0), cin, nullptr, 0, 0, ss_of(bk.g1), grd(h1), cout, cout, GR(c1.w_p))))
+      if ((rc = wgrad_c(bk.c1, lin, act(bk.x0), cin, nullptr, 0, 0, ss_of(bk.g1), grd(h1), cout, cout, GR(c1.w_p))))
         return rc;
       if ((rc = dgrad(bk.c1, grd(h1)))) return rc;
       if ((rc = gn_bwd(bk.g1, bk.x0, -1, 0))) return rc;
@@ -1438,7 +1582,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
       if ((rc = cwdm_channel_sum(grd(o), dt, B, Vo, cout, cout, nullptr, 0, GR(c2.b_p),
                                  c2.wsb_p >= 0 ? GR(c2.wsb_p) : nullptr, gb + G.chs, G.chs_bytes, stream)))
         return rc;
-      if ((rc = wgrad(lout, 3, act(h1), cout, nullptr, 0, 0, ss_of(bk.g2), grd(o), cout, cout, GR(c2.w_p))))
+      if ((rc = wgrad_c(bk.c2, lout, act(h1), cout, nullptr, 0, 0, ss_of(bk.g2), grd(o), cout, cout, GR(c2.w_p))))
         return rc;
       if (c2.ws_p >= 0) {
         const int c0 = u->tensors[c2.sb0].channels, cc1 = c2.sb1 >= 0 ? u->tensors[c2.sb1].channels : 0;
@@ -1501,8 +1645,8 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
           return rc;
       } else {
         const int c0 = u->tensors[bk.x0].channels, cc1 = bk.x1 >= 0 ? u->tensors[bk.x1].channels : 0;
-        if ((rc = wgrad(lout, 3, act(bk.x0), c0, act(bk.x1), cc1, bk.updown == 1 ? 1 : 0, ss_of(bk.g1), grd(h1),
-                        cout, cout, GR(c1.w_p))))
+        if ((rc = wgrad_c(bk.c1, lout, act(bk.x0), c0, act(bk.x1), cc1, bk.updown == 1 ? 1 : 0, ss_of(bk.g1),
+                          grd(h1), cout, cout, GR(c1.w_p))))
           return rc;
       }
       if ((rc = dgrad(bk.c1, grd(h1)))) return rc;

@@ -85,6 +85,101 @@ __device__ __forceinline__ int tap_rows(int t) {
   return (kz * WHY + ky) * WHX + kx;
 }
 
+// The MFMAs of one brick (16-bit types): the halo images (NCH x WIMG) and the
+// brick's dY rows (256 x DYP) are in LDS; every wave accumulates its taps.
+template <typename T, int MC, int TAPS>
+__device__ __forceinline__ void wg_brick_mfma(const unsigned char* halo, const unsigned char* dyl,
+                                              f32x16 (&acc)[TAPS == 27 ? 7 : 1][MC], const int (&toff)[TAPS == 27 ? 7 : 1],
+                                              int ntap, int wv, int lane) {
+  using C = WgCfg<T, MC>;
+  constexpr int NT = TAPS == 27 ? 7 : 1;
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, h = g >> 1;
+  const unsigned char* bimg = halo + (g & 1) * WIMG + 8 * pp;
+  constexpr int NS = TAPS == 27 ? 16 : 4;   // K-steps of this wave
+  const int s0 = TAPS == 27 ? 0 : 4 * wv;
+  // fragments of K-step s: dY (A) for every co sub-tile, U (B) for every tap
+  auto load_frags = [&](int s, u32x4* a, u32x4* bfr) {
+    const int y = s & 3, z = s >> 2;
+#pragma unroll
+    for (int m = 0; m < MC; ++m) {
+      const int v0 = 16 * s + 8 * h + q, v1 = v0 + 4;
+      const int qd = 4 * m + 2 * (g & 1) + (pp >> 1);
+      const v4s lo = tr_read(dyl + v0 * C::DYP + dy_quad<T, MC>(qd, v0) * 16 + 8 * (pp & 1));
+      const v4s hi = tr_read(dyl + v1 * C::DYP + dy_quad<T, MC>(qd, v1) * 16 + 8 * (pp & 1));
+      a[m] = join(lo, hi);
+    }
+    const int hrow = (z * WHY + y) * WHX + 8 * h + q;
+    // every wave reads NT fragments (a wave with 6 taps reads a valid
+    // dummy 7th, toff = tap 0, and skips its MFMAs): no divergent phi on
+    // the operand registers
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      const unsigned char* bp = bimg + (hrow + toff[k]) * 32;
+      bfr[k] = join(tr_read(bp), tr_read(bp + 4 * 32));
+    }
+  };
+  // software pipeline: K-step s+1's LDS reads are in flight during K-step s's MFMAs
+  u32x4 fa0[MC], fb0[NT], fa1[MC], fb1[NT];
+  // every wave runs NT taps: the wave with 6 real taps accumulates a dummy 7th
+  // (tap 0 again, dropped by wg_combine) -- it would wait for the 7-tap waves at
+  // the next barrier anyway, and a conditional MFMA makes the accumulators phis
+  // (~190 v_accvgpr_mov per brick)
+  (void)ntap;
+  auto mfmas = [&](const u32x4* a, const u32x4* bfr) {
+#pragma unroll
+    for (int k = 0; k < NT; ++k)
+#pragma unroll
+      for (int m = 0; m < MC; ++m) mfma_acc(acc[k][m], a[m], bfr[k], (T*)nullptr);
+  };
+  // the next K-step's transposed reads interleaved with this step's MFMAs
+  // (2 reads per MFMA pair): at most 15 LDS reads may be tracked by
+  // lgkmcnt, so a block of 18 reads ahead of the MFMAs made every step wait
+  auto interleave = [&]() {
+#pragma unroll
+    for (int r = 0; r < (2 * MC + 2 * NT + 1) / 2; ++r) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    }
+  };
+  load_frags(s0, fa0, fb0);
+#pragma unroll 1
+  for (int i = 0; i < NS - 2; i += 2) {
+    load_frags(s0 + i + 1, fa1, fb1);
+    mfmas(fa0, fb0);
+    interleave();
+    load_frags(s0 + i + 2, fa0, fb0);
+    mfmas(fa1, fb1);
+    interleave();
+  }
+  load_frags(s0 + NS - 1, fa1, fb1);
+  mfmas(fa0, fb0);
+  interleave();
+  mfmas(fa1, fb1);
+}
+
+// combine: fp32 atomics into the [tap][co][ci] scratch -- one accumulator
+// register is two 128-B row segments (ci contiguous), the full-rate atomic
+// shape; OIDHW order would scatter the 64 lanes over 64 rows (~17x slower)
+template <int MC, int TAPS>
+__device__ __forceinline__ void wg_combine(float* dw, const f32x16 (&acc)[TAPS == 27 ? 7 : 1][MC], int cout, int cin,
+                                           int co0, int ci0, int ntap, int wv, int lane) {
+  constexpr int NT = TAPS == 27 ? 7 : 1;
+  const int ci = ci0 + (lane & 31);
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    if (k < ntap) {
+      const int tap = TAPS == 27 ? wv + 4 * k : 0;
+#pragma unroll
+      for (int m = 0; m < MC; ++m)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int co = co0 + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+          if (co < cout && ci < cin) atomicAdd(dw + ((long long)tap * cout + co) * cin + ci, acc[k][m][i]);
+        }
+    }
+  }
+}
+
 template <typename T, int MC, int MODE, bool GN, int TAPS>
 __global__ void __launch_bounds__(256) wgrad_kernel(WgradParams p) {
   using C = WgCfg<T, MC>;
@@ -174,66 +269,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradParams p) {
     if (PF && bi + 1 < be) fetch(bi + 1);  // next brick's loads fly during the MFMAs
 
     if constexpr (sizeof(T) == 2) {
-      const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, h = g >> 1;
-      const unsigned char* bimg = halo + (g & 1) * WIMG + 8 * pp;
-      constexpr int NS = TAPS == 27 ? 16 : 4;   // K-steps of this wave
-      const int s0 = TAPS == 27 ? 0 : 4 * wv;
-      // fragments of K-step s: dY (A) for every co sub-tile, U (B) for every tap
-      auto load_frags = [&](int s, u32x4* a, u32x4* bfr) {
-        const int y = s & 3, z = s >> 2;
-#pragma unroll
-        for (int m = 0; m < MC; ++m) {
-          const int v0 = 16 * s + 8 * h + q, v1 = v0 + 4;
-          const int qd = 4 * m + 2 * (g & 1) + (pp >> 1);
-          const v4s lo = tr_read(dyl + v0 * C::DYP + dy_quad<T, MC>(qd, v0) * 16 + 8 * (pp & 1));
-          const v4s hi = tr_read(dyl + v1 * C::DYP + dy_quad<T, MC>(qd, v1) * 16 + 8 * (pp & 1));
-          a[m] = join(lo, hi);
-        }
-        const int hrow = (z * WHY + y) * WHX + 8 * h + q;
-        // every wave reads NT fragments (a wave with 6 taps reads a valid
-        // dummy 7th, toff = tap 0, and skips its MFMAs): no divergent phi on
-        // the operand registers
-#pragma unroll
-        for (int k = 0; k < NT; ++k) {
-          const unsigned char* bp = bimg + (hrow + toff[k]) * 32;
-          bfr[k] = join(tr_read(bp), tr_read(bp + 4 * 32));
-        }
-      };
-      // software pipeline: K-step s+1's LDS reads are in flight during K-step s's MFMAs
-      u32x4 fa0[MC], fb0[NT], fa1[MC], fb1[NT];
-      auto mfmas = [&](const u32x4* a, const u32x4* bfr) {
-#pragma unroll
-        for (int k = 0; k < NT; ++k) {
-          if (k + 1 < NT || k < ntap) {
-#pragma unroll
-            for (int m = 0; m < MC; ++m) mfma_acc(acc[k][m], a[m], bfr[k], (T*)nullptr);
-          }
-        }
-      };
-      // the next K-step's transposed reads interleaved with this step's MFMAs
-      // (2 reads per MFMA pair): at most 15 LDS reads may be tracked by
-      // lgkmcnt, so a block of 18 reads ahead of the MFMAs made every step wait
-      auto interleave = [&]() {
-#pragma unroll
-        for (int r = 0; r < (2 * MC + 2 * NT + 1) / 2; ++r) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        }
-      };
-      load_frags(s0, fa0, fb0);
-#pragma unroll 1
-      for (int i = 0; i < NS - 2; i += 2) {
-        load_frags(s0 + i + 1, fa1, fb1);
-        mfmas(fa0, fb0);
-        interleave();
-        load_frags(s0 + i + 2, fa0, fb0);
-        mfmas(fa1, fb1);
-        interleave();
-      }
-      load_frags(s0 + NS - 1, fa1, fb1);
-      mfmas(fa0, fb0);
-      interleave();
-      mfmas(fa1, fb1);
+      wg_brick_mfma<T, MC, TAPS>(halo, dyl, acc, toff, ntap, wv, lane);
     } else {
       const int col = lane & 31, hh = lane >> 5;
       const int s_begin = TAPS == 27 ? 0 : 32 * wv, s_end = TAPS == 27 ? 128 : 32 * wv + 32;
@@ -258,35 +294,175 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradParams p) {
     }
   }
 
-  // combine: fp32 atomics into the [tap][co][ci] scratch -- one accumulator
-  // register is two 128-B row segments (ci contiguous), the full-rate atomic
-  // shape; OIDHW order would scatter the 64 lanes over 64 rows (~17x slower)
-  const int ci = ci0 + (lane & 31);
+  wg_combine<MC, TAPS>(p.dw, acc, p.cout, p.cin, co0, ci0, ntap, wv, lane);
+}
+
+// ---------------------------------------------------------------------------
+// DMA-staged variant (16-bit types, 3x3x3): U is the forward's activated input
+// kept chunk-major ([B][cin / 16][SV][16], cwdm_gn_apply's output, retained by
+// the training forward), so staging is a pure copy -- every byte of the halo
+// images and of the brick's dY rows reaches LDS by LDS-DMA (buffer loads with
+// an LDS destination; out-of-volume voxels get an out-of-range offset and land
+// as zeros), double-buffered: brick i+1's DMA flies during brick i's MFMAs, with
+// no VGPRs and no VALU spent on it.  The same LDS images and MFMA loop as
+// wgrad_kernel, so the products are identical.
+struct WgDmaParams {
+  int D, H, W;                 // conv (output) grid
+  int SD, SH, SW;              // source grid of U (half of D, H, W for MODE 1)
+  int tx, ty, tz;
+  long long nbricks, per;
+  int nco, cin, cout, dy_cs;
+  const unsigned char* act; long long act_bs;  // per-batch bytes of U (cin * SV * esz)
+  const unsigned char* dy; long long dy_bs;    // per-batch bytes of dY (V * dy_cs * esz)
+  float* dw;
+};
+
+// One LDS-DMA of 16 B per lane (lane l -> lds + 16 l), issued by inline asm so
+// the compiler does not track it: its waitcnt pass cannot prove the transposed
+// LDS reads (ds_read_b64_tr_b16) disjoint from an LDS-DMA and would drain every
+// in-flight DMA (vmcnt(0)) before the first of them -- the prefetch would be
+// serial.  Completion is the explicit vmcnt(0) + barrier at the next brick.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; nothing else in these kernels uses it
+__device__ __forceinline__ void wg_dma16(__amdgpu_buffer_rsrc_t r, unsigned char* lds, unsigned voff) {
+  const unsigned la =
+      __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(la), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <typename T, int MC, int MODE>
+__global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
+  using C = WgCfg<T, MC>;
+  constexpr int NCH = C::NCH, EPQ = 16 / (int)sizeof(T), QPV = C::DYP / 16;
+  constexpr int BUF = C::SMEM;           // one stage: the halo images + the dY rows
+  constexpr int HP = WHV * 2;            // halo pieces (16 B) per chunk image
+  constexpr int HI = (HP + 63) / 64;     // ... = wave instructions per chunk (21)
+  constexpr int DI = 256 * QPV / 64;     // dY wave instructions per brick
+  constexpr int ESZ = (int)sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int ct = blockIdx.y % p.nco, it = blockIdx.y / p.nco;
+  const int co0 = ct * C::CO, ci0 = it * 32;
+  const long long bb = (long long)blockIdx.x * p.per;
+  const long long be = bb + p.per < p.nbricks ? bb + p.per : p.nbricks;
+  const int ntap = wv < 3 ? 7 : 6;
+  int toff[7];
 #pragma unroll
-  for (int k = 0; k < NT; ++k) {
-    if (k < ntap) {
-      const int tap = TAPS == 27 ? wv + 4 * k : 0;
+  for (int k = 0; k < 7; ++k) toff[k] = tap_rows(wv + 4 * k < 27 ? wv + 4 * k : 0);
+  f32x16 acc[7][MC];
 #pragma unroll
-      for (int m = 0; m < MC; ++m)
+  for (int k = 0; k < 7; ++k)
+#pragma unroll
+    for (int m = 0; m < MC; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[k][m][i] = 0.f;
+  const int nb_vol = p.tx * p.ty * p.tz;
+  const long long sv_n = (long long)p.SD * p.SH * p.SW;
+
+  auto issue = [&](long long bi, unsigned char* buf) {
+    const int b = (int)(bi / nb_vol);
+    int r = (int)(bi % nb_vol);
+    const int x0 = (r % p.tx) * WBX;
+    r /= p.tx;
+    const int y0 = (r % p.ty) * WBY;
+    const int z0 = (r / p.ty) * WBZ;
+    const __amdgpu_buffer_rsrc_t ra =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(p.act + (long long)b * p.act_bs), (short)0, (int)p.act_bs, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(p.dy + (long long)b * p.dy_bs), (short)0, (int)p.dy_bs, 0x00020000);
+    // halo: instruction k of a chunk image covers pieces 64 k .. +63 = voxel slots 32 k .. +31, both quads
+#pragma unroll
+    for (int j = 0; j < (HI + 3) / 4; ++j) {
+      const int k = wv + 4 * j;
+      if (k < HI) {
+        const int pc = k * 64 + lane, hv = pc >> 1, q = pc & 1;
+        unsigned vb = 0xFFFFFFF0u;
+        const int hx = hv % WHX, hy = (hv / WHX) % WHY, hz = hv / (WHX * WHY);
+        int ox = x0 + hx - 1, oy = y0 + hy - 1, oz = z0 + hz - 1;
+        if (ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) {
+          if (MODE == 1) { ox >>= 1; oy >>= 1; oz >>= 1; }
+          vb = (unsigned)(((oz * p.SH + oy) * p.SW + ox) * 32 + q * 16);
+        }
+        if (hv < WHV) {
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) {
+            const unsigned cofs = (unsigned)((long long)(ci0 / 16 + c) * sv_n * 32);  // chunk ci0 / 16 + c
+            const unsigned voff = vb == 0xFFFFFFF0u ? vb : vb + cofs;
+            wg_dma16(ra, buf + c * WIMG + k * 1024, voff);
+          }
+        }
+      }
+    }
+    // dY rows: instruction k covers pieces 64 k .. +63 = (voxel v, LDS quad position pos)
+#pragma unroll
+    for (int j = 0; j < DI / 4; ++j) {
+      const int k = wv + 4 * j;
+      const int pc = k * 64 + lane, v = pc / QPV, pos = pc % QPV;
+      const int qd = dy_quad<T, MC>(pos, v);  // the swizzle is an involution
+      const int x = x0 + (v & 15), y = y0 + ((v >> 4) & 3), z = z0 + (v >> 6);
+      const int cc = co0 + qd * EPQ;
+      const bool in = x < p.W && y < p.H && z < p.D && cc < p.dy_cs;
+      const unsigned voff =
+          in ? ((unsigned)((z * p.H + y) * p.W + x) * (unsigned)p.dy_cs + (unsigned)cc) * (unsigned)ESZ : 0xFFFFFFF0u;
+      wg_dma16(rd, buf + C::DY_OFF + k * 1024, voff);
+    }
+  };
+
+  if (bb < be) issue(bb, smem);
+  for (long long bi = bb; bi < be; ++bi) {
+    unsigned char* cur = smem + ((bi - bb) & 1) * BUF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this brick's DMA (issued one brick ago) landed
+    __syncthreads();                                  // ... for every wave; the other stage is free
+    if (bi + 1 < be) issue(bi + 1, smem + ((bi - bb + 1) & 1) * BUF);
+    wg_brick_mfma<T, MC, 27>(cur, cur + C::DY_OFF, acc, toff, ntap, wv, lane);
+  }
+  // combine straight into dw (OIDHW, fp32): per 32-channel half m of the tile the
+  // four waves' taps meet in LDS as [co 32][ci 32][tap 27] (the stages are
+  // free now), then every row co -- 32 ci x 27 taps = 864 contiguous floats of
+  // dw -- goes out as coalesced atomics.  No scratch, no memset, no
+  // transposing pass.
+  float* T3 = reinterpret_cast<float*>(smem);
+  const int cil = lane & 31;
+#pragma unroll
+  for (int m = 0; m < MC; ++m) {
+    __syncthreads();  // the previous half's rows are out (m = 0: the last brick's reads are done)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      if (k < ntap) {
+        const int tap = wv + 4 * k;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int co = co0 + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-          if (co < p.cout && ci < p.cin)
-            atomicAdd(p.dw + ((long long)tap * p.cout + co) * p.cin + ci, acc[k][m][i]);
+          const int col = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+          T3[(col * 32 + cil) * 27 + tap] = acc[k][m][i];
         }
+      }
+    }
+    __syncthreads();
+    const int ncol = min(32, p.cout - co0 - 32 * m), nci = min(32, p.cin - ci0);
+    for (int r = 0; r < ncol; ++r) {
+      float* row = p.dw + ((long long)(co0 + 32 * m + r) * p.cin + ci0) * 27;
+      for (int e = tid; e < nci * 27; e += 256) atomicAdd(row + e, T3[r * 864 + e]);
     }
   }
 }
 
 // dW[co][ci][tap] += scratch[tap][co][ci]
-__global__ void __launch_bounds__(256) wgrad_finish_kernel(const float* __restrict__ scr, float* __restrict__ dw,
-                                                          int cout, int cin, int taps) {
+// (rezero: leave the scratch zeroed for the next call -- the plan's backward
+// zeroes it once per call instead of once per conv)
+__global__ void __launch_bounds__(256) wgrad_finish_kernel(float* __restrict__ scr, float* __restrict__ dw,
+                                                          int cout, int cin, int taps, int rezero) {
   const long long n = (long long)cout * cin * taps;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const int tap = (int)(i % taps);
   const long long oc = i / taps;  // co * cin + ci
-  dw[i] += scr[(long long)tap * cout * cin + oc];
+  const long long si = (long long)tap * cout * cin + oc;
+  dw[i] += scr[si];
+  if (rezero) scr[si] = 0.f;
 }
 
 template <typename T, int MC, int MODE, bool GN, int TAPS>
@@ -307,10 +483,25 @@ int dispatch_wg(const WgradParams& p, int mode, bool gn, dim3 grid, hipStream_t 
   return gn ? launch_wg<T, MC, 0, true, 27>(p, grid, s) : launch_wg<T, MC, 0, false, 27>(p, grid, s);
 }
 
+template <typename T, int MC, int MODE>
+int launch_wg_dma(const WgDmaParams& p, dim3 grid, hipStream_t s) {
+  constexpr int smem = 2 * WgCfg<T, MC>::SMEM;
+  static_assert(smem <= 160 * 1024, "wgrad DMA LDS");
+  auto k = wgrad_dma_kernel<T, MC, MODE>;
+  CWDM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, smem));
+  hipLaunchKernelGGL(k, grid, dim3(256), smem, s, p);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
 }  // namespace
 }  // namespace cwdm
 
 using namespace cwdm;
+
+namespace cwdm {
+thread_local int g_wgrad_ws_zeroed = 0;  // the plan's backward: the scratch is zero on entry, leave it zero
+}
 
 extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream) {
   CWDM_REQUIRE(d, CWDM_E_INVALID, "cwdm_conv3d_wgrad: null desc");
@@ -357,15 +548,38 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
   hipStream_t s = (hipStream_t)stream;
   const bool gn = d->u_gn != nullptr;
   const long long nw = (long long)d->cout * cin * p.taps;
-  CWDM_HIP(hipMemsetAsync(d->workspace, 0, nw * 4, s));
+  const int zeroed = g_wgrad_ws_zeroed;
   int rc;
+  if (d->u_cm) {
+    // U kept chunk-major by the forward: the DMA-staged kernel
+    CWDM_REQUIRE(dtype_half(d->dtype) && d->ksize == 3 && !d->u_gn && !d->u1 && d->u_c1 == 0, CWDM_E_UNSUPPORTED,
+                 "cwdm_conv3d_wgrad: u_cm needs a 16-bit dtype, ksize 3, one source and no GroupNorm prologue");
+    WgDmaParams q{};
+    q.D = (int)d->D; q.H = (int)d->H; q.W = (int)d->W;
+    q.SD = d->u_mode == 1 ? q.D / 2 : q.D; q.SH = d->u_mode == 1 ? q.H / 2 : q.H; q.SW = d->u_mode == 1 ? q.W / 2 : q.W;
+    q.tx = p.tx; q.ty = p.ty; q.tz = p.tz; q.nbricks = p.nbricks; q.per = p.per; q.nco = p.nco;
+    q.cin = cin; q.cout = d->cout; q.dy_cs = d->dy_cs;
+    const long long sv = (long long)q.SD * q.SH * q.SW, V = d->D * d->H * d->W;
+    q.act = reinterpret_cast<const unsigned char*>(d->u0); q.act_bs = sv * cin * 2;
+    q.dy = reinterpret_cast<const unsigned char*>(d->dy); q.dy_bs = V * d->dy_cs * 2;
+    q.dw = d->dw;  // accumulated into directly (OIDHW)
+    CWDM_REQUIRE(q.act_bs < (1LL << 31) && q.dy_bs < (1LL << 31), CWDM_E_UNSUPPORTED,
+                 "cwdm_conv3d_wgrad: u_cm sources above 2 GB per batch");
+    rc = d->dtype == CWDM_F16
+             ? (mc == 2 ? (d->u_mode ? launch_wg_dma<f16_t, 2, 1>(q, grid, s) : launch_wg_dma<f16_t, 2, 0>(q, grid, s))
+                        : (d->u_mode ? launch_wg_dma<f16_t, 1, 1>(q, grid, s) : launch_wg_dma<f16_t, 1, 0>(q, grid, s)))
+             : (mc == 2 ? (d->u_mode ? launch_wg_dma<bf16_t, 2, 1>(q, grid, s) : launch_wg_dma<bf16_t, 2, 0>(q, grid, s))
+                        : (d->u_mode ? launch_wg_dma<bf16_t, 1, 1>(q, grid, s) : launch_wg_dma<bf16_t, 1, 0>(q, grid, s)));
+    return rc;
+  }
+  if (!zeroed) CWDM_HIP(hipMemsetAsync(d->workspace, 0, nw * 4, s));
   rc = dispatch_dtype(d->dtype, [&](auto tag) -> int {
     using T = decltype(tag);
     return mc == 2 ? dispatch_wg<T, 2>(p, d->u_mode, gn, grid, s) : dispatch_wg<T, 1>(p, d->u_mode, gn, grid, s);
   });
   if (rc) return rc;
   hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)ceil_div(nw, 256)), dim3(256), 0, s,
-                     reinterpret_cast<const float*>(d->workspace), d->dw, d->cout, cin, p.taps);
+                     reinterpret_cast<float*>(d->workspace), d->dw, d->cout, cin, p.taps, zeroed);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }

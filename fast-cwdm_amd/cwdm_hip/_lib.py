@@ -79,6 +79,7 @@ class WgradDesc(ctypes.Structure):
         ("dy", vp), ("dy_cs", ctypes.c_int), ("cout", ctypes.c_int),
         ("dw", vp),
         ("workspace", vp),
+        ("u_cm", ctypes.c_int),
     ]
 
 
@@ -173,6 +174,7 @@ _PROTOS = {
     "cwdm_unet_packed_bytes": (i64, [vp]),
     "cwdm_unet_pack": (ctypes.c_int, [vp, ctypes.POINTER(vp), vp, vp]),
     "cwdm_unet_workspace_bytes": (i64, [vp, i64, i64, i64, i64]),
+    "cwdm_unet_train_workspace_bytes": (i64, [vp, i64, i64, i64, i64]),
     "cwdm_unet_forward": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, i64, vp]),
     "cwdm_unet_forward_step": (ctypes.c_int, [vp, vp, vp, vp, ctypes.POINTER(SamplerArgs), i64, i64, i64, i64,
                                               vp, i64, ctypes.POINTER(ctypes.c_int), vp]),

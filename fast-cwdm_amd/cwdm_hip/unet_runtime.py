@@ -92,6 +92,14 @@ class UNetPlan:
             raise AssertionError("bad grid")
         return n
 
+    def train_workspace_bytes(self, B, D, H, W):
+        """Forward workspace that also keeps the convs' activated inputs for
+        the DMA-staged weight gradients (cwdm_unet_train_workspace_bytes)."""
+        n = int(lib().cwdm_unet_train_workspace_bytes(self._h, B, D, H, W))
+        if n < 0:
+            raise AssertionError("bad grid")
+        return n
+
     def workspace(self, B, D, H, W, device):
         key = (B, D, H, W, str(device))
         if self._ws_key != key:

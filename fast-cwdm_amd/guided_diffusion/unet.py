@@ -142,6 +142,9 @@ class UNetModel(nn.Module):
         self._packed_bwd_key = None
         self._grad_hook = None       # called per backward segment (DDP bucket all-reduce)
         self._last_grad_flat = None
+        # training forward keeps the DMA-staged convs' activated inputs (more
+        # workspace, no GroupNorm+SiLU recompute in the weight gradients)
+        self.keep_activations = True
         self._flatten_params()
 
     # ---- flat parameter storage ---------------------------------------------
@@ -243,7 +246,11 @@ class UNetModel(nn.Module):
         if self._packed is None or self._packed_key != key:
             ops._need_cuda(*params)
             flat = [p.detach().float().contiguous() for p in params]
-            self._packed = self.plan.pack(flat)
+            # re-pack in place (stream-ordered after earlier readers; a captured
+            # sampling graph keeps a valid pointer; the plan's batched pack job
+            # table stays cached when no pointer moved)
+            old = self._packed if (self._packed is not None and self._packed.device == flat[0].device) else None
+            self._packed = self.plan.pack(flat, packed=old)
             self._packed_key = key
         return self._packed
 
@@ -253,7 +260,9 @@ class UNetModel(nn.Module):
         key = self._weights_key()
         if self._packed_bwd is None or self._packed_bwd_key != key:
             ops._need_cuda(*params)
-            self._packed_bwd = self.plan.pack_bwd([p.detach() for p in params])
+            old = self._packed_bwd if (self._packed_bwd is not None and
+                                       self._packed_bwd.device == params[0].device) else None
+            self._packed_bwd = self.plan.pack_bwd([p.detach() for p in params], packed_bwd=old)
             self._packed_bwd_key = key
         return self._packed_bwd
 
@@ -334,7 +343,11 @@ class _UNetTrain(th.autograd.Function):
         B, C, D, H, W = x.shape
         plan = model.plan
         xin, t = model._prep_inputs(x, timesteps)
-        ws = th.empty(plan.workspace_bytes(B, D, H, W), dtype=th.uint8, device=x.device)
+        # the training workspace: the forward keeps each DMA-staged conv's
+        # activated input there for the backward's weight gradients
+        nbytes = plan.train_workspace_bytes(B, D, H, W) if model.keep_activations else \
+            plan.workspace_bytes(B, D, H, W)
+        ws = th.empty(nbytes, dtype=th.uint8, device=x.device)
         out_nd = th.empty((B, D, H, W, model.out_channels), dtype=th.float32, device=x.device)
         plan.forward(model.packed_weights(), xin, t, out_nd, B, D, H, W, ws=ws)
         ctx.model = model
@@ -366,12 +379,21 @@ class _UNetTrain(th.autograd.Function):
             hook(None, grads, 0, grads.numel())
         del ws, gws
         model._last_grad_flat = grads
-        views = []
+        # a parameter without a gradient gets its view of the flat buffer as
+        # .grad directly (autograd would clone each returned view: ~230 copies per
+        # step); one that already has one (gradient accumulation) gets the view
+        # returned and added by autograd as usual
+        out = []
         o = 0
-        for _, shape in plan.param_specs:
+        for p, (_, shape) in zip(model.parameters(), plan.param_specs):
             n = 1
             for s_ in shape:
                 n *= s_
-            views.append(grads[o:o + n].view(shape))
+            view = grads[o:o + n].view(shape)
             o += n
-        return (None, None, None, *views)
+            if p.grad is None and p.requires_grad:
+                p.grad = view
+                out.append(None)
+            else:
+                out.append(view)
+        return (None, None, None, *out)

@@ -385,6 +385,10 @@ typedef struct {
   const void* dy; int dy_cs; int cout;   /* dy [B][V][dy_cs] in dtype, first cout channels */
   float* dw;                /* fp32 [cout][cin][ksize^3] */
   void* workspace;
+  int u_cm;                 /* 1: u0 is the conv's input as the forward's GroupNorm pre-pass wrote it --
+                               activated, chunk-major [B][cin/16][SV][16] (SV = the source grid, half of
+                               D, H, W for u_mode 1), 16-bit dtype, ksize 3, u_gn NULL, no u1: staged by
+                               LDS-DMA with no recompute */
 } cwdm_wgrad_desc;
 int64_t cwdm_conv3d_wgrad_workspace_bytes(int cout, int cin, int ksize);
 int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* desc, cwdm_stream_t stream);
@@ -464,6 +468,13 @@ int64_t cwdm_unet_packed_bytes(const cwdm_unet* plan);
 int cwdm_unet_pack(const cwdm_unet* plan, const float* const* params, void* packed,
                    cwdm_stream_t stream);
 int64_t cwdm_unet_workspace_bytes(const cwdm_unet* plan, int64_t B, int64_t D, int64_t H, int64_t W);
+/* Training workspace: cwdm_unet_workspace_bytes plus room for the activated
+ * input (GroupNorm+SiLU, chunk-major) of every conv whose forward pre-pass
+ * writes one (16-bit plans, DMA-staged levels).  A forward given at least this
+ * many bytes keeps them there, and cwdm_unet_backward on that workspace stages
+ * those convs' weight gradients from them by LDS-DMA instead of recomputing the
+ * GroupNorm+SiLU (cwdm_wgrad_desc.u_cm). */
+int64_t cwdm_unet_train_workspace_bytes(const cwdm_unet* plan, int64_t B, int64_t D, int64_t H, int64_t W);
 /* x: NDHWC (B, D, H, W, in_channels) in plan dtype; t: device fp32[B] model timesteps;
  * out: NDHWC fp32 (B, D, H, W, out_channels). */
 int cwdm_unet_forward(cwdm_unet* plan, const void* packed, const void* x, const float* t,

@@ -367,9 +367,8 @@ def test_conv3d_dma_kernel_vs_torch(case, dtype_name):
 
 
 SG_CASES = [
-    # name, B, grid(out), c0, c1, cout, amode, gn, skip1x1, rmode  (bf16; W = 16, H % 4 == 0, D % 4 == 0,
-    # cout % 64 == 0, 32-channel K chunks: the small-grid kernel, conv3d_sg.hip, incl. its 1x1 skip mode;
-    # the W = 8 cases run the split-K brick kernels beside it)
+    # name, B, grid(out), c0, c1, cout, amode, gn, skip1x1, rmode  (16-bit; W < 32, cout % 64 == 0,
+    # 32-channel K chunks: the small-grid kernel, conv3d_sg.hip, incl. its 1x1 skip mode and K split)
     ("sg16_gn_res", 1, (16, 16, 16), 64, 0, 64, 0, True, False, 0),
     ("sg16_concat_skip", 2, (4, 8, 16), 48, 16, 128, 0, True, True, -1),
     ("sg16_up_res", 1, (8, 4, 16), 32, 0, 64, 1, True, False, 1),
@@ -377,6 +376,18 @@ SG_CASES = [
     ("sg8_up_nogn", 2, (4, 8, 8), 32, 0, 128, 1, False, False, -1),
     ("sg8_production", 1, (8, 8, 8), 256, 256, 256, 0, True, True, -1),
     ("sg16_production_skip", 1, (16, 16, 16), 256, 256, 256, 0, True, True, -1),
+    # partial bricks (r03: config 5's 28^3 / 14^3 levels and any W < 32): the last brick of
+    # an axis computes zero-padded voxels and drops them (stores, residual, statistics)
+    ("sg28_config5_res", 1, (28, 28, 28), 128, 0, 128, 0, True, False, 0),
+    ("sg14_config5_concat_skip", 1, (14, 14, 14), 128, 128, 128, 0, True, True, -1),
+    ("sg20_up_res", 1, (12, 20, 20), 64, 0, 64, 1, True, False, 1),
+    ("sg12_concat_nogn", 2, (6, 10, 12), 32, 32, 64, 0, False, False, -1),
+    ("sg_odd_gn_res", 1, (5, 7, 9), 32, 0, 64, 0, True, False, 0),
+    ("sg14_ksplit_skip", 1, (7, 7, 14), 256, 0, 256, 0, True, True, -1),
+    ("sg14_ksplit_res", 1, (7, 7, 14), 256, 0, 256, 0, True, False, 0),
+    # a 1x1 skip AND a residual: not a U-Net shape; the DMA / small-grid path
+    # refuses it (the skip is its residual slot) and the brick kernels run it
+    ("sg_skip_plus_res_legacy", 1, (4, 8, 12), 64, 0, 64, 0, True, True, 0),
 ]
 
 

@@ -79,7 +79,19 @@ def test_conv3d_wgrad_random_shapes_vs_torch(case, dtype_name):
     _run_wgrad_case(case, dtype_name)
 
 
-def _run_wgrad_case(case, dtype_name):
+CM_CASES = [c for c in WG_CASES + RANDOM_WG_CASES if c[8] == 3]
+
+
+@pytest.mark.parametrize("dtype_name", ["bf16", "fp16"])
+@pytest.mark.parametrize("case", CM_CASES, ids=[c[0] for c in CM_CASES])
+def test_conv3d_wgrad_kept_activation_vs_torch(case, dtype_name):
+    """u_cm: U handed over as the forward kept it (activated, chunk-major
+    [B][cin/16][SV][16]) and staged by LDS-DMA -- the exact staged input, so
+    only the fp32 summation order differs from torch (1e-4)."""
+    _run_wgrad_case(case, dtype_name, cm=True)
+
+
+def _run_wgrad_case(case, dtype_name, cm=False):
     from cwdm_hip import _lib
     from cwdm_hip._lib import check, lib
     name, B, grid, c0, c1, cout, umode, use_gn, k, dy_cs = case
@@ -99,10 +111,11 @@ def _run_wgrad_case(case, dtype_name):
         shift = 0.2 * torch.randn(B, cin, generator=g)
         gn = torch.stack([scale, shift], -1).contiguous()
         h = F.silu(x * scale[:, :, None, None, None] + shift[:, :, None, None, None])
-    if umode == 1:
-        h = F.interpolate(h, scale_factor=2, mode="nearest")
     if dtype_name != "fp32":
         h = h.to(tdt).float()   # staged in bf16 / fp16 like the forward
+    h_src = h
+    if umode == 1:
+        h = F.interpolate(h, scale_factor=2, mode="nearest")
     ref = torch.nn.grad.conv3d_weight(h, (cout, cin, k, k, k), dy, padding=(k // 2))
     xd = _nd(x).to(DEV, tdt)
     x0 = xd[..., :c0].contiguous()
@@ -119,10 +132,14 @@ def _run_wgrad_case(case, dtype_name):
     d.u_gn = gnd.data_ptr() if gnd is not None else None
     d.dy, d.dy_cs, d.cout = dyd.data_ptr(), dy_cs, cout
     d.dw = dw.data_ptr()
+    if cm:
+        sv = sD * sH * sW
+        act = _nd(h_src).reshape(B, sv, cin // 16, 16).permute(0, 2, 1, 3).contiguous().to(DEV, tdt)
+        d.u0, d.u_c0, d.u1, d.u_c1, d.u_gn, d.u_cm = act.data_ptr(), cin, None, 0, None, 1
     wsw = torch.empty(lib().cwdm_conv3d_wgrad_workspace_bytes(cout, cin, k), dtype=torch.uint8, device=DEV)
     d.workspace = wsw.data_ptr()
     check(lib().cwdm_conv3d_wgrad(ctypes.byref(d), None))
-    tol = 1e-4 if dtype_name == "fp32" else 1e-2
+    tol = 1e-4 if (dtype_name == "fp32" or cm) else 1e-2
     assert rel_err(dw, ref) < tol, name
 
 
@@ -330,8 +347,9 @@ def _product_model(cfg, groups, params, dtype):
     return m.to(DEV)
 
 
-def _unet_grads(cfg, G, P, x, t, R, dtype):
+def _unet_grads(cfg, G, P, x, t, R, dtype, keep=True):
     model = _product_model(cfg, G, P, dtype)
+    model.keep_activations = keep
     out = model(x.to(DEV), t.to(DEV))
     (out * R.to(DEV)).sum().backward()
     return out.detach().cpu(), {n: p.grad.detach().cpu() for n, p in model.named_parameters()}, model
@@ -559,6 +577,32 @@ def test_production_unet_backward_half_close_to_fp32(dtype, tol_out, tol_grad):
     print(dtype, "out rel", rel_err(out, ref_out), "worst grads", top)
     assert rel_err(out, ref_out) < tol_out
     assert top[0][1] < tol_grad, top
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_production_unet_backward_kept_activations(dtype):
+    """The training workspace (cwdm_unet_train_workspace_bytes): the forward
+    keeps every DMA-staged conv's activated input and their weight gradients
+    stage it by LDS-DMA (wgrad u_cm) instead of recomputing GroupNorm+SiLU --
+    the same products up to the recompute's 16-bit rounding and the atomics'
+    order: every gradient within 5e-3 rel-L2 of the recompute path, and the
+    output bit-identical (the forward only writes the pre-pass elsewhere)."""
+    from cwdm_hip._lib import lib
+    P, x, t, R = _prod_case()
+    prev = lib().cwdm_conv3d_set_path(2)
+    try:
+        out_k, g_k, m = _unet_grads(PROD_CFG, 32, P, x, t, R, dtype, keep=True)
+        B, _, D, H, W = x.shape
+        assert m.plan.train_workspace_bytes(B, D, H, W) > m.plan.workspace_bytes(B, D, H, W)
+        out_r, g_r, _ = _unet_grads(PROD_CFG, 32, P, x, t, R, dtype, keep=False)
+    finally:
+        lib().cwdm_conv3d_set_path(prev)
+    assert torch.equal(out_k, out_r)
+    worst = {k: float((g_k[k].double() - g_r[k].double()).norm() / g_r[k].double().norm().clamp_min(1e-30))
+             for k in g_r}
+    top = sorted(worst.items(), key=lambda kv: -kv[1])[:5]
+    print(dtype, "kept vs recompute worst", top)
+    assert top[0][1] < 5e-3, top
 
 
 @pytest.mark.parametrize("k", [0, 1], ids=["tiny", "runsh"])
