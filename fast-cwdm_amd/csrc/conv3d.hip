@@ -247,6 +247,8 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s);
 int legacy_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream);
 bool head_eligible(const cwdm_conv3d_desc* d);
 int head_conv_forward(const cwdm_conv3d_desc* d, hipStream_t s);
+bool pw_eligible(const cwdm_conv3d_desc* d);
+int pw_forward(const cwdm_conv3d_desc* d, hipStream_t s);
 }  // namespace cwdm
 
 extern "C" int64_t cwdm_conv3d_workspace_bytes(const cwdm_conv3d_desc* d) {
@@ -282,6 +284,7 @@ extern "C" int cwdm_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stre
   CWDM_REQUIRE(d->out_dtype == CWDM_F32 || d->out_dtype == d->dtype, CWDM_E_INVALID,
                "cwdm_conv3d_forward: output dtype must be fp32 or the compute dtype");
   if (head_eligible(d)) return head_conv_forward(d, (hipStream_t)stream);
+  if (pw_eligible(d)) return pw_forward(d, (hipStream_t)stream);
   if (v4_eligible(d)) {
     const int64_t need = v4_workspace_bytes(d);
     if (need == 0 || (d->workspace && d->ws_bytes >= need)) return conv3d_v4_forward(d, (hipStream_t)stream);

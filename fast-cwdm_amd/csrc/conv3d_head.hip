@@ -28,6 +28,7 @@
 // step's U-Net input.  The fp32 model output never reaches HBM, and with
 // Philox noise neither does the noise tensor.
 #include <atomic>
+#include <cstdlib>
 
 #include "conv3d_kernels.hpp"
 #include "sampler.hpp"
@@ -299,7 +300,9 @@ int head_conv_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
 }
 
 bool head_sampler_eligible(const cwdm_conv3d_desc* d, const cwdm_sampler_args* a) {
-  return head_eligible(d) && d->a_gn && d->cout == 8 && a->levels <= 1 && a->B == d->B && a->d == d->D && a->h == d->H &&
+  // CWDM_HEAD_SAMPLER=0: the unfused forward + cwdm_sampler_step (A/B switch)
+  static const bool on = [] { const char* e = std::getenv("CWDM_HEAD_SAMPLER"); return !(e && e[0] == '0'); }();
+  return on && head_eligible(d) && d->a_gn && d->cout == 8 && a->levels <= 1 && a->B == d->B && a->d == d->D && a->h == d->H &&
          a->w == d->W && a->x_t && a->x_prev && a->coef && a->t && a->T > 0 &&
          (!a->mirror || a->mirror_dtype == d->dtype || a->mirror_dtype == CWDM_F32);
 }

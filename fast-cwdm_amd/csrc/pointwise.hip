@@ -1,0 +1,167 @@
+// Pure 1x1x1 conv on the wide levels (segment B alone: the ResBlock
+// skip_connection conv of unet.py:264-271 where the forward does not fuse it,
+// and its input gradient in the backward -- the dual-output, accumulating
+// "skip dgrad" of the plan): a channels-last GEMM over voxels,
+//
+//   out[b, v, n] (+)= bias[n] + sum_k in[b, v, k] W[n][k],   in = concat(b0, b1)
+//
+// memory-bound (K, N <= a few hundred), so the design is about streaming: one
+// workgroup = 256 voxels x 128 output channels; wave w = 64 voxels (two 32-voxel
+// blocks) x 4 blocks of 32 channels = 8 accumulators of v_mfma_f32_32x32x16
+// (A = 32 output channels x 16 K of the packed weights, B = 16 K x 32 voxels
+// straight from the channels-last rows, 16 B per lane); the next K step's
+// fragments are loaded while this step's MFMAs run.  An accumulator lane holds
+// 4 runs of 4 consecutive channels of one voxel: 8-byte stores (and loads when
+// accumulating).  The brick kernels this replaces ran the R0 skip dgrads at
+// ~0.06 PF (690-910 us each, ~3 ms per training step).
+#include "conv3d_kernels.hpp"
+
+namespace cwdm {
+
+struct PwParams {
+  long long V;            // voxels per batch entry (all of them: B * V rows)
+  long long rows;         // B * V
+  int K, K0;              // input channels (b0: K0, b1: K - K0)
+  const void* b0;
+  const void* b1;
+  const unsigned char* w; // cwdm_conv3d_pack layout, ksize 1 (NT rows per channel tile, 16-channel chunks)
+  int N, NT;
+  const float* bias; long long bias_bs;
+  void* out; void* out1; int out_c0; int accumulate;
+  int nnb;                // 128-channel blocks of N
+};
+
+namespace {
+
+// element (co, ci) of the packed weights (pack_elem's layout, one tap)
+template <typename T>
+__device__ __forceinline__ long long pw_widx(int co, int ci, int K, int NT) {
+  constexpr int CK = ConvTr<T>::CK, EPQ = ConvTr<T>::EPQ;
+  const int ct = co / NT, n = co % NT, chunk = ci / CK, q = (ci % CK) / EPQ, e = ci % EPQ;
+  const int qp = q ^ ((n >> 3) & 1);
+  return ((((long long)ct * (K / CK) + chunk) * NT + n) * 2 + qp) * EPQ + e;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) pw_kernel(PwParams p) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const long long vt = blockIdx.x / p.nnb;
+  const int nb = blockIdx.x % p.nnb;
+  const long long row0 = vt * 256 + wv * 64;       // this wave's first voxel row (over B * V)
+  const int n0 = nb * 128;
+  const int col = lane & 31, kg = lane >> 5;       // MFMA operand lane: column / row 0..31, K half
+  const T* w = reinterpret_cast<const T*>(p.w);
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[j][m][i] = 0.f;
+
+  // operand sources of K step s (16 channels): B = voxel row (row0 + 32 j + col),
+  // channels 16 s + 8 kg .. +8; A = output channel n0 + 32 m + col, same channels
+  auto ldB = [&](int s, int j) -> u32x4 {
+    const long long r = row0 + 32 * j + col;
+    const int k = 16 * s + 8 * kg;
+    if (r >= p.rows) return u32x4{0u, 0u, 0u, 0u};
+    const T* src = k < p.K0 ? reinterpret_cast<const T*>(p.b0) + r * p.K0 + k
+                            : reinterpret_cast<const T*>(p.b1) + r * (p.K - p.K0) + (k - p.K0);
+    return *reinterpret_cast<const u32x4*>(src);
+  };
+  auto ldA = [&](int s, int m) -> u32x4 {
+    const int co = n0 + 32 * m + col;
+    if (co >= p.N) return u32x4{0u, 0u, 0u, 0u};
+    return *reinterpret_cast<const u32x4*>(w + pw_widx<T>(co, 16 * s + 8 * kg, p.K, p.NT));
+  };
+  const int ns = p.K / 16;
+  u32x4 a[4], b[2], an[4], bn[2];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) a[m] = ldA(0, m);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b[j] = ldB(0, j);
+  for (int s = 0; s < ns; ++s) {
+    if (s + 1 < ns) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) an[m] = ldA(s + 1, m);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bn[j] = ldB(s + 1, j);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) mfma_acc(acc[j][m], a[m], b[j], (T*)nullptr);
+    if (s + 1 < ns) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) a[m] = an[m];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = bn[j];
+    }
+  }
+  // epilogue: acc[j][m][i] = channel n0 + 32 m + 8 (i >> 2) + 4 kg + (i & 3) of voxel row row0 + 32 j + col
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const long long r = row0 + 32 * j + col;
+    if (r >= p.rows) continue;
+    const int bb = (int)(r / p.V);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = n0 + 32 * m + 8 * g + 4 * kg;   // 4 consecutive channels c .. c+3
+        if (c >= p.N) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e] = acc[j][m][4 * g + e] + (p.bias ? p.bias[(long long)bb * p.bias_bs + c + e] : 0.f);
+        T* o;
+        if (p.out1 && c >= p.out_c0) o = reinterpret_cast<T*>(p.out1) + r * (p.N - p.out_c0) + (c - p.out_c0);
+        else o = reinterpret_cast<T*>(p.out) + r * (p.out1 ? p.out_c0 : p.N) + c;
+        uint2 q;
+        if (p.accumulate) {
+          q = *reinterpret_cast<const uint2*>(o);
+          v[0] += lo2f<T>(q.x); v[1] += hi2f<T>(q.x);
+          v[2] += lo2f<T>(q.y); v[3] += hi2f<T>(q.y);
+        }
+        q.x = pack2<T>(v[0], v[1]);
+        q.y = pack2<T>(v[2], v[3]);
+        *reinterpret_cast<uint2*>(o) = q;
+      }
+  }
+}
+
+}  // namespace
+
+// shapes the pointwise kernel takes: a pure 1x1 (segment B only), 16-bit, no
+// residual / statistics, output in the compute dtype, channels in 16s
+bool pw_eligible(const cwdm_conv3d_desc* d) {
+  if (!dtype_half(d->dtype) || d->a_w || !d->b_w || d->res_mode >= 0 || d->stats || d->out_dtype != d->dtype)
+    return false;
+  const int K = d->b_c0 + d->b_c1;
+  if (K % 16 || d->b_c0 % 16 || d->cout % 8 || (d->out1 && d->out_c0 % 4)) return false;
+  return d->B * d->D * d->H * d->W < (1LL << 40);
+}
+
+int pw_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
+  PwParams p{};
+  p.V = d->D * d->H * d->W;
+  p.rows = d->B * p.V;
+  p.K = d->b_c0 + d->b_c1; p.K0 = d->b_c0;
+  p.b0 = d->b0; p.b1 = d->b1;
+  p.w = reinterpret_cast<const unsigned char*>(d->b_w);
+  p.N = d->cout;
+  p.NT = 32 * pick_nf(d->cout);   // the packed layout's rows per channel tile (cwdm_conv3d_pack)
+  p.bias = d->bias; p.bias_bs = d->bias_bstride;
+  p.out = d->out; p.out1 = d->out1; p.out_c0 = d->out_c0; p.accumulate = d->accumulate;
+  p.nnb = (int)ceil_div(d->cout, 128);
+  const long long nblk = ceil_div(p.rows, 256) * p.nnb;
+  CWDM_REQUIRE(nblk < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d (pointwise): grid too large");
+  prof_begin(s);
+  if (d->dtype == CWDM_F16) hipLaunchKernelGGL(pw_kernel<f16_t>, dim3((unsigned)nblk), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(pw_kernel<bf16_t>, dim3((unsigned)nblk), dim3(256), 0, s, p);
+  prof_end(s, 2.0 * p.rows * (double)p.N * p.K);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+}  // namespace cwdm

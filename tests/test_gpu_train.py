@@ -180,13 +180,17 @@ def test_conv3d_dgrad_packing_vs_torch(cfg, dtype_name):
 
 
 @pytest.mark.parametrize("dtype_name", ["fp32", "bf16", "fp16"])
-def test_conv3d_b_only_dual_output_accumulate(dtype_name):
-    """1x1 skip dgrad: B-only conv writing channel slices to two buffers, accumulating."""
+@pytest.mark.parametrize("shape", [(1, (4, 8, 16), 32, 40, 56), (2, (4, 4, 40), 64, 24, 48),
+                                   (1, (4, 4, 64), 128, 128, 64), (1, (3, 5, 7), 16, 8, 24)])
+def test_conv3d_b_only_dual_output_accumulate(shape, dtype_name):
+    """1x1 skip dgrad: B-only conv writing channel slices to two buffers,
+    accumulating (16-bit: the pointwise MFMA kernel, pointwise.hip; partial
+    channel and voxel blocks, batch 2, odd grids)."""
     from cwdm_hip import _lib
     from cwdm_hip._lib import check, lib
     dtype, tdt = _dt(dtype_name)
     g = torch.Generator().manual_seed(8)
-    B, grid, cout, c0, c1 = 1, (4, 8, 16), 32, 40, 56
+    B, grid, cout, c0, c1 = shape
     cin = c0 + c1
     w = (torch.randn(cout, cin, 1, 1, 1, generator=g) / math.sqrt(cin)).to(tdt).float()
     dy = torch.randn(B, cout, *grid, generator=g).to(tdt).float()
@@ -212,6 +216,38 @@ def test_conv3d_b_only_dual_output_accumulate(dtype_name):
     got = torch.cat([o0.float().cpu() - base0.float(), o1.float().cpu() - base1.float()], -1)
     tol = 2e-5 if dtype_name == "fp32" else 3e-2
     assert rel_err(_nc(got), ref) < tol
+
+
+@pytest.mark.parametrize("dtype_name", ["bf16", "fp16"])
+def test_conv3d_pointwise_two_sources_bias_vs_torch(dtype_name):
+    """A pure 1x1 conv of a concatenated input (two channels-last sources) with
+    a per-batch bias, the forward skip product's shape: pointwise kernel vs F.conv3d."""
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import check, lib
+    dtype, tdt = _dt(dtype_name)
+    g = torch.Generator().manual_seed(9)
+    B, grid, k0, k1, cout = 2, (4, 6, 36), 48, 16, 96
+    x = torch.randn(B, k0 + k1, *grid, generator=g).to(tdt).float()
+    w = (torch.randn(cout, k0 + k1, 1, 1, 1, generator=g) / 8).to(tdt).float()
+    bias = torch.randn(B, cout, generator=g)
+    ref = F.conv3d(x, w) + bias[:, :, None, None, None]
+    L = lib()
+    pk = torch.empty(L.cwdm_conv3d_packed_bytes(cout, k0 + k1, 1, dtype), dtype=torch.uint8, device=DEV)
+    wd = w.to(DEV).contiguous()
+    check(L.cwdm_conv3d_pack(ctypes.c_void_p(wd.data_ptr()), cout, k0 + k1, 1, dtype,
+                             ctypes.c_void_p(pk.data_ptr()), None))
+    xd = _nd(x).to(DEV, tdt)
+    x0, x1 = xd[..., :k0].contiguous(), xd[..., k0:].contiguous()
+    bd = bias.to(DEV).contiguous()
+    out = torch.empty(B, *grid, cout, device=DEV, dtype=tdt)
+    d = _lib.ConvDesc()
+    d.dtype, d.B, (d.D, d.H, d.W), d.cout = dtype, B, grid, cout
+    d.b0, d.b_c0, d.b1, d.b_c1, d.b_w = x0.data_ptr(), k0, x1.data_ptr(), k1, pk.data_ptr()
+    d.bias, d.bias_bstride = bd.data_ptr(), cout
+    d.res_mode = -1
+    d.out, d.out_dtype = out.data_ptr(), dtype
+    check(L.cwdm_conv3d_forward(ctypes.byref(d), None))
+    assert rel_err(_nc(out.float().cpu()), ref) < {"bf16": 2e-2, "fp16": 3e-3}[dtype_name]
 
 
 # --------------------------------------------------------------------------- GN/SiLU backward

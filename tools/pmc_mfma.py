@@ -3,7 +3,7 @@ from a rocprofv3 PMC pass (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE, ...).
 
 clock = GRBM_GUI_ACTIVE / 8 XCDs / wall (MI355X_MICROARCH.md 'DVFS give-back');
 mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8) / (256 CUs x 4 SIMDs)
-(fraction of SIMD-cycles with the matrix core busy).  usage: pmc_mfma.py DIR"""
+(fraction of SIMD-cycles with the matrix core busy).  usage: pmc_mfma.py DIR [OUT]"""
 import collections
 import csv
 import glob
@@ -21,8 +21,14 @@ def main():
         d[k][r["Counter_Name"]] = float(r["Counter_Value"])
         meta[k] = (r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
     ks = sorted(d)
-    idx = [k for k in ks if "sampler_kernel" in meta[k][0]]
-    a, b = idx[-2], idx[-1]
+    # the last complete bf16 step: time-embedding launch to the next (the
+    # sampler epilogue may live in the output head; an fp16 side leg may follow)
+    idx = [k for k in ks if "time_embed_kernel" in meta[k][0]]
+    pairs = [(a, b) for a, b in zip(idx[:-1], idx[1:])
+             if any("conv3d_v4_kernel<unsigned short" in meta[k][0] for k in ks if a <= k < b)]
+    a, b = pairs[-2] if len(pairs) > 1 else pairs[-1]   # not the last: side-leg setup may follow it
+    a -= 1   # (the window below is a < k <= b: shift it to a <= k < b)
+    b -= 1
     print(f"{'us':>8} {'GHz':>5} {'mfma_busy':>9}  kernel")
     tot_w = tot_busy = tot_cyc = 0.0
     for k in ks:

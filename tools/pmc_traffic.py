@@ -7,8 +7,8 @@ so read bytes = 2 x FETCH_SIZE; WRITE_SIZE (KB) is exact for 16-B stores.
 
 The "dominant kernel" of bench.py's roofline is every launch bracketed by the
 plan's per-conv events (conv kernels, their GroupNorm/skip pre-passes, split-K
-sums/reduces, the output head).  The step is the last complete one between two
-sampler launches.
+sums/reduces, the output head, which also runs the fused sampler epilogue).
+The step is the last complete bf16 one between two time-embedding launches.
 
 usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON
 """
@@ -22,13 +22,19 @@ CONV_FAMILY = ("conv3d_v4_kernel", "conv3d_sg_kernel", "conv3d_kernel", "conv3d_
 
 
 def last_step(d, counter):
+    """The last complete bf16 step: from one time-embedding launch (the first of
+    every U-Net forward) to the next, whose convs are the bf16 ones (bench.py
+    may run an fp16 side leg after the headline loop)."""
     rows = []
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         rows += [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    idx = [i for i, r in enumerate(rows) if "sampler_kernel" in r["Kernel_Name"]]
-    a, b = idx[-2], idx[-1]
-    return rows[a + 1:b + 1]
+    idx = [i for i, r in enumerate(rows) if "time_embed_kernel" in r["Kernel_Name"]]
+    steps = [rows[a:b] for a, b in zip(idx[:-1], idx[1:])
+             if any("conv3d_v4_kernel<unsigned short" in r["Kernel_Name"] for r in rows[a:b])]
+    if steps:
+        return steps[-2] if len(steps) > 1 else steps[-1]   # not the last: side-leg setup may follow it
+    raise SystemExit("no complete bf16 step in " + d)
 
 
 def short(name):

@@ -1,6 +1,6 @@
 """Per-launch timeline of one denoising step from a rocprofv3 kernel trace of
 bench.py (a complete step: from one time-embedding launch to the next).
-usage: python tools/trace_step.py gpurun_out/TAG/trace [--agg] [--last]"""
+usage: python tools/trace_step.py gpurun_out/TAG/trace [--agg] [--last] [--back=N]"""
 import csv
 import glob
 import os
@@ -30,7 +30,16 @@ def main():
     if "--last" in sys.argv:
         step = rows[marks[-1]:]
     else:
-        step = rows[marks[-3]:marks[-2]]
+        # the second-to-last complete step of the bf16 headline loop (a side leg,
+        # e.g. the fp16 model, may follow it)
+        steps = [(a, b) for a, b in zip(marks[:-1], marks[1:])
+                 if any("conv3d_v4_kernel<unsigned short" in r["Kernel_Name"] for r in rows[a:b])]
+        back = 2
+        for arg in sys.argv:
+            if arg.startswith("--back="):
+                back = int(arg.split("=")[1])   # which step from the end (2: the one before the last)
+        a, b = steps[-back] if len(steps) >= back else steps[-1]
+        step = rows[a:b]
     tot = 0.0
     agg = defaultdict(lambda: [0, 0.0])
     for i, r in enumerate(step):
