@@ -551,7 +551,9 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
   const int mc = d->cout > 32 ? 2 : 1;
   p.nco = (int)ceil_div(d->cout, 32 * mc);
   const long long tiles = (long long)p.nco * (cin / 32);
-  long long S = ceil_div(256, tiles);
+  // one workgroup per CU (LDS / 224 accumulators): S brick ranges x tiles <= 256,
+  // else the last few workgroups run as a second round (cin 192: 43 x 6 = 258 ran 2x long)
+  long long S = 256 / tiles;
   if (S > p.nbricks) S = p.nbricks;
   if (S < 1) S = 1;
   p.per = ceil_div(p.nbricks, S);

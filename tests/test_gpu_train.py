@@ -191,6 +191,8 @@ def test_conv3d_b_only_dual_output_accumulate(shape, dtype_name):
     dtype, tdt = _dt(dtype_name)
     g = torch.Generator().manual_seed(8)
     B, grid, cout, c0, c1 = shape
+    if dtype_name == "fp32" and (c0 + c1) % 32 and c0 + c1 > 32:
+        pytest.skip("fp32 brick kernels: output channels a multiple of 32 or below 32")
     cin = c0 + c1
     w = (torch.randn(cout, cin, 1, 1, 1, generator=g) / math.sqrt(cin)).to(tdt).float()
     dy = torch.randn(B, cout, *grid, generator=g).to(tdt).float()
