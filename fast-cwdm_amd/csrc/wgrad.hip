@@ -312,6 +312,7 @@ struct WgDmaParams {
   int tx, ty, tz;
   long long nbricks, per;
   int nco, cin, cout, dy_cs;
+  int units, upx;              // (brick range, channel tile) units; units per XCD
   const unsigned char* act; long long act_bs;  // per-batch bytes of U (cin * SV * esz)
   const unsigned char* dy; long long dy_bs;    // per-batch bytes of dY (V * dy_cs * esz)
   float* dw;
@@ -346,14 +347,18 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   // XCD-aware map of the 1-D grid: workgroups are dealt to the 8 XCDs round
-  // robin, so the k-th workgroup of XCD j gets brick range x = j + 8 (k / tiles)
-  // and channel tile k % tiles -- every channel tile of a brick range runs on
-  // one XCD and the range's dY rows (and halo) are fetched into one L2, not
-  // into up to 8 (cin 192: 1.7x the time per flop with the plain 2-D grid)
+  // robin, so the k-th workgroup of XCD j takes unit j * upx + k of the
+  // range-major (brick range, channel tile) list -- the channel tiles of a
+  // brick range run on one XCD (two at a seam) and the range's dY rows (and
+  // halo) are fetched into one L2, not into up to 8 (cin 192: 1.7x the time
+  // per flop with the plain 2-D grid); upx <= 32 keeps every XCD to one round
+  // of its 32 CUs (ranges dealt j + 8 k put 36 on XCD 0 at cin 192: 2.5x)
   const int ntiles = p.nco * (p.cin / 32);
   const int xj = (int)(blockIdx.x & 7), xk = (int)(blockIdx.x >> 3);
-  const long long sx = xj + 8LL * (xk / ntiles);
-  const int tile = xk % ntiles;
+  const int u = xj * p.upx + xk;
+  if (xk >= p.upx || u >= p.units) return;
+  const long long sx = u / ntiles;
+  const int tile = u % ntiles;
   if (sx * p.per >= p.nbricks) return;
   const int ct = tile % p.nco, it = tile / p.nco;
   const int co0 = ct * C::CO, ci0 = it * 32;
@@ -494,13 +499,13 @@ int dispatch_wg(const WgradParams& p, int mode, bool gn, dim3 grid, hipStream_t 
 }
 
 template <typename T, int MC, int MODE>
-int launch_wg_dma(const WgDmaParams& p, dim3 grid, hipStream_t s) {
+int launch_wg_dma(const WgDmaParams& p, dim3, hipStream_t s) {
   constexpr int smem = 2 * WgCfg<T, MC>::SMEM;
   static_assert(smem <= 160 * 1024, "wgrad DMA LDS");
   auto k = wgrad_dma_kernel<T, MC, MODE>;
   CWDM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, smem));
-  // 1-D: brick ranges (grid.x, rounded up to the 8 XCDs) x channel tiles (grid.y)
-  const long long n = (grid.x + 7) / 8 * 8 * (long long)grid.y;
+  // 1-D: 8 XCDs x upx units of (brick range grid.x, channel tile grid.y)
+  const long long n = 8LL * p.upx;
   CWDM_REQUIRE(n < (1LL << 31), CWDM_E_UNSUPPORTED, "cwdm_conv3d_wgrad: grid too large");
   hipLaunchKernelGGL(k, dim3((unsigned)n), dim3(256), smem, s, p);
   CWDM_LAUNCHED();
@@ -574,6 +579,7 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
     q.SD = d->u_mode == 1 ? q.D / 2 : q.D; q.SH = d->u_mode == 1 ? q.H / 2 : q.H; q.SW = d->u_mode == 1 ? q.W / 2 : q.W;
     q.tx = p.tx; q.ty = p.ty; q.tz = p.tz; q.nbricks = p.nbricks; q.per = p.per; q.nco = p.nco;
     q.cin = cin; q.cout = d->cout; q.dy_cs = d->dy_cs;
+    q.units = (int)(S * tiles); q.upx = (q.units + 7) / 8;
     const long long sv = (long long)q.SD * q.SH * q.SW, V = d->D * d->H * d->W;
     q.act = reinterpret_cast<const unsigned char*>(d->u0); q.act_bs = sv * cin * 2;
     q.dy = reinterpret_cast<const unsigned char*>(d->dy); q.dy_bs = V * d->dy_cs * 2;
