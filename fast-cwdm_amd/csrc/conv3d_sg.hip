@@ -106,6 +106,14 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  V4_STAMP(0);
+#ifdef CWDM_CONV_STAMPS
+  if (p.stamps && tid == 0) {
+    p.stamps[(long long)blockIdx.x * 24 + 20] = __builtin_amdgcn_s_memrealtime();
+    p.stamps[(long long)blockIdx.x * 24 + 22] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+    p.stamps[(long long)blockIdx.x * 24 + 23] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // XCC_ID
+  }
+#endif
 
   // work item -> (batch, brick, 16-channel tile); channel tile fastest (the 16
   // workgroups of a brick share its halo in L2)
@@ -192,6 +200,7 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   issue_w(cb0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  V4_STAMP(1);
   for (int c = cb0; c < cb1; ++c) {
     const bool has_next = c + 1 < cb1;
     const int buf = (c - cb0) & 1;
@@ -243,7 +252,9 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
+    if (c - cb0 < 8) V4_STAMP(4 + c - cb0);
   }
+  V4_STAMP(12);
 
   if (q.ksplit > 1) {
     // K split: publish this slice, the tile's last arrival finishes it.  Hand-off
@@ -268,7 +279,14 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
     if (tid == 0)
       *flag = __hip_atomic_fetch_add(&q.count[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    if (*flag != (unsigned)(q.ksplit - 1)) return;
+    V4_STAMP(13);
+    if (*flag != (unsigned)(q.ksplit - 1)) {
+      V4_STAMP(15);
+#ifdef CWDM_CONV_STAMPS
+      if (p.stamps && tid == 0) p.stamps[(long long)blockIdx.x * 24 + 21] = __builtin_amdgcn_s_memrealtime();
+#endif
+      return;
+    }
     if (tid == 0) __hip_atomic_store(&q.count[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     float bi[4];
 #pragma unroll
@@ -281,6 +299,7 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
                                   __builtin_amdgcn_raw_buffer_load_b128(prs, (unsigned)k * 16384u + lofs + m * 1024u, 0, 16));
       acc[m] = sum + sg_f32x4{bi[0], bi[1], bi[2], bi[3]};
     }
+    V4_STAMP(14);
   }
 
   // epilogue: lane (l16, kq) of operand m holds channels t16 16 + 4 kq + i of
@@ -359,6 +378,10 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
       p.stats[pidx * 2 + 1] = s2;
     }
   }
+  V4_STAMP(15);
+#ifdef CWDM_CONV_STAMPS
+  if (p.stamps && tid == 0) p.stamps[(long long)blockIdx.x * 24 + 21] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 template __global__ void conv3d_sg_kernel<bf16_t, 16, 4, 0, 27>(SGParams);

@@ -32,6 +32,10 @@ CASES = {
     "L1_128_128_gn": (64, 128, 0, 128, 0, True, 0, -1),
     "L1_128_128_nogn": (64, 128, 0, 128, 0, False, 0, -1),
     "L2_128_128_gn": (32, 128, 0, 128, 0, True, 0, -1),
+    "L3_256_256_gn": (16, 256, 0, 256, 0, True, 0, -1),
+    "L3_256_256_res": (16, 256, 0, 256, 0, False, 0, 0),
+    "L4_256_256_gn": (8, 256, 0, 256, 0, True, 0, -1),
+    "L4_256_256_nogn": (8, 256, 0, 256, 0, False, 0, -1),
 }
 
 
