@@ -151,4 +151,14 @@ struct PackJob {
   long long blk0;
 };
 static_assert(sizeof(PackJob) == 64, "PackJob layout");
+
+// host side of the fused GroupNorm backward reduce (see V4Params::gx0): the
+// plan fills it before a dgrad conv and reads back used / nblk
+struct GbwdFuse {
+  const void* x0; const void* x1; int c0;   // the GroupNorm input (channels-last; x1: channels [c0, C))
+  const float* ss; const float* mr; int groups;
+  float* part; long long part_bytes;        // [B][nblk][C][2] partials out
+  bool used; int nblk;
+};
+extern thread_local GbwdFuse* g_gbwd;
 }  // namespace cwdm

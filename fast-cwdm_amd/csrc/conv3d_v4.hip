@@ -13,12 +13,16 @@ namespace cwdm {
 
 template __global__ void conv3d_v4_kernel<bf16_t, 0, true>(V4Params);
 template __global__ void conv3d_v4_kernel<bf16_t, 0, true, true>(V4Params);
+template __global__ void conv3d_v4_kernel<bf16_t, 0, true, false, true>(V4Params);
+template __global__ void conv3d_v4_kernel<bf16_t, 0, true, true, true>(V4Params);
 template __global__ void conv3d_v4_kernel<bf16_t, 1, true, true>(V4Params);
 template __global__ void conv3d_v4_kernel<bf16_t, 1, true>(V4Params);
 template __global__ void conv3d_v4_kernel<bf16_t, 0, false>(V4Params);
 template __global__ void conv3d_v4_kernel<bf16_t, 1, false>(V4Params);
 template __global__ void conv3d_v4_kernel<f16_t, 0, true>(V4Params);
 template __global__ void conv3d_v4_kernel<f16_t, 0, true, true>(V4Params);
+template __global__ void conv3d_v4_kernel<f16_t, 0, true, false, true>(V4Params);
+template __global__ void conv3d_v4_kernel<f16_t, 0, true, true, true>(V4Params);
 template __global__ void conv3d_v4_kernel<f16_t, 1, true, true>(V4Params);
 template __global__ void conv3d_v4_kernel<f16_t, 1, true>(V4Params);
 template __global__ void conv3d_v4_kernel<f16_t, 0, false>(V4Params);
@@ -192,6 +196,11 @@ int64_t v4_workspace_bytes(const cwdm_conv3d_desc* d) {
 
 int legacy_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream);
 
+// the U-Net plan's backward: fuse the reduce pass of the SiLU(GroupNorm)
+// backward that follows this dgrad conv into its epilogue (GbwdFuse, conv3d_v4.hpp
+// V4Params::gx0); taken only by the 16-bit fast epilogue without K split
+thread_local GbwdFuse* g_gbwd = nullptr;
+
 int gn_apply(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
              void* out, hipStream_t s, int cm = 0) {
   constexpr int VPT = 4;
@@ -279,7 +288,10 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   prof_begin(s);
   auto launch16 = [&](auto tag) {
     using T = decltype(tag);
-    if (ct32) {
+    if (p.gx0) {   // fused GroupNorm-backward reduce (dgrad, same-grid source: amode 0)
+      if (ct32) hipLaunchKernelGGL((conv3d_v4_kernel<T, 0, true, true, true>), grid, dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((conv3d_v4_kernel<T, 0, true, false, true>), grid, dim3(256), 0, s, p);
+    } else if (ct32) {
       if (p.amode == 1) hipLaunchKernelGGL((conv3d_v4_kernel<T, 1, true, true>), grid, dim3(256), 0, s, p);
       else hipLaunchKernelGGL((conv3d_v4_kernel<T, 0, true, true>), grid, dim3(256), 0, s, p);
     } else if (fast) {
@@ -290,6 +302,27 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
       else hipLaunchKernelGGL((conv3d_v4_kernel<T, 0, false>), grid, dim3(256), 0, s, p);
     }
   };
+  // (only where the conv leaves VALU room: at 128^3 the epilogue's ~13 VALU + 2
+  // transcendentals per output element cost the MFMA-bound kernel more (+30 %)
+  // than the separate reduce pass it saves; at 64^3 / 32^3 it is a net win --
+  // same-box kernel traces, DESIGN.md §3b.  Env CWDM_GBWD_MAXW, default 64)
+  static const int gb_maxw = [] { const char* e = std::getenv("CWDM_GBWD_MAXW"); return e ? std::atoi(e) : 64; }();
+  if (g_gbwd && !g_gbwd->used && dtype_half(d->dtype) && (ct32 || fast) && S == 1 && rmode < 0 && !p.stats &&
+      p.amode == 0 && p.W <= gb_maxw) {
+    GbwdFuse& g = *g_gbwd;
+    const int nc = ct32 ? 32 : 64;
+    const int C = d->cout;
+    const long long need = (long long)p.B * p.tx * p.ty * p.tz * C * 8;
+    if (g.groups > 0 && C % g.groups == 0 && C / g.groups >= 2 && g.c0 % nc == 0 && g.c0 <= C &&
+        (g.c0 == C || g.x1) && need <= g.part_bytes) {
+      p.gx0 = g.x0; p.gx1 = g.x1; p.gc0 = g.c0;
+      p.gss = g.ss; p.gmr = g.mr; p.ggroups = g.groups;
+      p.gdiv = make_fastdiv((unsigned)(C / g.groups));
+      p.stats = g.part;
+      g.used = true;
+      g.nblk = p.tx * p.ty * p.tz;
+    }
+  }
   if (d->dtype == CWDM_BF16) {
     launch16(bf16_t{});
   } else if (d->dtype == CWDM_F16) {

@@ -66,7 +66,19 @@ struct V4Params {
   int ksplit, kper;
   long long ks_stride;
   unsigned long long* stamps;  // diagnostics: per-workgroup s_memtime stamps (cwdm_debug_conv_stamps), else null
+  // Fused reduce pass of the SiLU(GroupNorm) backward (training: the dgrad conv
+  // whose output du feeds gn_silu_bwd at the same grid; cwdm::GbwdFuse).  With
+  // gx0 set the 16-bit fast epilogue stores du as usual and, instead of the
+  // forward statistics, writes per-(tile, channel) partials (sum dz, sum dz xhat)
+  // to stats (the [B][tiles][C][2] layout gn_bwd_finalize reads):
+  // dz = du SiLU'(x sc + sh), xhat = (x - mu) rs, du as stored (rounded).  x =
+  // the GroupNorm input (gx0: channels [0, gc0), gx1: the rest; channels-last);
+  // gss = its [B][C][2] scale / shift, gmr = [B][G][2] mean / rstd, gdiv = C / G.
+  const void* gx0; const void* gx1; int gc0;
+  const float* gss; const float* gmr; int ggroups;
+  FastDiv gdiv;
 };
+
 
 __device__ unsigned g_v4_cu_arrivals[8 * 256];
 struct V4Cfg {
@@ -77,8 +89,13 @@ struct V4Cfg {
   static constexpr int SMEM = 2 * HALO_B;                            // double-buffered halo: 80 KB
   // unused padding slots 1224..1279 of quad plane k & 1 of halo buffer k >> 1
   // (896 B each; the halo DMA never writes them): statistics scratch of wave k
-  // and, in region 0 at +256, the bias of the next tile
+  // and, in region 0 at +256, the bias of the next tile; fused GroupNorm
+  // backward (gx0): the tile's scale / shift rows (64 channels x 8 B) in region
+  // 1 + 2 s at +256 and its groups' mean / rstd in region 2 at +256 + 256 s,
+  // double-buffered by tile parity s (the next tile's land before this epilogue)
   static constexpr int pad(int k) { return (k >> 1) * HALO_B + (k & 1) * HVP * 16 + HV * 16; }
+  static constexpr int gss_off(int s) { return pad(1 + 2 * s) + 256; }
+  static constexpr int gmr_off(int s) { return pad(2) + 256 + 256 * s; }
 };
 
 template <typename T>
@@ -137,9 +154,10 @@ __device__ __forceinline__ void v4_read_step(u32x4 (&av)[6], const unsigned char
 // CT32: 32-channel tiles (ct counts 32-channel tiles; wave wv = z-plane wv, one
 // plane per wave); else 64-channel tiles, wave = (32-channel half wv & 1, plane
 // pair wv >> 1)
-template <typename T, bool FAST, bool CT32 = false>
+template <typename T, bool FAST, bool CT32 = false, bool GB = false>
 __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][4], int b, int sl, int ct, int x0,
-                                            int y0, int z0, int ks, int tid, int wv, unsigned char* smem) {
+                                            int y0, int z0, int ks, int tid, int wv, unsigned char* smem,
+                                            int gslot = 0) {
   constexpr int NPL = CT32 ? 1 : 2;
   using T16 = std::conditional_t<sizeof(T) == 2, T, bf16_t>;   // the 16-bit storage type (bf16 / fp16)
   const int lane = tid & 63, lr = lane & 31, hh = lane >> 5;
@@ -235,7 +253,75 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
         }
       }
     };
-    if (p.rmode >= 0) run(std::true_type{});
+    // fused GroupNorm backward reduce (no residual: a dgrad conv).  Phase 1 stores
+    // du and keeps it, packed and swapped (8 consecutive channels per lane, 64
+    // registers), while the 128 accumulators die; phase 2 walks the same rows of
+    // x with the same layout -- so the sums need no swaps and the kernel stays
+    // inside its 256 registers (taking the sums from the accumulators spilled).
+    // GB sums: ssum / ssq [8 jj + k] = channel c0w + 16 jj + 8 hh + k.
+    auto run_gb = [&]() {
+      u32x4 du16[NPL][4][2];
+#pragma unroll
+      for (int pl = 0; pl < NPL; ++pl)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const unsigned oo = obase + (unsigned)pl * planeb + (unsigned)m * rowb;
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = acc[pl][m][8 * jj + k];
+            const unsigned p0 = pack2<T16>(v[0], v[1]), p1 = pack2<T16>(v[2], v[3]);
+            const unsigned p2 = pack2<T16>(v[4], v[5]), p3 = pack2<T16>(v[6], v[7]);
+            const auto t0 = __builtin_amdgcn_permlane32_swap(p0, p2, false, false);
+            const auto t1 = __builtin_amdgcn_permlane32_swap(p1, p3, false, false);
+            u32x4 w;
+            w[0] = t0[0]; w[1] = t1[0]; w[2] = t0[1]; w[3] = t1[1];
+            __builtin_amdgcn_raw_buffer_store_b128(w, ro, xin ? oo + 32u * jj : 0xFFFFFFF0u, 0, 0);
+            du16[pl][m][jj] = w;
+          }
+        }
+      const int tb = CT32 ? ct * 32 : ct * 64;                 // the tile's first channel
+      const float* cf = reinterpret_cast<const float*>(smem + V4Cfg::gss_off(gslot));   // [c - tb][sc, sh]
+      const bool first = tb < p.gc0;                           // one source per tile (host-checked)
+      const int xc = first ? p.gc0 : p.cout - p.gc0, xco = first ? 0 : p.gc0;
+      const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(reinterpret_cast<const T16*>(first ? p.gx0 : p.gx1) + (long long)b * V * xc), (short)0,
+          (int)(V * xc * 2), 0x00020000);
+      const unsigned xrowb = (unsigned)p.W * (unsigned)xc * 2u, xplaneb = (unsigned)HW * (unsigned)xc * 2u;
+      const unsigned xbase = vb0 * (unsigned)xc * 2u + (unsigned)(cl - xco) * 2u;
+      const int lc0 = cl - tb;   // the lane's first channel within the tile
+#pragma unroll
+      for (int pl = 0; pl < NPL; ++pl) {
+        u32x4 xq[4][2];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            xq[m][jj] = __builtin_amdgcn_raw_buffer_load_b128(
+                rx, xin ? xbase + (unsigned)pl * xplaneb + (unsigned)m * xrowb + 32u * jj : 0xFFFFFFF0u, 0, 0);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const u32x4 dq = du16[pl][m][jj], xqq = xq[m][jj];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const unsigned dw = dq[k >> 1], xw = xqq[k >> 1];
+              const float du = (k & 1) ? hi2f<T16>(dw) : lo2f<T16>(dw);
+              const float xv = (k & 1) ? hi2f<T16>(xw) : lo2f<T16>(xw);
+              const float2 scsh = *reinterpret_cast<const float2*>(cf + 2 * (lc0 + 16 * jj + k));
+              const float z = xv * scsh.x + scsh.y;
+              const float s = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
+              const float dz = du * (s * (1.0f + z * (1.0f - s))) * xm;
+              ssum[8 * jj + k] += dz;
+              ssq[8 * jj + k] += dz * xv;   // sum dz x; the tile's sum dz xhat = rs (sum dz x - mu sum dz), below
+            }
+          }
+      }
+    };
+    if constexpr (GB) run_gb();
+    else if (p.rmode >= 0) run(std::true_type{});
     else run(std::false_type{});
   } else {
 #pragma unroll
@@ -323,8 +409,11 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (CT32 ? tid < 32 : tid < 64) {
-      const int ff = tid >> 5, c32 = tid & 31, j = c32 >> 3, h2 = (c32 >> 2) & 1, k = c32 & 3;
-      const int i = 4 * j + k;
+      const int ff = tid >> 5, c32 = tid & 31;
+      // channel c32 of the wave's slice: accumulator layout (i = 4 j + k, half h2 ->
+      // 8 j + 4 h2 + k), or GB's swapped layout (i = 8 jj + k -> 16 jj + 8 h2 + k)
+      const int h2 = GB ? (c32 >> 3) & 1 : (c32 >> 2) & 1;
+      const int i = GB ? 8 * (c32 >> 4) + (c32 & 7) : 4 * (c32 >> 3) + (c32 & 3);
       const int tiles = p.tx * p.ty * p.tz;
       float su, sq;
       if constexpr (CT32) {  // the 4 plane waves hold the same 32 channels
@@ -342,6 +431,12 @@ __device__ __forceinline__ void v4_epilogue(const V4Params& p, f32x16 (&acc)[2][
         sq = R0[16 + i] + R1[16 + i];
       }
       const int c = (CT32 ? ct * 32 : ct * 64) + tid;
+      if constexpr (GB) {
+        // (sum dz, sum dz x) -> (sum dz, sum dz xhat) with xhat = (x - mu) rs of c's group
+        const float* gm = reinterpret_cast<const float*>(smem + V4Cfg::gmr_off(gslot));   // [g - glo][mu, rs]
+        const unsigned gi = fdiv((unsigned)c, p.gdiv) - fdiv((unsigned)(c - tid), p.gdiv);
+        sq = gm[2 * gi + 1] * (sq - gm[2 * gi] * su);
+      }
       const long long pidx = ((long long)b * tiles + sl) * p.cout + c;
       p.stats[pidx * 2 + 0] = su;
       p.stats[pidx * 2 + 1] = sq;
@@ -433,7 +528,8 @@ __device__ __forceinline__ void v4_issue_halo(const V4Params& p, const V4Tile& t
 // Persistent: gridDim.x <= the number of tiles; workgroup k runs tiles
 // k, k + gridDim.x, ... as one continuous chunk stream, so the next tile's halo,
 // weights and bias are prefetched under the current tile's last chunk.
-template <typename T, int MODE, bool FAST, bool CT32 = false>
+// GB: the dgrad instance with the fused GroupNorm-backward reduce (V4Params::gx0)
+template <typename T, int MODE, bool FAST, bool CT32 = false, bool GB = false>
 __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   static_assert(!FAST || sizeof(T) == 2, "the fast epilogue is 16-bit (bf16 / fp16) only");
   using C = V4Cfg;
@@ -502,6 +598,25 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
                                            p.bias + (long long)tt.b * p.bias_bs + tt.ct * (CT32 ? 32 : 64) + lane),
                                        (__attribute__((address_space(3))) void*)(smem + C::pad(0) + 256), 4, 0, 0);
   };
+  // fused GroupNorm backward: the tile's scale / shift and its groups' mean /
+  // rstd into slot s of the LDS padding (wave 1, 4-byte DMA per lane)
+  auto issue_gcoef = [&](const Tile& tt, int s) {
+    if (!GB || wv != 1) return;
+    const int nc = CT32 ? 32 : 64, tb = tt.ct * nc;
+    const float* gsrc = p.gss + ((long long)tt.b * p.cout + tb) * 2;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (64 * j + lane < 2 * nc)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(gsrc + 64 * j + lane),
+                                         (__attribute__((address_space(3))) void*)(smem + C::gss_off(s) + 256 * j), 4,
+                                         0, 0);
+    const unsigned glo = fdiv((unsigned)tb, p.gdiv), ghi = fdiv((unsigned)(tb + nc - 1), p.gdiv);
+    const int nf = 2 * (int)(ghi - glo + 1);   // <= 64 floats (the host requires C / G >= 2)
+    const float* msrc = p.gmr + ((long long)tt.b * p.ggroups + glo) * 2;
+    if (lane < nf)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(msrc + lane),
+                                       (__attribute__((address_space(3))) void*)(smem + C::gmr_off(s)), 4, 0, 0);
+  };
   // accumulators start at the bias of their output channel (i = 4 j + k -> channel 8 j + 4 hh + k)
   f32x16 acc[2][4];
   auto init_acc = [&](int ks) {
@@ -530,6 +645,7 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
   Tile cur = tile_of(0);
   u32x4 wr[3][3];
   issue_bias(cur);
+  issue_gcoef(cur, 0);
   issue_halo(cur, cur.c0, 0);
   load_w0(wr[0], cur.ct, cur.c0);
   int gch = 0;  // chunk counter of the stream (selects the halo buffer)
@@ -592,6 +708,7 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
         // which every wave finished before the previous barrier)
         const Tile nxt = tile_of(it + 1);
         issue_bias(nxt);
+        issue_gcoef(nxt, (it + 1) & 1);
         issue_halo(nxt, nxt.c0, (gch + 1) & 1);
       }
       if (it == 0 && c - cur.c0 < 8) V4_STAMP(4 + c - cur.c0);
@@ -603,10 +720,12 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
     Tile nxt = cur;
     if (more) {
       nxt = tile_of(it + 1);
-      load_w0(wr[0], nxt.ct, nxt.c0);
+      // (GB: after the epilogue -- its x rows and GroupNorm sums need the registers)
+      if constexpr (!GB) load_w0(wr[0], nxt.ct, nxt.c0);
     }
     // (K split: out is this slice's fp32 partial, see V4Params)
-    v4_epilogue<T, FAST, CT32>(p, acc, cur.b, cur.sl, cur.ct, cur.x0, cur.y0, cur.z0, cur.ks, tid, wv, smem);
+    v4_epilogue<T, FAST, CT32, GB>(p, acc, cur.b, cur.sl, cur.ct, cur.x0, cur.y0, cur.z0, cur.ks, tid, wv, smem, it & 1);
+    if constexpr (GB) if (more) load_w0(wr[0], nxt.ct, nxt.c0);
     if (it == 0) V4_STAMP(13);
     cur = nxt;
   }

@@ -418,6 +418,7 @@ __global__ void __launch_bounds__(256) channel_sum_kernel(const T* __restrict__ 
   for (int e = 0; e < 8; ++e) a[e] = 0.f;
   if (slot < nslots) {
     const long long v0 = blk * vpb, v1 = v0 + vpb < V ? v0 + vpb : V;
+#pragma unroll 4
     for (long long v = v0 + slot; v < v1; v += nslots) {
       float f[8];
       load8<T>(src + ((long long)b * V + v) * cs + cg * 8, f);
@@ -570,9 +571,13 @@ int dispatch_mode(int mode, F&& f) {
   return f(std::integral_constant<int, 2>{});
 }
 
+// voxel blocks of the reduce pass: one trip of 4 voxels per slot (256 / (C / 8)
+// voxel slots per workgroup) where that stays below 512 blocks -- the small
+// levels ran 1-8 workgroups looping over 512 voxels each (35-70 us per call at
+// 16^3 / 8^3, latency-bound) -- else 512 blocks
 long long gn_bwd_blocks(int C, long long V) {
-  (void)C;
-  long long nb = ceil_div(V, 512);
+  const long long slots = std::max(1, 256 / std::max(1, C / 8));
+  long long nb = ceil_div(V, 4 * slots);
   if (nb > 512) nb = 512;
   if (nb < 1) nb = 1;
   return nb;
@@ -606,7 +611,40 @@ int launch_temb_bwd(const float* t, int B, int mc, const float* w1, const float*
 int gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode, const float* ss,
                      const float* mr, const float* gamma, int groups, int64_t B, int64_t d, int64_t h, int64_t w,
                      int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma, float* dbeta, void* ws,
-                     int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream, int acc_affine);
+                     int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream, int acc_affine,
+                     const float* pre_part = nullptr, int pre_nblk = 0);
+// Fixed-order slice sums of [B][nblk][W2] partial rows -> [B][slices][W2]
+// (the fused GroupNorm-backward partials: one row per dgrad tile, 4096 at
+// 128^3, too many for the single-workgroup gn_bwd_finalize).  Workgroup (slice,
+// b); thread f sums column f over its rows in order, 8 loads in flight.
+__global__ void __launch_bounds__(256) gb_part_reduce_kernel(const float* __restrict__ in, int nblk, int W2, int per,
+                                                             float* __restrict__ out) {
+  const int sl = blockIdx.x, b = blockIdx.y, S = gridDim.x;
+  const int r0 = sl * per, r1 = min(nblk, r0 + per);
+  const float* base = in + (long long)b * nblk * W2;
+  for (int f = threadIdx.x; f < W2; f += 256) {
+    float acc = 0.f;
+    int r = r0;
+    for (; r + 8 <= r1; r += 8) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = base[(long long)(r + k) * W2 + f];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += v[k];
+    }
+    for (; r < r1; ++r) acc += base[(long long)r * W2 + f];
+    out[((long long)b * S + sl) * W2 + f] = acc;
+  }
+}
+
+int gb_part_reduce(const float* part, int nblk, int C, int64_t B, int slices, float* out, hipStream_t s) {
+  CWDM_REQUIRE(nblk > 0 && slices > 0 && B > 0 && B < 65536, CWDM_E_SHAPE, "gb_part_reduce: bad shape");
+  const int per = (int)ceil_div(nblk, slices);
+  hipLaunchKernelGGL(gb_part_reduce_kernel, dim3((unsigned)slices, (unsigned)B), dim3(256), 0, s, part, nblk, 2 * C,
+                     per, out);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
 }  // namespace cwdm
 
 using namespace cwdm;
@@ -626,7 +664,7 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
                            const float* ss, const float* mr, const float* gamma, int groups, int64_t B, int64_t d,
                            int64_t h, int64_t w, int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma,
                            float* dbeta, void* ws, int64_t ws_bytes, float* chs, int64_t chs_stride,
-                           cwdm_stream_t stream, int acc_affine) {
+                           cwdm_stream_t stream, int acc_affine, const float* pre_part, int pre_nblk) {
   CWDM_REQUIRE(!chs || (c1 == 0 && chs_stride >= c0), CWDM_E_UNSUPPORTED,
                "gn_silu_bwd: fused channel sums need one source");
   CWDM_REQUIRE(x0 && du && ss && mr && gamma && dx0 && dgamma && dbeta && ws, CWDM_E_INVALID,
@@ -653,7 +691,10 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
   float* chs_part = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(coef) + (B * (int64_t)C * 4 * 4 + 255) / 256 * 256);
   hipStream_t s = (hipStream_t)stream;
   int rc;
-  if ((rc = dispatch_mode(du_mode, [&](auto M) -> int {
+  // pre_part: the (sum dz, sum dz xhat) partials already written by the epilogue
+  // of the dgrad conv that produced du ([B][pre_nblk][C][2], cwdm::GbwdFuse)
+  CWDM_REQUIRE(!pre_part || (du_mode == 0 && pre_nblk > 0), CWDM_E_INVALID, "gn_silu_bwd: bad fused partials");
+  if (!pre_part && (rc = dispatch_mode(du_mode, [&](auto M) -> int {
          constexpr int MD = decltype(M)::value;
          dispatch_dtype(dtype, [&](auto tag) -> int {
            using T = decltype(tag);
@@ -666,8 +707,8 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
          return CWDM_OK;
        })))
     return rc;
-  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(512), 0, s, part, (int)nb, C, (int)B, gamma, mr, groups, V,
-                     coef, dgamma, dbeta, acc_affine);
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(512), 0, s, pre_part ? pre_part : part,
+                     pre_part ? pre_nblk : (int)nb, C, (int)B, gamma, mr, groups, V, coef, dgamma, dbeta, acc_affine);
   CWDM_LAUNCHED();
   // workgroups of (256 / ncg) voxels x ncg channel groups; two voxels per
   // thread (the kernel's UNR; du_mode 1 loops twice instead); with channel
@@ -736,15 +777,19 @@ extern "C" int cwdm_resample_add(void* dst, const void* src, int C, int64_t B, i
 }
 
 namespace {
-long long channel_sum_blocks(int64_t V) {
-  long long nb = ceil_div(V, 2048);
-  return nb > 512 ? 512 : nb;
+// voxel blocks: ~8 loads per voxel slot (256 / (C / 8) slots per workgroup),
+// at most 512 -- the small levels ran 1-2 workgroups over 2048 voxels each
+// (70 us per call at 16^3 x 256 channels, latency-bound)
+long long channel_sum_blocks(int64_t V, int C) {
+  const long long slots = std::max(1, 256 / std::max(1, (C + 7) / 8));
+  long long nb = ceil_div(V, 8 * slots);
+  return nb > 512 ? 512 : (nb < 1 ? 1 : nb);
 }
 }  // namespace
 
 extern "C" int64_t cwdm_channel_sum_workspace_bytes(int64_t B, int64_t V, int C) {
   if (B <= 0 || V <= 0 || C <= 0) return -1;
-  return B * channel_sum_blocks(V) * C * 4;
+  return B * channel_sum_blocks(V, C) * C * 4;
 }
 
 extern "C" int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V, int C, int cs, float* out_bc,
@@ -757,7 +802,7 @@ extern "C" int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V
   CWDM_REQUIRE(B > 0 && B < 65536 && V > 0, CWDM_E_SHAPE, "cwdm_channel_sum: empty input");
   CWDM_REQUIRE(!workspace || ws_bytes >= cwdm_channel_sum_workspace_bytes(B, V, C), CWDM_E_WORKSPACE,
                "cwdm_channel_sum: workspace too small");
-  const long long nb = channel_sum_blocks(V);
+  const long long nb = channel_sum_blocks(V, C);
   const long long vpb = ceil_div(V, nb);
   dim3 grid((unsigned)nb, (unsigned)B);
   hipStream_t s = (hipStream_t)stream;

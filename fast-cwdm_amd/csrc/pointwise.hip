@@ -11,9 +11,10 @@
 // (A = 32 output channels x 16 K of the packed weights, B = 16 K x 32 voxels
 // straight from the channels-last rows, 16 B per lane); the next K step's
 // fragments are loaded while this step's MFMAs run.  An accumulator lane holds
-// 4 runs of 4 consecutive channels of one voxel: 8-byte stores (and loads when
-// accumulating).  The brick kernels this replaces ran the R0 skip dgrads at
-// ~0.06 PF (690-910 us each, ~3 ms per training step).
+// 4 runs of 4 consecutive channels of one voxel; lane pairs (l, l + 32) swap
+// halves so the epilogue stores (and, accumulating, loads) 16 bytes = 8
+// channels per lane.  The brick kernels this replaces ran the R0 skip dgrads
+// at ~0.06 PF (690-910 us each, ~3 ms per training step).
 #include "conv3d_kernels.hpp"
 
 namespace cwdm {
@@ -98,35 +99,94 @@ __global__ void __launch_bounds__(256) pw_kernel(PwParams p) {
       for (int j = 0; j < 2; ++j) b[j] = bn[j];
     }
   }
-  // epilogue: acc[j][m][i] = channel n0 + 32 m + 8 (i >> 2) + 4 kg + (i & 3) of voxel row row0 + 32 j + col
+  // epilogue: acc[j][m][i] = channel n0 + 32 m + 8 (i >> 2) + 4 kg + (i & 3) of voxel row row0 + 32 j + col.
+  // Lanes l and l + 32 hold the two 4-channel halves of each 8-channel group:
+  // v_permlane32_swap over the group pairs (2 gg, 2 gg + 1) gives every lane 8
+  // consecutive channels, channel base n0 + 32 m + 16 gg + 8 kg -> 16-byte stores
+  // (the 8-byte stores scattered every instruction over 32 rows: the R0 skip
+  // dgrads ran at 1.5-2.2 TB/s).  The swaps run on every lane (no divergence
+  // around a cross-lane op); only the loads / stores are predicated.
+  const bool f8 = p.N % 8 == 0 && (!p.out1 || p.out_c0 % 8 == 0);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const long long r = row0 + 32 * j + col;
-    if (r >= p.rows) continue;
-    const int bb = (int)(r / p.V);
+    const bool rin = r < p.rows;
+    const int bb = rin ? (int)(r / p.V) : 0;
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < 4; ++m) {
+      if (f8) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c = n0 + 32 * m + 8 * g + 4 * kg;   // 4 consecutive channels c .. c+3
-        if (c >= p.N) continue;
-        float v[4];
+        for (int gg = 0; gg < 2; ++gg) {
+          // groups ga = 2 gg, gb = 2 gg + 1; in the accumulator layout this lane holds
+          // channels 8 g + 4 kg + e of both; after the swap, the 8 channels from c
+          const int ga = 2 * gg, gb = 2 * gg + 1;
+          const int c = n0 + 32 * m + 16 * gg + 8 * kg;
+          const bool ok = rin && c < p.N;
+          T* o = nullptr;
+          if (ok) {
+            if (p.out1 && c >= p.out_c0) o = reinterpret_cast<T*>(p.out1) + r * (p.N - p.out_c0) + (c - p.out_c0);
+            else o = reinterpret_cast<T*>(p.out) + r * (p.out1 ? p.out_c0 : p.N) + c;
+          }
+          float v[8];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          v[e] = acc[j][m][4 * g + e] + (p.bias ? p.bias[(long long)bb * p.bias_bs + c + e] : 0.f);
-        T* o;
-        if (p.out1 && c >= p.out_c0) o = reinterpret_cast<T*>(p.out1) + r * (p.N - p.out_c0) + (c - p.out_c0);
-        else o = reinterpret_cast<T*>(p.out) + r * (p.out1 ? p.out_c0 : p.N) + c;
-        uint2 q;
-        if (p.accumulate) {
-          q = *reinterpret_cast<const uint2*>(o);
-          v[0] += lo2f<T>(q.x); v[1] += hi2f<T>(q.x);
-          v[2] += lo2f<T>(q.y); v[3] += hi2f<T>(q.y);
+          for (int e = 0; e < 4; ++e) {
+            v[e] = acc[j][m][4 * ga + e];
+            v[4 + e] = acc[j][m][4 * gb + e];
+          }
+          if (p.bias && rin) {
+            const float* bs = p.bias + (long long)bb * p.bias_bs + n0 + 32 * m + 4 * kg;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              if (8 * ga + 4 * kg + e + n0 + 32 * m < p.N) v[e] += bs[8 * ga + e];
+              if (8 * gb + 4 * kg + e + n0 + 32 * m < p.N) v[4 + e] += bs[8 * gb + e];
+            }
+          }
+          if (p.accumulate) {
+            // the existing 8 channels at c, swapped into the accumulator layout (as the
+            // residual of conv3d_v4.hpp's fast epilogue)
+            u32x4 q = u32x4{0u, 0u, 0u, 0u};
+            if (ok) q = *reinterpret_cast<const u32x4*>(o);
+            const auto s0 = __builtin_amdgcn_permlane32_swap(q[0], q[2], false, false);
+            const auto s1 = __builtin_amdgcn_permlane32_swap(q[1], q[3], false, false);
+            const unsigned g0 = s0[0], g1 = s1[0], h0 = s0[1], h1 = s1[1];
+            v[0] += lo2f<T>(g0); v[1] += hi2f<T>(g0);
+            v[2] += lo2f<T>(g1); v[3] += hi2f<T>(g1);
+            v[4] += lo2f<T>(h0); v[5] += hi2f<T>(h0);
+            v[6] += lo2f<T>(h1); v[7] += hi2f<T>(h1);
+          }
+          const unsigned p0 = pack2<T>(v[0], v[1]), p1 = pack2<T>(v[2], v[3]);
+          const unsigned p2 = pack2<T>(v[4], v[5]), p3 = pack2<T>(v[6], v[7]);
+          const auto t0 = __builtin_amdgcn_permlane32_swap(p0, p2, false, false);
+          const auto t1 = __builtin_amdgcn_permlane32_swap(p1, p3, false, false);
+          u32x4 w;
+          w[0] = t0[0]; w[1] = t1[0]; w[2] = t0[1]; w[3] = t1[1];
+          if (ok) *reinterpret_cast<u32x4*>(o) = w;
         }
-        q.x = pack2<T>(v[0], v[1]);
-        q.y = pack2<T>(v[2], v[3]);
-        *reinterpret_cast<uint2*>(o) = q;
+      } else {
+        if (!rin) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = n0 + 32 * m + 8 * g + 4 * kg;   // 4 consecutive channels c .. c+3
+          if (c >= p.N) continue;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] = acc[j][m][4 * g + e] + (p.bias ? p.bias[(long long)bb * p.bias_bs + c + e] : 0.f);
+          T* o;
+          if (p.out1 && c >= p.out_c0) o = reinterpret_cast<T*>(p.out1) + r * (p.N - p.out_c0) + (c - p.out_c0);
+          else o = reinterpret_cast<T*>(p.out) + r * (p.out1 ? p.out_c0 : p.N) + c;
+          uint2 q;
+          if (p.accumulate) {
+            q = *reinterpret_cast<const uint2*>(o);
+            v[0] += lo2f<T>(q.x); v[1] += hi2f<T>(q.x);
+            v[2] += lo2f<T>(q.y); v[3] += hi2f<T>(q.y);
+          }
+          q.x = pack2<T>(v[0], v[1]);
+          q.y = pack2<T>(v[2], v[3]);
+          *reinterpret_cast<uint2*>(o) = q;
+        }
       }
+    }
   }
 }
 

@@ -28,7 +28,9 @@ int launch_temb_bwd(const float* t, int B, int mc, const float* w1, const float*
 int gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const void* du, int du_mode, const float* ss,
                      const float* mr, const float* gamma, int groups, int64_t B, int64_t d, int64_t h, int64_t w,
                      int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma, float* dbeta, void* ws,
-                     int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream, int acc_affine);
+                     int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream, int acc_affine,
+                     const float* pre_part = nullptr, int pre_nblk = 0);
+int gb_part_reduce(const float* part, int nblk, int C, int64_t B, int slices, float* out, hipStream_t s);
 int haar_nd_synth_add(int dtype, int64_t B, int64_t d, int64_t h, int64_t w, int C, const void* L, int64_t l_vs,
                       float lll, const void* H, int64_t h_vs, float high, void* fine, int acc, hipStream_t s);
 int haar_nd_anal_add(int dtype, int64_t B, int64_t d, int64_t h, int64_t w, int C, const void* fine, void* L,
@@ -1182,8 +1184,12 @@ namespace {
 
 struct GLayout {
   std::vector<int64_t> g_off;
-  int64_t sync, tmp, dout, deb, dsil, gnws, gnws_bytes, split, split_bytes, wgws, wgws_bytes, dwe, chs, chs_bytes, total;
+  int64_t sync, tmp, dout, deb, dsil, gnws, gnws_bytes, split, split_bytes, wgws, wgws_bytes, dwe, chs, chs_bytes;
+  int64_t gbp, gbp_bytes;   // fused GroupNorm-backward partials ([B][tiles][C][2]) + their slice sums
+  int64_t total;
 };
+
+constexpr int kGbSlices = 64;   // slice sums of the fused GroupNorm-backward partials (cwdm::gb_part_reduce)
 
 int ckpad(const cwdm_unet* u, int c) {
   const int ck = 32 / esize(u->cfg.dtype);
@@ -1252,6 +1258,16 @@ GLayout glayout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) 
                                                          std::max(cs.cout, 8)));
   G.chs_bytes = chs;
   G.chs = take(chs);
+  // the dgrad epilogue's GroupNorm-backward partials: one row per 32x4x4 tile
+  // of the DMA conv (cwdm::GbwdFuse), then kGbSlices slice sums of them
+  int64_t gbp = 0;
+  for (const auto& g : u->gns) {
+    const int lv = g.level;
+    const int64_t tiles = ceil_div(W >> lv, 32) * ceil_div(H >> lv, 4) * ceil_div(D >> lv, 4);
+    gbp = std::max(gbp, B * tiles * g.channels * 8 + align_up(B * (int64_t)kGbSlices * g.channels * 8));
+  }
+  G.gbp_bytes = gbp;
+  G.gbp = take(gbp);
   G.total = off;
   return G;
 }
@@ -1410,7 +1426,36 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
     d.ws_bytes = G.split_bytes;
     return cwdm_conv3d_forward(&d, stream);
   };
-  auto gn_bwd = [&](int gi, int x0, int x1, int du_mode) -> int {
+  // dgrad conv ci whose output du (tmp) feeds the SiLU(GroupNorm gi) backward at
+  // the same grid, input x = (xid0, xid1): the conv's epilogue takes the reduce
+  // pass of that backward when its kernel can (cwdm::GbwdFuse: 16-bit DMA conv,
+  // no K split); pre then names the partials for gn_silu_bwd_impl
+  struct Pre { const float* part = nullptr; int nblk = 0; };
+  static const bool gb_on = [] { const char* e = std::getenv("CWDM_GBWD_FUSE"); return !(e && e[0] == '0'); }();
+  float* gbp = reinterpret_cast<float*>(gb + G.gbp);
+  auto dgrad_gn = [&](int ci, const void* dy, int gi, int xid0, int xid1, Pre& pre) -> int {
+    pre = Pre{};
+    if (!gb_on || G.gbp_bytes <= 0) return dgrad(ci, dy);
+    const auto& g = u->gns[gi];
+    cwdm::GbwdFuse f{};
+    f.x0 = act(xid0); f.x1 = act(xid1); f.c0 = u->tensors[xid0].channels;
+    f.ss = ss_of(gi); f.mr = mr_of(gi); f.groups = u->cfg.num_groups;
+    f.part = gbp;
+    f.part_bytes = G.gbp_bytes - align_up(B * (int64_t)kGbSlices * g.channels * 8);
+    cwdm::g_gbwd = &f;
+    const int r = dgrad(ci, dy);
+    cwdm::g_gbwd = nullptr;
+    if (r || !f.used) return r;
+    if (f.nblk <= 512) {   // few tiles: gn_bwd_finalize reads them directly
+      pre.part = gbp; pre.nblk = f.nblk;
+      return CWDM_OK;
+    }
+    float* sl = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(gbp) + f.part_bytes);
+    if (int rc2 = gb_part_reduce(gbp, f.nblk, g.channels, B, kGbSlices, sl, s)) return rc2;
+    pre.part = sl; pre.nblk = kGbSlices;
+    return CWDM_OK;
+  };
+  auto gn_bwd = [&](int gi, int x0, int x1, int du_mode, const Pre* pre = nullptr) -> int {
     const auto& g = u->gns[gi];
     const int lv = g.level;
     const int c0 = u->tensors[x0].channels, c1 = x1 >= 0 ? u->tensors[x1].channels : 0;
@@ -1418,7 +1463,8 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
     // affine gradients accumulate (zeroed at segment 0): a reused WavUNetModel block adds its second use
     return gn_silu_bwd_impl(act(x0), c0, act(x1), c1, tmp, du_mode, ss_of(gi), mr_of(gi), P(g.gamma_off),
                             u->cfg.num_groups, B, D >> lv, H >> lv, W >> lv, dt, grd(x0), a0, grd(x1), a1,
-                            GR(g.gamma_p), GR(g.beta_p), gb + G.gnws, G.gnws_bytes, nullptr, 0, stream, 1);
+                            GR(g.gamma_p), GR(g.beta_p), gb + G.gnws, G.gnws_bytes, nullptr, 0, stream, 1,
+                            pre ? pre->part : nullptr, pre ? pre->nblk : 0);
   };
 
   for (int seg = seg_begin; seg < seg_end; ++seg) {
@@ -1442,8 +1488,9 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
         return rc;
       if ((rc = wgrad(0, 3, act(co.a0), co.cin_a, nullptr, 0, 0, ss_of(u->head_g), d16, ocp, oc, GR(co.w_p))))
         return rc;
-      if ((rc = dgrad(u->head_c, d16))) return rc;
-      if ((rc = gn_bwd(u->head_g, hg.src0, -1, 0))) return rc;
+      Pre pre;
+      if ((rc = dgrad_gn(u->head_c, d16, u->head_g, hg.src0, -1, pre))) return rc;
+      if ((rc = gn_bwd(u->head_g, hg.src0, -1, 0, &pre))) return rc;
       continue;
     }
     if (seg <= nb && u->blocks[nb - seg].updown == 7) {
@@ -1493,7 +1540,8 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
       if ((rc = cwdm_resample_add(grd(hx.out), grd(o), cout, B, D >> lout, H >> lout, W >> lout, 0, take_acc(hx.out),
                                   dt, stream)))
         return rc;
-      if ((rc = dgrad(bk.c2, grd(o)))) return rc;
+      Pre pre2;
+      if ((rc = dgrad_gn(bk.c2, grd(o), bk.g2, hh.out, -1, pre2))) return rc;
       // ---- GN2 -> d(h + emb), with its channel sums = the emb projection's gradient
       const int k = bk.emb_k;
       const int roff = u->emb_rows_off[k], rn = u->emb_rows_n[k];
@@ -1502,7 +1550,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
         if ((rc = gn_silu_bwd_impl(act(hh.out), cout, nullptr, 0, tmp, 0, ss_of(bk.g2), mr_of(bk.g2), P(g.gamma_off),
                                    u->cfg.num_groups, B, D >> lout, H >> lout, W >> lout, dt, grd(hh.out),
                                    take_acc(hh.out), nullptr, 0, GR(g.gamma_p), GR(g.beta_p), gb + G.gnws,
-                                   G.gnws_bytes, deb + roff, u->R, stream, 1)))
+                                   G.gnws_bytes, deb + roff, u->R, stream, 1, pre2.part, pre2.nblk)))
           return rc;
       }
       if ((rc = launch_emb_bwd(deb + roff, u->R, rn, (int)B, temb, u->E, P(u->off_emb_w) + (int64_t)roff * u->E,
@@ -1537,8 +1585,9 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
         return rc;
       if ((rc = wgrad_c(bk.c1, lin, act(bk.x0), cin, nullptr, 0, 0, ss_of(bk.g1), grd(h1), cout, cout, GR(c1.w_p))))
         return rc;
-      if ((rc = dgrad(bk.c1, grd(h1)))) return rc;
-      if ((rc = gn_bwd(bk.g1, bk.x0, -1, 0))) return rc;
+      Pre pre1;
+      if ((rc = dgrad_gn(bk.c1, grd(h1), bk.g1, bk.x0, -1, pre1))) return rc;
+      if ((rc = gn_bwd(bk.g1, bk.x0, -1, 0, &pre1))) return rc;
       continue;
     }
     if (seg <= nb && u->blocks[nb - seg].updown >= 3) {
@@ -1615,7 +1664,8 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
                                     stream)))
           return rc;
       }
-      if ((rc = dgrad(bk.c2, grd(o)))) return rc;
+      Pre pre2;
+      if ((rc = dgrad_gn(bk.c2, grd(o), bk.g2, h1, -1, pre2))) return rc;
       // ---- GN2 -> dh1, with the per-channel sums of dh1 (the emb projection's
       // gradient) taken in the same pass when dh1 is written, not accumulated
       const int k = bk.emb_k;
@@ -1626,10 +1676,10 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
         if ((rc = gn_silu_bwd_impl(act(h1), cout, nullptr, 0, tmp, 0, ss_of(bk.g2), mr_of(bk.g2), P(g.gamma_off),
                                    u->cfg.num_groups, B, D >> lout, H >> lout, W >> lout, dt, grd(h1), take_acc(h1),
                                    nullptr, 0, GR(g.gamma_p), GR(g.beta_p), gb + G.gnws, G.gnws_bytes, deb + roff, u->R,
-                                   stream, 1)))
+                                   stream, 1, pre2.part, pre2.nblk)))
           return rc;
       } else {
-        if ((rc = gn_bwd(bk.g2, h1, -1, 0))) return rc;
+        if ((rc = gn_bwd(bk.g2, h1, -1, 0, &pre2))) return rc;
         if ((rc = cwdm_channel_sum(grd(h1), dt, B, Vo, cout, cout, deb + roff, u->R, nullptr, nullptr, gb + G.chs,
                                    G.chs_bytes, stream)))
           return rc;
@@ -1649,9 +1699,15 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
                           grd(h1), cout, cout, GR(c1.w_p))))
           return rc;
       }
-      if ((rc = dgrad(bk.c1, grd(h1)))) return rc;
-      // ---- GN1 (+ resample adjoint) -> dx0 / dx1
-      if ((rc = gn_bwd(bk.g1, bk.x0, bk.x1, bk.updown == 1 ? 1 : (bk.updown == 2 ? 2 : 0)))) return rc;
+      // ---- GN1 (+ resample adjoint) -> dx0 / dx1 (the reduce in the dgrad's epilogue
+      // when the GroupNorm's grid is the conv's: no resampling in between)
+      Pre pre1;
+      if (bk.updown == 0) {
+        if ((rc = dgrad_gn(bk.c1, grd(h1), bk.g1, bk.x0, bk.x1, pre1))) return rc;
+      } else if ((rc = dgrad(bk.c1, grd(h1)))) {
+        return rc;
+      }
+      if ((rc = gn_bwd(bk.g1, bk.x0, bk.x1, bk.updown == 1 ? 1 : (bk.updown == 2 ? 2 : 0), &pre1))) return rc;
       continue;
     }
     // conv_in + time_embed

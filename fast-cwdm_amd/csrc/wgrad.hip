@@ -465,6 +465,164 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// 1x1 weight gradient (the ResBlock skip_connection conv, unet.py:264-271;
+// 16-bit types): dW[co][ci] = sum_v dY[v][co] U[v][ci] with U the raw
+// concat(u0, u1).  A GEMM with K = B * V voxels and a 64 x 128 output tile, so
+// HBM-bound (R0 of the run.sh U-Net: 192 -> 64 channels over 2 M voxels reads
+// 1.07 GB for 0.05 TFLOP).  The brick kernel staged a 3^3 halo per 16x4x4
+// brick (2.5x the voxels) and re-read dY once per 32-channel input tile
+// (386-607 us per R0 call, ~2.2 ms per training step); here a unit = a range of
+// 64-voxel stages x one (64 co, 128 ci) tile, every stage -- 8 chunk images of
+// U (16 channels, 32-B rows) + the 64 dY rows -- lands in LDS by LDS-DMA,
+// double-buffered, and feeds the transposed-read MFMA operands of the 3x3x3
+// kernels (tap offset 0).  Wave w owns input channels [32 w, +32) of the tile.
+// Partial tiles go straight into dw (OIDHW) as full-rate fp32 atomics.
+struct Wg1Params {
+  const unsigned char* u0; const unsigned char* u1;
+  int c0, c1, cin;
+  const unsigned char* dy; int dy_cs, cout;
+  long long rows;   // B * V voxel rows (u0 / u1 / dy are row-contiguous over the batch)
+  long long nst;    // 64-row stages = ceil(rows / 64)
+  long long per;    // stages per unit
+  int nco, nci;     // 64-channel co tiles x 128-channel ci tiles
+  int units, upx;   // (stage range, tile) units; units per XCD
+  float* dw;
+};
+constexpr int W1_NV = 64;
+constexpr int W1_IMG = W1_NV * 32 + 128;         // one 16-channel chunk image (+128 B: complementary banks)
+constexpr int W1_DY = 8 * W1_IMG;                // the 64 dY rows (128 B, quad-swizzled) after the 8 images
+constexpr int W1_BUF = W1_DY + W1_NV * 128;      // one stage: 25.6 KB (three workgroups per CU double-buffered)
+
+template <typename T>
+__global__ void __launch_bounds__(256) wgrad1_kernel(Wg1Params p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the DMA descriptors are SGPRs
+  const int ntiles = p.nco * p.nci;
+  // XCD-aware: the k-th workgroup of XCD j takes unit j * upx + k of the
+  // range-major list, so the tiles of one stage range share an L2
+  const int xj = (int)(blockIdx.x & 7), xk = (int)(blockIdx.x >> 3);
+  const int u = xj * p.upx + xk;
+  if (xk >= p.upx || u >= p.units) return;
+  const long long sr = u / ntiles;
+  const int tile = u % ntiles;
+  const long long sb = sr * p.per, se = min(sb + p.per, p.nst);
+  if (sb >= se) return;
+  const int co0 = (tile % p.nco) * 64, ci0 = (tile / p.nco) * 128;
+  const bool wact = ci0 + 32 * wv < p.cin;   // this wave's 32 input channels exist
+  f32x16 acc[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[m][i] = 0.f;
+
+  // DMA of stage st into buf: 16 image instructions (chunk c, half k) + 8 dY
+  // instructions, 6 per wave; rows past the end read zeros (buffer range check)
+  auto issue = [&](long long st, unsigned char* buf) {
+    const long long r0 = st * W1_NV;
+    const int nr = (int)min((long long)W1_NV, p.rows - r0);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int k = wv + 4 * j;   // instruction 0..23
+      if (k < 16) {
+        const int c = k >> 1, half = k & 1;
+        const int gc = ci0 + 16 * c;
+        if (gc < p.cin) {
+          const bool s0 = gc < p.c0;
+          const int cs = s0 ? p.c0 : p.c1;
+          const unsigned char* base = (s0 ? p.u0 : p.u1) + r0 * cs * 2;
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nr * cs * 2, 0x00020000);
+          const int row = 32 * half + (lane >> 1);
+          const unsigned voff = (unsigned)(row * cs + (s0 ? gc : gc - p.c0)) * 2u + (unsigned)(lane & 1) * 16u;
+          wg_dma16(rs, buf + c * W1_IMG + half * 1024, voff);
+        }
+      } else {
+        const int kk = k - 16;
+        const int pc = kk * 64 + lane, v = pc >> 3, pos = pc & 7;
+        const int qd = dy_quad<T, 2>(pos, v);   // the swizzle is an involution
+        const int cc = co0 + qd * 8;
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.dy + r0 * p.dy_cs * 2), (short)0, nr * p.dy_cs * 2, 0x00020000);
+        const unsigned voff = cc < p.dy_cs ? (unsigned)(v * p.dy_cs + cc) * 2u : 0xFFFFFFF0u;
+        wg_dma16(rd, buf + W1_DY + kk * 1024, voff);
+      }
+    }
+  };
+
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, h = g >> 1;
+  issue(sb, smem);
+  for (long long st = sb; st < se; ++st) {
+    unsigned char* cur = smem + ((st - sb) & 1) * W1_BUF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this stage's DMA (issued one stage ago) landed
+    __syncthreads();                                  // ... for every wave; the other buffer is free
+    if (st + 1 < se) issue(st + 1, smem + ((st - sb + 1) & 1) * W1_BUF);
+    if (wact) {
+      const unsigned char* dyl = cur + W1_DY;
+      const unsigned char* bimg = cur + (2 * wv + (g & 1)) * W1_IMG + 8 * pp;
+#pragma unroll
+      for (int s = 0; s < W1_NV / 16; ++s) {
+        const int v0 = 16 * s + 8 * h + q, v1 = v0 + 4;
+        u32x4 a[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const int qd = 4 * m + 2 * (g & 1) + (pp >> 1);
+          a[m] = join(tr_read(dyl + v0 * 128 + dy_quad<T, 2>(qd, v0) * 16 + 8 * (pp & 1)),
+                      tr_read(dyl + v1 * 128 + dy_quad<T, 2>(qd, v1) * 16 + 8 * (pp & 1)));
+        }
+        const u32x4 b = join(tr_read(bimg + v0 * 32), tr_read(bimg + v1 * 32));
+#pragma unroll
+        for (int m = 0; m < 2; ++m) mfma_acc(acc[m], a[m], b, (T*)nullptr);
+      }
+    }
+  }
+  if (!wact) return;
+  const int ci = ci0 + 32 * wv + (lane & 31);
+  if (ci >= p.cin) return;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int co = co0 + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+      if (co < p.cout) atomicAdd(p.dw + (long long)co * p.cin + ci, acc[m][i]);
+    }
+}
+
+template <typename T>
+int launch_wg1(const cwdm_wgrad_desc* d, hipStream_t s) {
+  Wg1Params q{};
+  q.u0 = reinterpret_cast<const unsigned char*>(d->u0);
+  q.u1 = reinterpret_cast<const unsigned char*>(d->u1);
+  q.c0 = d->u_c0; q.c1 = d->u_c1; q.cin = d->u_c0 + d->u_c1;
+  q.dy = reinterpret_cast<const unsigned char*>(d->dy); q.dy_cs = d->dy_cs; q.cout = d->cout;
+  q.rows = d->B * d->D * d->H * d->W;
+  q.nst = ceil_div(q.rows, (int64_t)W1_NV);
+  q.nco = (int)ceil_div(d->cout, 64);
+  q.nci = (int)ceil_div(q.cin, 128);
+  const long long ntiles = (long long)q.nco * q.nci;
+  // ~3 workgroups per CU slot (51 KB of LDS each): stage ranges x tiles ~ 768
+  long long S = std::max<long long>(1, 768 / ntiles);
+  if (S > q.nst) S = q.nst;
+  q.per = ceil_div(q.nst, S);
+  S = ceil_div(q.nst, q.per);
+  q.units = (int)(S * ntiles);
+  q.upx = (q.units + 7) / 8;
+  q.dw = d->dw;
+  constexpr int smem = 2 * W1_BUF;
+  auto k = wgrad1_kernel<T>;
+  CWDM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, smem));
+  hipLaunchKernelGGL(k, dim3((unsigned)(8LL * q.upx)), dim3(256), smem, s, q);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+// the 1x1 kernel's shapes: 16-bit, source boundary on a 16-channel chunk, < 2 GB per stage row block
+bool wg1_eligible(const cwdm_wgrad_desc* d) {
+  if (d->ksize != 1 || !dtype_half(d->dtype) || d->u_gn || d->u_mode != 0 || d->u_cm) return false;
+  if (d->u_c0 % 16 || (d->u_c0 + d->u_c1) % 32 || d->dy_cs % 8) return false;
+  return d->B * d->D * d->H * d->W * (int64_t)(d->u_c0 + d->u_c1) * 2 < (1LL << 40);
+}
+
 // dW[co][ci][tap] += scratch[tap][co][ci]
 // (rezero: leave the scratch zeroed for the next call -- the plan's backward
 // zeroes it once per call instead of once per conv)
@@ -570,6 +728,11 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
   const long long nw = (long long)d->cout * cin * p.taps;
   const int zeroed = g_wgrad_ws_zeroed;
   int rc;
+  static const bool wg1_on = !std::getenv("CWDM_WG1_OFF");   // A/B knob: the brick kernel for 1x1
+  if (wg1_on && wg1_eligible(d)) {
+    // 1x1: the streaming kernel, accumulating straight into dw (no scratch)
+    return d->dtype == CWDM_F16 ? launch_wg1<f16_t>(d, s) : launch_wg1<bf16_t>(d, s);
+  }
   if (d->u_cm) {
     // U kept chunk-major by the forward: the DMA-staged kernel
     CWDM_REQUIRE(dtype_half(d->dtype) && d->ksize == 3 && !d->u_gn && !d->u1 && d->u_c1 == 0, CWDM_E_UNSUPPORTED,

@@ -174,8 +174,11 @@ class TrainLoop:
             self.grad_scaler.unscale_(self.opt)
         with th.no_grad():
             if self.native:
-                info["norm/param_max"] = self.model.flat_params.abs().max()
-                info["norm/grad_max"] = self.model.flat_grad().abs().max()
+                # max |p| over the flat buffers as ONE reduction each (abs().max() wrote
+                # a 326 MB |p| temporary first: ~0.4 ms per step at 81.5 M parameters)
+                inf = float("inf")
+                info["norm/param_max"] = th.linalg.vector_norm(self.model.flat_params, inf)
+                info["norm/grad_max"] = th.linalg.vector_norm(self.model.flat_grad(), inf)
             else:
                 info["norm/param_max"] = max(p.abs().max() for p in self.model.parameters())
                 info["norm/grad_max"] = max(p.grad.abs().max() for p in self.model.parameters() if p.grad is not None)

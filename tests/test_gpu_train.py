@@ -44,6 +44,11 @@ WG_CASES = [
     ("head_cout8", 1, (8, 8, 8), 64, 0, 8, 0, True, 3, 16),
     ("skip1x1", 2, (4, 8, 16), 64, 32, 64, 0, False, 1, 64),
     ("tiny_grid", 1, (2, 2, 2), 64, 64, 128, 0, True, 3, 128),
+    # 1x1 streaming kernel (wgrad1_kernel): R0-like concat 128 + 64 -> 64 over two
+    # batches with a partial last 64-row stage, and a 512 -> 256 tile grid
+    ("skip1x1_r0", 2, (6, 10, 34), 128, 64, 64, 0, False, 1, 64),
+    ("skip1x1_wide", 1, (4, 8, 8), 256, 256, 256, 0, False, 1, 256),
+    ("skip1x1_cout40", 1, (3, 5, 7), 48, 16, 40, 0, False, 1, 48),
 ]
 
 
@@ -181,8 +186,11 @@ def test_conv3d_dgrad_packing_vs_torch(cfg, dtype_name):
 
 @pytest.mark.parametrize("dtype_name", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("shape", [(1, (4, 8, 16), 32, 40, 56), (2, (4, 4, 40), 64, 24, 48),
-                                   (1, (4, 4, 64), 128, 128, 64), (1, (3, 5, 7), 16, 8, 24)])
-def test_conv3d_b_only_dual_output_accumulate(shape, dtype_name):
+                                   (1, (4, 4, 64), 128, 128, 64), (1, (3, 5, 7), 16, 8, 24),
+                                   (2, (3, 4, 22), 64, 128, 64), (1, (2, 3, 40), 64, 64, 64),
+                                   (1, (2, 4, 12), 32, 20, 28)])
+@pytest.mark.parametrize("acc", [1, 0])
+def test_conv3d_b_only_dual_output_accumulate(shape, dtype_name, acc):
     """1x1 skip dgrad: B-only conv writing channel slices to two buffers,
     accumulating (16-bit: the pointwise MFMA kernel, pointwise.hip; partial
     channel and voxel blocks, batch 2, odd grids)."""
@@ -210,12 +218,12 @@ def test_conv3d_b_only_dual_output_accumulate(shape, dtype_name):
     d.dtype, d.B, (d.D, d.H, d.W), d.cout = dtype, B, grid, cin
     d.b0, d.b_c0, d.b_w = a.data_ptr(), cout, pk.data_ptr()
     d.res_mode = -1
-    d.out, d.out_dtype, d.out1, d.out_c0, d.accumulate = o0.data_ptr(), dtype, o1.data_ptr(), c0, 1
+    d.out, d.out_dtype, d.out1, d.out_c0, d.accumulate = o0.data_ptr(), dtype, o1.data_ptr(), c0, acc
     nws = L.cwdm_conv3d_workspace_bytes(ctypes.byref(d))
     ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=DEV)
     d.workspace, d.ws_bytes = ws.data_ptr(), nws
     check(L.cwdm_conv3d_forward(ctypes.byref(d), None))
-    got = torch.cat([o0.float().cpu() - base0.float(), o1.float().cpu() - base1.float()], -1)
+    got = torch.cat([o0.float().cpu() - acc * base0.float(), o1.float().cpu() - acc * base1.float()], -1)
     tol = 2e-5 if dtype_name == "fp32" else 3e-2
     assert rel_err(_nc(got), ref) < tol
 
