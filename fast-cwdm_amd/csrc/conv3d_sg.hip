@@ -78,6 +78,7 @@ struct SGParams {
   // own in the workspace).  Never a process-wide array: launches on other
   // streams or plans would share tiles' counters.
   unsigned* count;
+  int xcd;   // 1: XCD-aware work map (below), 0: plain (env CWDM_SG_XCD=0, A/B)
 };
 
 // counter block pre-zeroed by the caller (the U-Net plan, per forward /
@@ -115,11 +116,21 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   }
 #endif
 
-  // work item -> (batch, brick, 16-channel tile); channel tile fastest (the 16
-  // workgroups of a brick share its halo in L2)
-  const int t16 = blockIdx.x % q.ntile16;
-  const int ks = (blockIdx.x / q.ntile16) % q.ksplit;
-  const int st = blockIdx.x / (q.ntile16 * q.ksplit);
+  // work item -> (batch, brick, 16-channel tile); channel tile fastest.  The
+  // hardware deals consecutive workgroups to the 8 XCDs round robin, so with the
+  // plain map XCD j ran channel tiles j, j + 8 of EVERY brick and fetched every
+  // brick's halo into its own L2 (8x the halo traffic; at 28^3 x 128 channels
+  // ~128 MB per conv from MALL).  XCD-aware: XCD j runs one contiguous run of
+  // work items -- whole bricks with all their channel tiles (and K slices), so
+  // a halo is fetched into one L2 and the tiles' weights stay L2-resident.
+  int wi = blockIdx.x;
+  if (q.xcd) {
+    const int n = (int)gridDim.x, xj = wi & 7, q8 = n >> 3, r8 = n & 7;
+    wi = (xj < r8 ? xj * (q8 + 1) : r8 * (q8 + 1) + (xj - r8) * q8) + (wi >> 3);
+  }
+  const int t16 = wi % q.ntile16;
+  const int ks = (wi / q.ntile16) % q.ksplit;
+  const int st = wi / (q.ntile16 * q.ksplit);
   const int b = st / q.parts, brick = st - b * q.parts;
   const int tx = q.tx, ty = q.ty;
   const int x0 = (brick % tx) * BX, y0 = ((brick / tx) % ty) * BY, z0 = (brick / (tx * ty)) * 4;
@@ -503,7 +514,10 @@ void sg_go_t(const SGParams& q, const cwdm_conv3d_desc* d, int taps, hipStream_t
   }
 }
 
-int sg_go(const SGParams& q, const cwdm_conv3d_desc* d, int taps, double flops, hipStream_t s) {
+int sg_go(const SGParams& q0, const cwdm_conv3d_desc* d, int taps, double flops, hipStream_t s) {
+  static const int xcd_map = [] { const char* e = std::getenv("CWDM_SG_XCD"); return !(e && e[0] == '0'); }();
+  SGParams q = q0;
+  q.xcd = xcd_map;
   prof_begin(s);
   if (d->dtype == CWDM_F16) sg_go_t<f16_t>(q, d, taps, s);
   else sg_go_t<bf16_t>(q, d, taps, s);

@@ -36,6 +36,12 @@ CASES = {
     "L3_256_256_res": (16, 256, 0, 256, 0, False, 0, 0),
     "L4_256_256_gn": (8, 256, 0, 256, 0, True, 0, -1),
     "L4_256_256_nogn": (8, 256, 0, 256, 0, False, 0, -1),
+    # config 5 (224^3 input -> 56^3 / 28^3 / 14^3 levels)
+    "C5_L1_128_128_gn": (28, 128, 0, 128, 0, True, 0, -1),
+    "C5_L1_64_128_gn": (28, 64, 0, 128, 0, True, 0, -1),
+    "C5_L1_256_128_cat": (28, 128, 128, 128, 0, True, 0, -1),
+    "C5_L2_128_128_gn": (14, 128, 0, 128, 0, True, 0, -1),
+    "C5_L0_64_64_gn": (56, 64, 0, 64, 0, True, 0, -1),
 }
 
 
