@@ -989,9 +989,16 @@ __global__ void __launch_bounds__(256) conv3d_wide_kernel(ConvParams p) {
 inline int pick_nf(int cout) { return (cout % 64 == 0) ? 2 : 1; }
 
 struct Brick { int bx, by, bz; };
+// Grids from kWideMinW up take the 32-wide x tiles of the DMA conv (conv3d_v4.hpp,
+// the last x tile masked) and its statistics bricks; below, the small-grid
+// kernel's 16x4x4 / 8x8x4 bricks (conv3d_sg.hip).  24: config 5's 28^3 level ran
+// on the small-grid kernel at 0.28 PF (per 32-channel chunk ~8.3k cycles of
+// LDS-DMA for 1.7k of MFMA, tools/sg_stamps.py); on the DMA kernel with 32-channel
+// tiles it computes 12.5 % masked voxels but stays MFMA-bound.
+constexpr int kWideMinW = 24;
 inline Brick pick_brick(int64_t D, int64_t H, int64_t W) {
   (void)D; (void)H;
-  if (W >= 32) return {32, 4, 4};  // conv3d_wide_kernel
+  if (W >= kWideMinW) return {32, 4, 4};  // conv3d_wide_kernel / conv3d_v4_kernel
   if (W >= 16) return {16, 4, 4};
   return {8, 8, 4};
 }

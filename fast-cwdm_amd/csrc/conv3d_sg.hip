@@ -414,9 +414,9 @@ namespace {
 bool sg_shape_ok(const cwdm_conv3d_desc* d) {
   if (g_conv_path.load(std::memory_order_relaxed) == 1) return false;
   if (!dtype_half(d->dtype) || d->out_dtype != d->dtype || d->accumulate || d->out1 || d->cout % 64) return false;
-  // W < 32 (the wide kernels take W >= 32): 16 x 4 x 4 bricks for W >= 16, 8 x 8 x 4
-  // below (pick_brick's statistics bricks), the last brick of an axis partial
-  return d->W >= 1 && d->W < 32 && d->H >= 1 && d->D >= 1;
+  // W < kWideMinW (the wide kernels take the rest): 16 x 4 x 4 bricks for W >= 16,
+  // 8 x 8 x 4 below (pick_brick's statistics bricks), the last brick of an axis partial
+  return d->W >= 1 && d->W < kWideMinW && d->H >= 1 && d->D >= 1;
 }
 
 // statistics bricks of a small grid: (bx, tx, ty, tz), parts = tx ty tz (== cwdm_conv3d_parts)

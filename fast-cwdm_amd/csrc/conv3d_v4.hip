@@ -149,6 +149,9 @@ int v4_ksplit(const cwdm_conv3d_desc* d) {
   const int64_t nblk = v4_items(d);
   const int64_t target = v4_ksplit_target();
   if (nblk >= target || nch < 2) return 1;
+  // 16-bit: v4_launch doubles the work items with 32-channel tiles (no finishing
+  // passes) -- enough at config 5's 28^3 level (98 -> 196)
+  if (dtype_half(d->dtype) && 2 * nblk >= target && d->cout % 64 == 0) return 1;
   int S = (int)std::min<int64_t>((target + nblk - 1) / nblk, nch / 2);
   if (S < 1) S = 1;
   const int per = (nch + S - 1) / S;
@@ -162,13 +165,16 @@ bool v4_eligible(const cwdm_conv3d_desc* d) {
   if (d->b_w && d->res_mode >= 0) return false;
   if (sg_eligible(d)) return true;  // 16^3 / 8^3 levels: conv3d_sg.hip behind the same pre-passes
   if (!dtype_compute(d->dtype)) return false;
-  // W >= 32: the statistics partials follow cwdm_conv3d_parts' 32-wide x tiles (pick_brick)
-  if (!d->a_w || d->W < 32 || d->H % 4 || d->D % 4 || d->cout % 64) return false;
+  // W >= kWideMinW: the statistics partials follow cwdm_conv3d_parts' 32-wide x tiles (pick_brick)
+  if (!d->a_w || d->W < kWideMinW || d->H % 4 || d->D % 4 || d->cout % 64) return false;
   if (d->a_mode != 0 && d->a_mode != 1) return false;
   if (d->res_mode < -1 || d->res_mode > 1) return false;
   if (d->out1 && d->out_c0 % 8) return false;
   const int64_t nblk = v4_items(d);
-  if (nblk * v4_ksplit(d) < std::min<int64_t>(384, v4_ksplit_target()) && path != 2) return false;  // too few work items even K-split: the brick kernels
+  // work items: K slices, or (16-bit, no split, < 256 tiles) v4_launch's 32-channel tiles
+  const int S = v4_ksplit(d);
+  const int64_t items = nblk * S * (S == 1 && dtype_half(d->dtype) && nblk < 256 ? 2 : 1);
+  if (items < std::min<int64_t>(384, v4_ksplit_target()) && path != 2) return false;  // too few work items even K-split: the brick kernels
   const int esz = dtype_size(d->dtype);
   const int64_t sv = src_voxels(d);
   // the DMA range check works on 32-bit byte offsets per batch

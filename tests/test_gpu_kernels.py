@@ -349,6 +349,10 @@ V4_CASES = [
     ("v4_partial_x_gn_res", 1, (4, 8, 56), 64, 0, 64, 0, True, False, 0),
     ("v4_partial_x_ksplit_up", 1, (8, 4, 40), 64, 0, 64, 1, True, False, 1),
     ("v4_partial_x_concat_skip", 2, (4, 4, 48), 32, 16, 64, 0, True, True, -1),
+    # 24 <= W < 32 (r03): one partial x tile (config 5's 28^3 level, 32-channel tiles)
+    ("v4_w28_config5_res", 1, (28, 28, 28), 128, 0, 128, 0, True, False, 0),
+    ("v4_w24_concat_skip", 1, (8, 8, 24), 64, 64, 64, 0, True, True, -1),
+    ("v4_w26_up_res", 2, (8, 8, 26), 64, 0, 64, 1, True, False, 1),
 ]
 
 
