@@ -714,9 +714,13 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
   // thread (the kernel's UNR; du_mode 1 loops twice instead); with channel
   // sums at most 1024 workgroups per batch entry (one partial row each, summed
   // in workgroup order by chs_reduce_kernel), each looping over its share
+  // (at most 1024 workgroups per batch entry in every case: each thread loads its
+  // 40 coefficient words once and loops; one voxel pair per thread spent more
+  // load instructions on coefficients than on the tensors -- R0 64-channel
+  // apply 216 us with one pair per thread vs 160 us capped, same trace)
   const int ncg = C / 8, nvb = 256 / ncg;
   long long nblk = ceil_div(V, 2LL * nvb);
-  if (chs && nblk > 1024) nblk = 1024;
+  if (nblk > 1024) nblk = 1024;
   dim3 grid((unsigned)nblk, (unsigned)B);
   const dim3 block((unsigned)(nvb * ncg));
   float* cp = chs ? chs_part : nullptr;
