@@ -18,10 +18,13 @@
 //   * K chunks of 32 input channels (two 16-channel sub-chunks: chunk-major
 //     gn_apply output or channels-last sources, concat boundary per
 //     sub-chunk); MFMA K = the chunk's 32 channels of one tap.
-//   * Halo image in LDS, quad-major [4 quads][HVP slots][16 B], double
-//     buffered, filled by LDS-DMA (out-of-volume voxels read as zeros through
-//     the buffer range check).  A ds_read_b128 of 16 lanes reads 16
-//     consecutive halo slots of one quad plane.
+//   * Halo image in LDS, per 16-channel sub-chunk [HVP slots][2 quads][16 B]
+//     (32-B slot pitch), double buffered, filled by LDS-DMA (out-of-volume
+//     voxels read as zeros through the buffer range check).  A DMA instruction
+//     covers 32 consecutive slots x both quads, i.e. whole 32-B voxel rows of
+//     the chunk-major source (a quad-major image made every instruction fetch
+//     64 half-used lines: ~8 B/clk per CU, tools/sg_stamps.py); a ds_read_b128
+//     of 16 lanes reads 16 consecutive slots of one quad (2-way bank conflict).
 //   * The chunk's A fragments (16 output channels x 32 K per tap, 27 KB) are
 //     LDS-DMA'd beside its halo, double-buffered too: one workgroup per CU
 //     (144 KB of LDS) has no co-resident partner to hide global-load latency,
@@ -49,10 +52,10 @@ template <int BX, int BY, int PAD>
 struct SGCfg {
   // PAD 1: the 3x3x3 halo (648 / 600 voxels); PAD 0: the brick itself (1x1 skip)
   static constexpr int HX = BX + 2 * PAD, HY = BY + 2 * PAD, HZ = 4 + 2 * PAD, HV = HX * HY * HZ;
-  static constexpr int PCS = (HV + 63) / 64;                                   // 64-slot pieces per quad plane
+  static constexpr int PCS = (HV + 63) / 64;                                   // 1 KB pieces per quad's worth of slots
   static constexpr int HVP = PCS * 64;                                         // 704 slots
-  static constexpr int QB = HVP * 16;                                          // bytes per quad plane
-  static constexpr int BUF = 4 * QB;                                           // one halo buffer (32 channels)
+  static constexpr int SUB = HVP * 32;                                         // bytes per 16-channel sub-chunk image
+  static constexpr int BUF = 2 * SUB;                                          // one halo buffer (32 channels)
   static constexpr int WBUF = 27 * 1024;       // one chunk's A fragments: [tap][lane][16 B]
   static constexpr int SMEM = 2 * BUF + 2 * WBUF;
   static constexpr int LPO = 16 / BX;         // x lines per 16-voxel operand
@@ -139,16 +142,17 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   const int cb0 = ks * q.kper, cb1 = min(nch, cb0 + q.kper);  // this slice's chunks
 
   // halo DMA of 32-channel chunk c into buffer hbuf: pieces pc = wv + 4 j (44 in
-  // all: quad plane pc / PCS, slot block pc % PCS); quads 0-1 / 2-3 are the two
-  // 16-channel sub-chunks 2c / 2c + 1
+  // all: 16-channel sub-chunk 2c + pc / (2 PCS), 32-slot block pc % (2 PCS)),
+  // lane = (slot 32 blk + lane / 2, quad lane & 1)
   auto issue_halo = [&](int c, int hbuf) {
     unsigned char* hb = smem + hbuf * C::BUF;
 #pragma unroll
     for (int j = 0; j < C::PCS; ++j) {
       const int pc = wv + 4 * j;
-      const int qd = pc / C::PCS, blk = pc - qd * C::PCS;
-      const int hv = blk * 64 + lane;
-      if (hv >= C::HV) continue;  // padding slots: statistics scratch
+      const int sub = pc / (2 * C::PCS), blk = pc - sub * (2 * C::PCS);
+      const int hv = blk * 32 + (lane >> 1);
+      const int qd = 2 * sub + (lane & 1);
+      if (hv >= C::HV) continue;  // padding slots
       int sv = -1;
       {
         const int hx = hv % C::HX, hy = (hv / C::HX) % C::HY, hz = hv / (C::HX * C::HY);
@@ -193,9 +197,9 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
     }
   };
 
-  // lane read base: halo slot of (plane wv, operand line yl, x) in quad plane kq
+  // lane read base: halo slot of (plane wv, operand line yl, x), quad kq
   const int xl = l16 % BX, yl = l16 / BX;
-  const int hlane = kq * C::QB + ((wv * C::HY + yl) * C::HX + xl) * 16;
+  const int hlane = (kq >> 1) * C::SUB + (kq & 1) * 16 + ((wv * C::HY + yl) * C::HX + xl) * 32;
 
   sg_f32x4 acc[4];
   {
@@ -224,7 +228,7 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
       for (int dy = 0; dy < 3; ++dy) w[dy] = *reinterpret_cast<const u32x4*>(wb + (dz * 9 + dy * 3 + dx) * 1024);
 #pragma unroll
       for (int s = 0; s < C::NR; ++s)
-        a[s] = *reinterpret_cast<const u32x4*>(hb + ((dz * C::HY + s) * C::HX + dx) * 16);
+        a[s] = *reinterpret_cast<const u32x4*>(hb + ((dz * C::HY + s) * C::HX + dx) * 32);
     };
     if constexpr (TAPS == 27) {
       read_group(av[0], aw[0], 0);
@@ -233,7 +237,7 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
       // fragment sits at tap slot 0
 #pragma unroll
       for (int s2 = 0; s2 < 4 * C::LPO; s2 += C::LPO)
-        av[0][s2] = *reinterpret_cast<const u32x4*>(hb + s2 * C::HX * 16);
+        av[0][s2] = *reinterpret_cast<const u32x4*>(hb + s2 * C::HX * 32);
       aw[0][0] = *reinterpret_cast<const u32x4*>(wb);
     }
     // the next chunk's halo and weights go to the other buffers (last read by

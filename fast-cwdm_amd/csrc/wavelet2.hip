@@ -267,6 +267,125 @@ __global__ void __launch_bounds__(256) sampler2_kernel(cwdm_sampler_args a, S3w 
   }
 }
 
+// The same step with every tensor access staged through LDS (the fast path of
+// the resident loop: model_out, x_t, x_prev channels-last and 16-byte aligned,
+// Philox noise, no pred_xstart).  One thread still owns one coarse voxel's 64
+// channels (the 2-level transform mixes all of them), but a thread-per-voxel
+// float4 access touches 64 rows of 256 B per wave instruction (1.2 TB/s, 122 us
+// per 56^3 step); here each 16-lane group moves one whole 256-byte row.  Rows
+// are padded to 272 B so the per-thread row reads are conflict-free.  Bit-
+// identical to sampler2_kernel (same expressions in the same order).
+constexpr int S2V = 256;               // voxels per workgroup (one per thread)
+constexpr int S2P = 68;                // row pitch in floats (272 B)
+template <typename MirT>
+__global__ void __launch_bounds__(256) sampler2_lds_kernel(cwdm_sampler_args a, S3w mo, S3w xt, S3w xp, S3w mi) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];   // [S2V][S2P]
+  const int64_t nvox = a.d * a.h * a.w, total = a.B * nvox;
+  const int64_t i0 = (int64_t)blockIdx.x * S2V;
+  const int tid = threadIdx.x;
+  // whole rows in / out: pass k moves voxels 16 k + tid / 16, float4 tid % 16
+  auto stage_in = [&](const float* base, S3w st) {
+#pragma unroll 4
+    for (int k = 0; k < S2V / 16; ++k) {
+      const int lv = 16 * k + (tid >> 4), g = tid & 15;
+      const int64_t idx = i0 + lv;
+      float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < total) {
+        const int64_t b = idx / nvox, v = idx - b * nvox;
+        u = *reinterpret_cast<const float4*>(base + b * st.b + v * st.v + 4 * g);
+      }
+      *reinterpret_cast<float4*>(tile + lv * S2P + 4 * g) = u;
+    }
+  };
+  const int64_t idx = i0 + tid;
+  const bool live = idx < total;
+  const int64_t b = live ? idx / nvox : 0, v = live ? idx - b * nvox : 0;
+  int64_t t = a.t[b];
+  t = t < 0 ? 0 : (t >= a.T ? a.T - 1 : t);
+  const int bs = a.per_band ? 8 : 0;
+  const float* cf = a.coef + t * (a.per_band ? 64 * 8 : 8);
+  float* row = tile + tid * S2P;
+  float m[64];
+  stage_in(a.model_out, mo);
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const float4 u = *reinterpret_cast<const float4*>(row + 4 * g);
+    m[4 * g] = u.x; m[4 * g + 1] = u.y; m[4 * g + 2] = u.z; m[4 * g + 3] = u.w;
+  }
+  __syncthreads();
+  stage_in(a.x_t, xt);
+  __syncthreads();
+  if (a.mean_type == 1) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const float4 u = *reinterpret_cast<const float4*>(row + 4 * g);
+      const float xq[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = 4 * g + k;
+        m[q] = sb(mr(cf[q * bs + 3], xq[k]), mr(cf[q * bs + 4], m[q]));
+      }
+    }
+  }
+  float pred[64];
+  if (a.clip_denoised) {
+    float img[64];
+    wav2_inv(m, img);
+#pragma unroll
+    for (int q = 0; q < 64; ++q) img[q] = fminf(fmaxf(img[q], 0.0f), 1.0f);
+    wav2_fwd(img, pred);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 64; ++q) pred[q] = m[q];
+  }
+  const bool noisy = a.update != 1 && t != 0 && a.noise_philox;
+  // x_{t-1} over the x_t row (each thread owns its row)
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const float4 u = *reinterpret_cast<const float4*>(row + 4 * g);
+    const float xq[4] = {u.x, u.y, u.z, u.w};
+    float nq[4] = {0.f, 0.f, 0.f, 0.f};
+    if (noisy) philox_normal4(a.noise_seed, v, b, t, g, nq);
+    float r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = 4 * g + k;
+      const float* c = cf + q * bs;
+      if (a.update == 1) {
+        const float eps = __fdiv_rn(sb(mr(c[3], xq[k]), pred[q]), c[4]);
+        r[k] = ad(mr(pred[q], c[5]), mr(c[6], eps));
+      } else {
+        r[k] = ad(mr(c[0], pred[q]), mr(c[1], xq[k]));
+        if (noisy) r[k] = ad(r[k], mr(c[2], nq[k]));
+      }
+    }
+    *reinterpret_cast<float4*>(row + 4 * g) = make_float4(r[0], r[1], r[2], r[3]);
+  }
+  __syncthreads();
+  // rows out: x_prev (fp32) and the mirror (the next step's U-Net input channels)
+#pragma unroll 4
+  for (int k = 0; k < S2V / 16; ++k) {
+    const int lv = 16 * k + (tid >> 4), g = tid & 15;
+    const int64_t j = i0 + lv;
+    if (j >= total) continue;
+    const int64_t bb = j / nvox, vv = j - bb * nvox;
+    const float4 u = *reinterpret_cast<const float4*>(tile + lv * S2P + 4 * g);
+    *reinterpret_cast<float4*>(a.x_prev + bb * xp.b + vv * xp.v + 4 * g) = u;
+    if (a.mirror) {
+      MirT* o = reinterpret_cast<MirT*>(a.mirror) + bb * mi.b + vv * mi.v + 4 * g;
+      if constexpr (sizeof(MirT) == 2) {
+        uint2 q2;
+        q2.x = pack2<MirT>(u.x, u.y);
+        q2.y = pack2<MirT>(u.z, u.w);
+        *reinterpret_cast<uint2*>(o) = q2;
+      } else {
+        *reinterpret_cast<float4*>(o) = u;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 int sampler2_launch(const cwdm_sampler_args* a, hipStream_t s) {
@@ -285,6 +404,27 @@ int sampler2_launch(const cwdm_sampler_args* a, hipStream_t s) {
   if (ok(a->pred_xstart, px, 4)) vec |= 16;
   if (a->mirror && mi.c == 1 && ((uintptr_t)a->mirror % 8) == 0 && (mi.b * mesz) % 8 == 0 && (mi.v * mesz) % 8 == 0)
     vec |= 32;
+  // the staged kernel: every tensor channels-last (channel stride 1), 16-byte
+  // aligned rows, Philox noise (or none), no pred_xstart output
+  static const bool lds_on = [] { const char* e = std::getenv("CWDM_SAMPLER2_LDS"); return !(e && e[0] == '0'); }();
+  const bool mir_ok = !a->mirror || ((vec & 32) && (a->mirror_dtype == CWDM_F32 ? ok(a->mirror, mi, 4) : true));
+  if (lds_on && (vec & 7) == 7 && !a->pred_xstart && !a->noise && mir_ok) {
+    const dim3 g2((unsigned)ceil_div(a->B * a->d * a->h * a->w, S2V));
+    const size_t sm = (size_t)S2V * S2P * 4;
+    auto go = [&](auto k) -> int {
+      CWDM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+      hipLaunchKernelGGL(k, g2, dim3(256), sm, s, *a, mo, xt, xp, mi);
+      return (int)CWDM_OK;
+    };
+    int rc;
+    if (a->mirror && a->mirror_dtype == CWDM_BF16) rc = go(sampler2_lds_kernel<bf16_t>);
+    else if (a->mirror && a->mirror_dtype == CWDM_F16) rc = go(sampler2_lds_kernel<f16_t>);
+    else if (!a->mirror || a->mirror_dtype == CWDM_F32) rc = go(sampler2_lds_kernel<float>);
+    else return fail(CWDM_E_INVALID, "cwdm_sampler_step: bad mirror dtype");
+    if (rc) return rc;
+    CWDM_LAUNCHED();
+    return CWDM_OK;
+  }
   const dim3 grid((unsigned)ceil_div(a->B * a->d * a->h * a->w, 256));
   if (a->mirror && a->mirror_dtype == CWDM_BF16)
     hipLaunchKernelGGL(sampler2_kernel<bf16_t>, grid, dim3(256), 0, s, *a, mo, xt, xp, nz, px, mi, vec);

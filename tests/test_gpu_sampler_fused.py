@@ -191,3 +191,46 @@ def test_fused_graph_loop_equals_eager_and_is_seeded(dtype):
     # one flipped rounding grows through the U-Net (bf16: 0.15 after 12 steps)
     err = float((tensor_path[0] - eager[0]).abs().max())
     assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("mirror", [None, "bf16", "fp16"])
+@pytest.mark.parametrize("clip,mean_type,per_band,update", [(True, 0, True, 0), (False, 1, False, 0),
+                                                           (True, 0, False, 1)])
+def test_sampler2_staged_kernel_equals_strided(clip, mean_type, per_band, update, mirror):
+    """Levels 2 with channels-last model_out / x_t / x_prev and Philox noise runs
+    the LDS-staged kernel (sampler2_lds_kernel: whole 256-byte rows per 16-lane
+    group); NCDHW strides run the per-voxel kernel.  Same expressions in the same
+    order: bit-identical outputs, a partial last workgroup, two batch entries
+    (t = 0 draws no noise), and the 16-bit mirror equal to x_prev rounded."""
+    from cwdm_hip import ops
+    from guided_diffusion import script_util
+    shift = [-1.0 + 0.15 * k for k in range(15)] if per_band else None
+    diff = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=(mean_type == 0), mode="i2i",
+                                                 wavelet_levels=2, band_log_snr_shift=shift)
+    g = torch.Generator().manual_seed(21)
+    B, C, d, h, w = 2, 64, 5, 6, 7          # 210 voxels per entry: one partial workgroup of 256
+    mo = (torch.rand(B, C, d, h, w, generator=g) * 0.4).to(DEV)
+    x = torch.randn(B, C, d, h, w, generator=g).to(DEV)
+    t = torch.tensor([0, 417], device=DEV)
+    coef = diff.coef_table(DEV, 0.3 if update else 0.0)
+    seed = 0x5151_2A2A_77
+    kw = dict(clip_denoised=clip, mean_type=mean_type, update=update, per_band=diff.per_band, levels=2,
+              noise_seed=seed)
+    s = ops.ncdhw_strides(x)
+    ref = torch.full_like(x, float("nan"))
+    ops.sampler_step(mo, s, x, s, ref, s, None, (0, 0, 0), coef, t, diff.num_timesteps, B, d, h, w, **kw)
+    cl = lambda z: z.permute(0, 2, 3, 4, 1).contiguous()
+    V = d * h * w
+    cs = (V * C, 1, C)
+    out = torch.full((B, d, h, w, C), float("nan"), device=DEV)
+    mir, ms = None, (0, 0, 0)
+    if mirror:
+        tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[mirror]
+        mir = torch.zeros(B, d, h, w, 96, device=DEV, dtype=tdt)   # the U-Net input: channels 0..63 of 96
+        ms = (V * 96, 1, 96)
+    ops.sampler_step(cl(mo), cs, cl(x), cs, out, cs, None, (0, 0, 0), coef, t, diff.num_timesteps, B, d, h, w,
+                     mirror=mir, mr_s=ms, **kw)
+    assert torch.equal(out, cl(ref))
+    if mirror:
+        assert torch.equal(mir[..., :64], out.to(mir.dtype))
+        assert mir[..., 64:].abs().max() == 0
