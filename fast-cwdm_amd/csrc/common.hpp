@@ -161,4 +161,16 @@ struct GbwdFuse {
   bool used; int nblk;
 };
 extern thread_local GbwdFuse* g_gbwd;
+
+// the U-Net plan's backward: the SiLU(GroupNorm) backward's apply pass of a
+// skip block's GN1, fused into its 1x1 skip dgrad (pointwise.hip pw_kernel):
+// dx = W_skip^T dY (+ dx) + k0 SiLU'(x sc + sh) du + k1 x + k2, written once
+struct GapplyFuse {
+  const void* x0; const void* x1;  // the GroupNorm input = the skip conv's input (split as the dgrad's outputs)
+  const void* du;                  // [B][V][N] gradient of the SiLU output
+  const float* ss;                 // [B][N][2] scale / shift
+  const float* coef;               // [B][N][4] k0, k1, k2 (gn_bwd_finalize)
+  bool used;
+};
+extern thread_local GapplyFuse* g_gapply;
 }  // namespace cwdm

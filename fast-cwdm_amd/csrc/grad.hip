@@ -612,7 +612,7 @@ int gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const void*
                      const float* mr, const float* gamma, int groups, int64_t B, int64_t d, int64_t h, int64_t w,
                      int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma, float* dbeta, void* ws,
                      int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream, int acc_affine,
-                     const float* pre_part = nullptr, int pre_nblk = 0);
+                     const float* pre_part = nullptr, int pre_nblk = 0, const float** coef_out = nullptr);
 // Fixed-order slice sums of [B][nblk][W2] partial rows -> [B][slices][W2]
 // (the fused GroupNorm-backward partials: one row per dgrad tile, 4096 at
 // 128^3, too many for the single-workgroup gn_bwd_finalize).  Workgroup (slice,
@@ -664,7 +664,8 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
                            const float* ss, const float* mr, const float* gamma, int groups, int64_t B, int64_t d,
                            int64_t h, int64_t w, int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma,
                            float* dbeta, void* ws, int64_t ws_bytes, float* chs, int64_t chs_stride,
-                           cwdm_stream_t stream, int acc_affine, const float* pre_part, int pre_nblk) {
+                           cwdm_stream_t stream, int acc_affine, const float* pre_part, int pre_nblk,
+                           const float** coef_out) {
   CWDM_REQUIRE(!chs || (c1 == 0 && chs_stride >= c0), CWDM_E_UNSUPPORTED,
                "gn_silu_bwd: fused channel sums need one source");
   CWDM_REQUIRE(x0 && du && ss && mr && gamma && dx0 && dgamma && dbeta && ws, CWDM_E_INVALID,
@@ -710,6 +711,13 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
   hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(512), 0, s, pre_part ? pre_part : part,
                      pre_part ? pre_nblk : (int)nb, C, (int)B, gamma, mr, groups, V, coef, dgamma, dbeta, acc_affine);
   CWDM_LAUNCHED();
+  // coef_out: reduce + finalize only; the caller fuses the apply into a
+  // later kernel (cwdm::GapplyFuse) reading coef ([B][C][4]) from the workspace
+  if (coef_out) {
+    CWDM_REQUIRE(!chs, CWDM_E_INVALID, "gn_silu_bwd: deferred apply with channel sums");
+    *coef_out = coef;
+    return CWDM_OK;
+  }
   // workgroups of (256 / ncg) voxels x ncg channel groups; two voxels per
   // thread (the kernel's UNR; du_mode 1 loops twice instead); with channel
   // sums at most 1024 workgroups per batch entry (one partial row each, summed

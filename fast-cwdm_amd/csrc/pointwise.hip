@@ -30,7 +30,11 @@ struct PwParams {
   const float* bias; long long bias_bs;
   void* out; void* out1; int out_c0; int accumulate;
   int nnb;                // 128-channel blocks of N
+  // fused GroupNorm-backward apply (GapplyFuse): gx0 / gx1 split as out / out1
+  const void* gx0; const void* gx1; const void* gdu; const float* gss; const float* gcoef;
 };
+
+thread_local GapplyFuse* g_gapply = nullptr;
 
 namespace {
 
@@ -43,13 +47,36 @@ __device__ __forceinline__ long long pw_widx(int co, int ci, int K, int NT) {
   return ((((long long)ct * (K / CK) + chunk) * NT + n) * 2 + qp) * EPQ + e;
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) pw_kernel(PwParams p) {
+// d/dz SiLU(z) * du as gn_bwd_apply_kernel computes it (grad.hip dsilu)
+__device__ __forceinline__ float pw_dsilu(float z, float du) {
+  const float s = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
+  return du * (s * (1.0f + z * (1.0f - s)));
+}
+
+template <typename T, bool GA>
+__global__ void __launch_bounds__(256, 2) pw_kernel(PwParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const long long vt = blockIdx.x / p.nnb;
   const int nb = blockIdx.x % p.nnb;
   const long long row0 = vt * 256 + wv * 64;       // this wave's first voxel row (over B * V)
   const int n0 = nb * 128;
+  // fused GroupNorm-backward apply (GA): the block's 128 channels' (sc, sh, k0,
+  // k1, k2) for the (at most two) batch entries its 256 rows touch, in LDS
+  __shared__ float gk[2][5][128];
+  const long long b_lo = (vt * 256) / p.V;
+  if (GA) {
+    for (int i = tid; i < 2 * 128; i += 256) {
+      const int bl = i >> 7, cl = i & 127, c = n0 + cl;
+      const long long b = b_lo + bl;
+      if (c < p.N && b * p.V < p.rows) {
+        const float2 ss = *reinterpret_cast<const float2*>(p.gss + (b * p.N + c) * 2);
+        const float4 k = *reinterpret_cast<const float4*>(p.gcoef + (b * p.N + c) * 4);
+        gk[bl][0][cl] = ss.x; gk[bl][1][cl] = ss.y;
+        gk[bl][2][cl] = k.x; gk[bl][3][cl] = k.y; gk[bl][4][cl] = k.z;
+      }
+    }
+    __syncthreads();
+  }
   const int col = lane & 31, kg = lane >> 5;       // MFMA operand lane: column / row 0..31, K half
   const T* w = reinterpret_cast<const T*>(p.w);
   f32x16 acc[2][4];
@@ -107,26 +134,50 @@ __global__ void __launch_bounds__(256) pw_kernel(PwParams p) {
   // dgrads ran at 1.5-2.2 TB/s).  The swaps run on every lane (no divergence
   // around a cross-lane op); only the loads / stores are predicated.
   const bool f8 = p.N % 8 == 0 && (!p.out1 || p.out_c0 % 8 == 0);
+  if (f8) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const long long r = row0 + 32 * j + col;
-    const bool rin = r < p.rows;
-    const int bb = rin ? (int)(r / p.V) : 0;
+    for (int j = 0; j < 2; ++j) {
+      const long long r = row0 + 32 * j + col;
+      const bool rin = r < p.rows;
+      const int bb = rin ? (int)(r / p.V) : 0;
+      const int bl = GA && rin ? (int)(bb - b_lo) : 0;
+      // groups ga = 2 gg, gb = 2 gg + 1 of acc[j][m]: in the accumulator layout
+      // this lane holds channels 8 g + 4 kg + e of both; after the swap, the 8
+      // channels from c.  All of the row's loads first (one memory latency per
+      // row instead of one per 8 channels: the epilogue runs at 1 wave / SIMD)
+      auto chan = [&](int m, int gg) { return n0 + 32 * m + 16 * gg + 8 * kg; };
+      auto optr = [&](int c) -> T* {
+        if (p.out1 && c >= p.out_c0) return reinterpret_cast<T*>(p.out1) + r * (p.N - p.out_c0) + (c - p.out_c0);
+        return reinterpret_cast<T*>(p.out) + r * (p.out1 ? p.out_c0 : p.N) + c;
+      };
+      // (GA: half a row's loads at a time -- the fused apply's registers fit 2 waves / SIMD)
+      constexpr int MB = GA ? 2 : 4;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      if (f8) {
+      for (int m0 = 0; m0 < 4; m0 += MB) {
+      u32x4 qo[4][2], qx[4][2], qd[4][2];
+#pragma unroll
+      for (int m = m0; m < m0 + MB; ++m)
 #pragma unroll
         for (int gg = 0; gg < 2; ++gg) {
-          // groups ga = 2 gg, gb = 2 gg + 1; in the accumulator layout this lane holds
-          // channels 8 g + 4 kg + e of both; after the swap, the 8 channels from c
-          const int ga = 2 * gg, gb = 2 * gg + 1;
-          const int c = n0 + 32 * m + 16 * gg + 8 * kg;
+          const int c = chan(m, gg);
           const bool ok = rin && c < p.N;
-          T* o = nullptr;
-          if (ok) {
-            if (p.out1 && c >= p.out_c0) o = reinterpret_cast<T*>(p.out1) + r * (p.N - p.out_c0) + (c - p.out_c0);
-            else o = reinterpret_cast<T*>(p.out) + r * (p.out1 ? p.out_c0 : p.N) + c;
+          qo[m][gg] = qx[m][gg] = qd[m][gg] = u32x4{0u, 0u, 0u, 0u};
+          if (ok && p.accumulate) qo[m][gg] = *reinterpret_cast<const u32x4*>(optr(c));
+          if (GA && ok) {
+            const T* xs = (p.out1 && c >= p.out_c0)
+                              ? reinterpret_cast<const T*>(p.gx1) + r * (p.N - p.out_c0) + (c - p.out_c0)
+                              : reinterpret_cast<const T*>(p.gx0) + r * (p.out1 ? p.out_c0 : p.N) + c;
+            qx[m][gg] = *reinterpret_cast<const u32x4*>(xs);
+            qd[m][gg] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(p.gdu) + r * p.N + c);
           }
+        }
+#pragma unroll
+      for (int m = m0; m < m0 + MB; ++m) {
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          const int ga = 2 * gg, gb = 2 * gg + 1;
+          const int c = chan(m, gg);
+          const bool ok = rin && c < p.N;
           float v[8];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -141,18 +192,39 @@ __global__ void __launch_bounds__(256) pw_kernel(PwParams p) {
               if (8 * gb + 4 * kg + e + n0 + 32 * m < p.N) v[4 + e] += bs[8 * gb + e];
             }
           }
-          if (p.accumulate) {
-            // the existing 8 channels at c, swapped into the accumulator layout (as the
-            // residual of conv3d_v4.hpp's fast epilogue)
-            u32x4 q = u32x4{0u, 0u, 0u, 0u};
-            if (ok) q = *reinterpret_cast<const u32x4*>(o);
+          // 8 channels at c (post-swap layout) -> the accumulator layout (as the
+          // residual of conv3d_v4.hpp's fast epilogue); the swaps run on every lane
+          auto to_acc = [&](const u32x4& q, float (&f)[8]) {
             const auto s0 = __builtin_amdgcn_permlane32_swap(q[0], q[2], false, false);
             const auto s1 = __builtin_amdgcn_permlane32_swap(q[1], q[3], false, false);
             const unsigned g0 = s0[0], g1 = s1[0], h0 = s0[1], h1 = s1[1];
-            v[0] += lo2f<T>(g0); v[1] += hi2f<T>(g0);
-            v[2] += lo2f<T>(g1); v[3] += hi2f<T>(g1);
-            v[4] += lo2f<T>(h0); v[5] += hi2f<T>(h0);
-            v[6] += lo2f<T>(h1); v[7] += hi2f<T>(h1);
+            f[0] = lo2f<T>(g0); f[1] = hi2f<T>(g0); f[2] = lo2f<T>(g1); f[3] = hi2f<T>(g1);
+            f[4] = lo2f<T>(h0); f[5] = hi2f<T>(h0); f[6] = lo2f<T>(h1); f[7] = hi2f<T>(h1);
+          };
+          if (p.accumulate) {
+            float f[8];
+            to_acc(qo[m][gg], f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += f[e];
+          }
+          if (GA) {
+            // + the GroupNorm-backward apply of the same (voxel, channel)
+            float xv[8], dv[8];
+            to_acc(qx[m][gg], xv);
+            to_acc(qd[m][gg], dv);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int lc = 32 * m + 8 * (h ? gb : ga) + 4 * kg;   // channel - n0 of v[4 h .. 4 h + 3]
+              float4 k[5];
+#pragma unroll
+              for (int t = 0; t < 5; ++t) k[t] = *reinterpret_cast<const float4*>(&gk[bl][t][lc]);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float x = xv[4 * h + e];
+                const float dz = pw_dsilu(x * k[0][e] + k[1][e], dv[4 * h + e]);
+                v[4 * h + e] += k[2][e] * dz + k[3][e] * x + k[4][e];
+              }
+            }
           }
           const unsigned p0 = pack2<T>(v[0], v[1]), p1 = pack2<T>(v[2], v[3]);
           const unsigned p2 = pack2<T>(v[4], v[5]), p3 = pack2<T>(v[6], v[7]);
@@ -160,31 +232,41 @@ __global__ void __launch_bounds__(256) pw_kernel(PwParams p) {
           const auto t1 = __builtin_amdgcn_permlane32_swap(p1, p3, false, false);
           u32x4 w;
           w[0] = t0[0]; w[1] = t1[0]; w[2] = t0[1]; w[3] = t1[1];
-          if (ok) *reinterpret_cast<u32x4*>(o) = w;
+          if (ok) *reinterpret_cast<u32x4*>(optr(c)) = w;
         }
-      } else {
-        if (!rin) continue;
+      }
+      }
+    }
+    return;
+  }
+  if (GA) return;   // (the host takes the fused apply only with f8)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int c = n0 + 32 * m + 8 * g + 4 * kg;   // 4 consecutive channels c .. c+3
-          if (c >= p.N) continue;
-          float v[4];
+  for (int j = 0; j < 2; ++j) {
+    const long long r = row0 + 32 * j + col;
+    if (r >= p.rows) continue;
+    const int bb = (int)(r / p.V);
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            v[e] = acc[j][m][4 * g + e] + (p.bias ? p.bias[(long long)bb * p.bias_bs + c + e] : 0.f);
-          T* o;
-          if (p.out1 && c >= p.out_c0) o = reinterpret_cast<T*>(p.out1) + r * (p.N - p.out_c0) + (c - p.out_c0);
-          else o = reinterpret_cast<T*>(p.out) + r * (p.out1 ? p.out_c0 : p.N) + c;
-          uint2 q;
-          if (p.accumulate) {
-            q = *reinterpret_cast<const uint2*>(o);
-            v[0] += lo2f<T>(q.x); v[1] += hi2f<T>(q.x);
-            v[2] += lo2f<T>(q.y); v[3] += hi2f<T>(q.y);
-          }
-          q.x = pack2<T>(v[0], v[1]);
-          q.y = pack2<T>(v[2], v[3]);
-          *reinterpret_cast<uint2*>(o) = q;
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = n0 + 32 * m + 8 * g + 4 * kg;   // 4 consecutive channels c .. c+3
+        if (c >= p.N) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e] = acc[j][m][4 * g + e] + (p.bias ? p.bias[(long long)bb * p.bias_bs + c + e] : 0.f);
+        T* o;
+        if (p.out1 && c >= p.out_c0) o = reinterpret_cast<T*>(p.out1) + r * (p.N - p.out_c0) + (c - p.out_c0);
+        else o = reinterpret_cast<T*>(p.out) + r * (p.out1 ? p.out_c0 : p.N) + c;
+        uint2 q;
+        if (p.accumulate) {
+          q = *reinterpret_cast<const uint2*>(o);
+          v[0] += lo2f<T>(q.x); v[1] += hi2f<T>(q.x);
+          v[2] += lo2f<T>(q.y); v[3] += hi2f<T>(q.y);
         }
+        q.x = pack2<T>(v[0], v[1]);
+        q.y = pack2<T>(v[2], v[3]);
+        *reinterpret_cast<uint2*>(o) = q;
       }
     }
   }
@@ -202,6 +284,13 @@ bool pw_eligible(const cwdm_conv3d_desc* d) {
   return d->B * d->D * d->H * d->W < (1LL << 40);
 }
 
+bool head_eligible(const cwdm_conv3d_desc* d);
+// the skip dgrad d runs pw_kernel and can take a GapplyFuse (the conditions pw_forward checks)
+bool pw_gapply_ok(const cwdm_conv3d_desc* d) {
+  return !head_eligible(d) && pw_eligible(d) && d->cout % 8 == 0 && (!d->out1 || d->out_c0 % 8 == 0) &&
+         d->D * d->H * d->W >= 256 && !d->bias;
+}
+
 int pw_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   PwParams p{};
   p.V = d->D * d->H * d->W;
@@ -214,11 +303,23 @@ int pw_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   p.bias = d->bias; p.bias_bs = d->bias_bstride;
   p.out = d->out; p.out1 = d->out1; p.out_c0 = d->out_c0; p.accumulate = d->accumulate;
   p.nnb = (int)ceil_div(d->cout, 128);
+  if (g_gapply && !g_gapply->used && p.N % 8 == 0 && (!d->out1 || d->out_c0 % 8 == 0) && p.V >= 256 &&
+      !d->bias) {
+    p.gx0 = g_gapply->x0; p.gx1 = g_gapply->x1; p.gdu = g_gapply->du;
+    p.gss = g_gapply->ss; p.gcoef = g_gapply->coef;
+    g_gapply->used = true;
+  }
   const long long nblk = ceil_div(p.rows, 256) * p.nnb;
   CWDM_REQUIRE(nblk < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d (pointwise): grid too large");
   prof_begin(s);
-  if (d->dtype == CWDM_F16) hipLaunchKernelGGL(pw_kernel<f16_t>, dim3((unsigned)nblk), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(pw_kernel<bf16_t>, dim3((unsigned)nblk), dim3(256), 0, s, p);
+  const bool ga = p.gdu != nullptr;
+  if (d->dtype == CWDM_F16) {
+    if (ga) hipLaunchKernelGGL((pw_kernel<f16_t, true>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((pw_kernel<f16_t, false>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+  } else {
+    if (ga) hipLaunchKernelGGL((pw_kernel<bf16_t, true>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((pw_kernel<bf16_t, false>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+  }
   prof_end(s, 2.0 * p.rows * (double)p.N * p.K);
   CWDM_LAUNCHED();
   return CWDM_OK;

@@ -29,8 +29,9 @@ int gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const void*
                      const float* mr, const float* gamma, int groups, int64_t B, int64_t d, int64_t h, int64_t w,
                      int dtype, void* dx0, int acc0, void* dx1, int acc1, float* dgamma, float* dbeta, void* ws,
                      int64_t ws_bytes, float* chs, int64_t chs_stride, cwdm_stream_t stream, int acc_affine,
-                     const float* pre_part = nullptr, int pre_nblk = 0);
+                     const float* pre_part = nullptr, int pre_nblk = 0, const float** coef_out = nullptr);
 int gb_part_reduce(const float* part, int nblk, int C, int64_t B, int slices, float* out, hipStream_t s);
+bool pw_gapply_ok(const cwdm_conv3d_desc* d);
 int haar_nd_synth_add(int dtype, int64_t B, int64_t d, int64_t h, int64_t w, int C, const void* L, int64_t l_vs,
                       float lll, const void* H, int64_t h_vs, float high, void* fine, int acc, hipStream_t s);
 int haar_nd_anal_add(int dtype, int64_t B, int64_t d, int64_t h, int64_t w, int C, const void* fine, void* L,
@@ -1633,18 +1634,11 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
         return rc;
       if ((rc = wgrad_c(bk.c2, lout, act(h1), cout, nullptr, 0, 0, ss_of(bk.g2), grd(o), cout, cout, GR(c2.w_p))))
         return rc;
-      if (c2.ws_p >= 0) {
+      // 1x1 skip dgrad into dx0 / dx1 (dual output); with skip_gapply the
+      // GroupNorm-1 backward's apply pass rides in its epilogue (GapplyFuse),
+      // so it runs after GN1's reduce / finalize below
+      auto skip_dgrad = [&](cwdm::GapplyFuse* gf, bool dry) -> int {
         const int c0 = u->tensors[c2.sb0].channels, cc1 = c2.sb1 >= 0 ? u->tensors[c2.sb1].channels : 0;
-        if ((rc = wgrad(lout, 1, act(c2.sb0), c0, act(c2.sb1), cc1, 0, nullptr, grd(o), cout, cout, GR(c2.ws_p))))
-          return rc;
-        // 1x1 dgrad into dx0 / dx1 (dual output); equalise the store/accumulate state
-        int a0 = take_acc(c2.sb0), a1 = c2.sb1 >= 0 ? take_acc(c2.sb1) : a0;
-        if (a0 != a1) {
-          const int zid = a0 ? c2.sb1 : c2.sb0;
-          const auto& zt = u->tensors[zid];
-          CWDM_HIP(hipMemsetAsync(grd(zid), 0, B * vox(zt.level) * zt.channels * es, s));
-          a0 = a1 = 1;
-        }
         cwdm_conv3d_desc d{};
         d.dtype = dt; d.B = B; d.D = D >> lout; d.H = H >> lout; d.W = W >> lout;
         d.cout = c0 + cc1;
@@ -1652,9 +1646,32 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
         d.res_mode = -1;
         d.out = grd(c2.sb0); d.out_dtype = dt;
         if (c2.sb1 >= 0) { d.out1 = grd(c2.sb1); d.out_c0 = c0; }
+        if (dry) return pw_gapply_ok(&d) ? 1 : 0;
+        // equalise the store/accumulate state of the two outputs
+        int a0 = take_acc(c2.sb0), a1 = c2.sb1 >= 0 ? take_acc(c2.sb1) : a0;
+        if (a0 != a1) {
+          const int zid = a0 ? c2.sb1 : c2.sb0;
+          const auto& zt = u->tensors[zid];
+          CWDM_HIP(hipMemsetAsync(grd(zid), 0, B * vox(zt.level) * zt.channels * es, s));
+          a0 = a1 = 1;
+        }
         d.accumulate = a0;
         d.workspace = gb + G.split; d.ws_bytes = G.split_bytes;
-        if ((rc = cwdm_conv3d_forward(&d, stream))) return rc;
+        cwdm::g_gapply = gf;
+        const int r = cwdm_conv3d_forward(&d, stream);
+        cwdm::g_gapply = nullptr;
+        if (r) return r;
+        CWDM_REQUIRE(!gf || gf->used, CWDM_E_UNSUPPORTED, "train plan: skip dgrad did not take the fused apply");
+        return CWDM_OK;
+      };
+      static const bool gapply_on = [] { const char* e = std::getenv("CWDM_GAPPLY_FUSE"); return !(e && e[0] == '0'); }();
+      const bool skip_gapply = c2.ws_p >= 0 && gapply_on && bk.updown == 0 && c2.sb0 == bk.x0 &&
+                               c2.sb1 == bk.x1 && skip_dgrad(nullptr, true) == 1;
+      if (c2.ws_p >= 0) {
+        const int c0 = u->tensors[c2.sb0].channels, cc1 = c2.sb1 >= 0 ? u->tensors[c2.sb1].channels : 0;
+        if ((rc = wgrad(lout, 1, act(c2.sb0), c0, act(c2.sb1), cc1, 0, nullptr, grd(o), cout, cout, GR(c2.ws_p))))
+          return rc;
+        if (!skip_gapply && (rc = skip_dgrad(nullptr, false))) return rc;
       } else {
         // identity residual (possibly through the block's resampling)
         const int xt = bk.x0;
@@ -1706,6 +1723,21 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
         if ((rc = dgrad_gn(bk.c1, grd(h1), bk.g1, bk.x0, bk.x1, pre1))) return rc;
       } else if ((rc = dgrad(bk.c1, grd(h1)))) {
         return rc;
+      }
+      if (skip_gapply) {
+        // GN1 reduce / finalize, then the skip dgrad applying it: dx = skip + GN1 backward
+        const auto& g = u->gns[bk.g1];
+        const int c0 = u->tensors[bk.x0].channels, cc1 = bk.x1 >= 0 ? u->tensors[bk.x1].channels : 0;
+        const float* coef = nullptr;
+        if ((rc = gn_silu_bwd_impl(act(bk.x0), c0, act(bk.x1), cc1, tmp, 0, ss_of(bk.g1), mr_of(bk.g1),
+                                   P(g.gamma_off), u->cfg.num_groups, B, D >> lout, H >> lout, W >> lout, dt,
+                                   grd(bk.x0), 0, grd(bk.x1), 0, GR(g.gamma_p), GR(g.beta_p), gb + G.gnws,
+                                   G.gnws_bytes, nullptr, 0, stream, 1, pre1.part, pre1.nblk, &coef)))
+          return rc;
+        cwdm::GapplyFuse gf{};
+        gf.x0 = act(bk.x0); gf.x1 = act(bk.x1); gf.du = tmp; gf.ss = ss_of(bk.g1); gf.coef = coef;
+        if ((rc = skip_dgrad(&gf, false))) return rc;
+        continue;
       }
       if ((rc = gn_bwd(bk.g1, bk.x0, bk.x1, bk.updown == 1 ? 1 : (bk.updown == 2 ? 2 : 0), &pre1))) return rc;
       continue;
