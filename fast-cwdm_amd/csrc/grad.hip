@@ -162,27 +162,28 @@ __global__ void __launch_bounds__(256) gn_bwd_reduce_kernel(const T* __restrict_
   }
 }
 
-__global__ void __launch_bounds__(512) gn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C,
+// One workgroup per group g (all batch entries in order): the group's channels'
+// partial sums over the nblk blocks (sub threads per channel, 8 loads in flight
+// each, fixed order), the group terms, the apply coefficients and dgamma /
+// dbeta.  (One workgroup for all channels ran 10 us per call, 71 calls per
+// training step.)
+__global__ void __launch_bounds__(256) gn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C,
                                                              int B, const float* __restrict__ gamma,
                                                              const float* __restrict__ mr, int groups,
                                                              long long V, float* __restrict__ coef,
                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                              int acc_affine) {
-  __shared__ double sA[1024], sB[1024], s1[256], s2[256], rA[512], rB[512];
-  const int cpg = C / groups;
-  // C <= 512: `sub` threads per channel split the partial blocks; C > 512: 2 channels per thread
-  const int sub = C <= 512 ? 512 / C : 1;
-  const int cpt = C <= 512 ? 1 : 2;
-  double dg[2] = {0.0, 0.0}, db[2] = {0.0, 0.0};
+  __shared__ double rA[256], rB[256], cA[1024], cB[1024], dG[1024], dB[1024], gs[2];
+  const int g = blockIdx.x, cpg = C / groups, c0 = g * cpg;
+  const int t = threadIdx.x;
+  for (int c = t; c < cpg; c += 256) { dG[c] = 0.0; dB[c] = 0.0; }
   for (int b = 0; b < B; ++b) {
-    for (int k = 0; k < cpt; ++k) {
-      const int c = cpt == 1 ? threadIdx.x % C : threadIdx.x + 512 * k;
-      const int j = cpt == 1 ? threadIdx.x / C : 0;
+    for (int w0 = 0; w0 < cpg; w0 += 256) {
+      const int cw = min(256, cpg - w0), sub = 256 / cw;
+      const int cl = t % cw, j = t / cw;
       double a = 0.0, bb = 0.0;
-      if (c < C && j < sub) {
-        // 8 partial blocks' loads in flight per trip (one at a time left this
-        // single-workgroup pass latency-bound: ~50 us at 128^3 x 64 channels)
-        const float2* pc = reinterpret_cast<const float2*>(part + ((long long)b * nblk * C + c) * 2);
+      if (j < sub) {
+        const float2* pc = reinterpret_cast<const float2*>(part + ((long long)b * nblk * C + c0 + w0 + cl) * 2);
         int i = j;
         for (; i + 7 * sub < nblk; i += 8 * sub) {
           float2 v[8];
@@ -197,55 +198,42 @@ __global__ void __launch_bounds__(512) gn_bwd_finalize_kernel(const float* __res
           bb += (double)v.y;
         }
       }
-      if (cpt == 1) {
-        rA[threadIdx.x] = a; rB[threadIdx.x] = bb;
-      } else if (c < C) {
-        sA[c] = a; sB[c] = bb;
+      rA[t] = a; rB[t] = bb;
+      __syncthreads();
+      if (t < cw) {
+        double sa = 0.0, sb = 0.0;
+        for (int k = 0; k < sub; ++k) { sa += rA[k * cw + t]; sb += rB[k * cw + t]; }
+        cA[w0 + t] = sa; cB[w0 + t] = sb;
+        dG[w0 + t] += sb; dB[w0 + t] += sa;
       }
+      __syncthreads();
     }
-    __syncthreads();
-    if (cpt == 1 && threadIdx.x < C) {
+    if (t == 0) {
       double a = 0.0, bb = 0.0;
-      for (int j = 0; j < sub; ++j) {
-        a += rA[j * C + threadIdx.x];
-        bb += rB[j * C + threadIdx.x];
+      for (int c = 0; c < cpg; ++c) {
+        a += (double)gamma[c0 + c] * cA[c];
+        bb += (double)gamma[c0 + c] * cB[c];
       }
-      sA[threadIdx.x] = a; sB[threadIdx.x] = bb;
-    }
-    __syncthreads();
-    for (int k = 0; k < 2; ++k) {
-      const int c = threadIdx.x + 512 * k;
-      if (c < C) { dg[k] += sB[c]; db[k] += sA[c]; }
-    }
-    if (threadIdx.x < groups) {
-      const int g = threadIdx.x;
-      double a = 0.0, bb = 0.0;
-      for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
-        a += (double)gamma[c] * sA[c];
-        bb += (double)gamma[c] * sB[c];
-      }
-      s1[g] = a; s2[g] = bb;
+      gs[0] = a; gs[1] = bb;
     }
     __syncthreads();
     const double N = (double)cpg * (double)V;
-    for (int c = threadIdx.x; c < C; c += 512) {
-      const int g = c / cpg;
-      const double mu = mr[((long long)b * groups + g) * 2], rs = mr[((long long)b * groups + g) * 2 + 1];
-      const double k1 = rs * gamma[c];
-      const double k2 = -rs * rs * s2[g] / N;
-      const double k3 = -rs * s1[g] / N + rs * rs * s2[g] * mu / N;
-      coef[((long long)b * C + c) * 4 + 0] = (float)k1;
-      coef[((long long)b * C + c) * 4 + 1] = (float)k2;
-      coef[((long long)b * C + c) * 4 + 2] = (float)k3;
+    const double mu = mr[((long long)b * groups + g) * 2], rs = mr[((long long)b * groups + g) * 2 + 1];
+    for (int c = t; c < cpg; c += 256) {
+      const double k1 = rs * gamma[c0 + c];
+      const double k2 = -rs * rs * gs[1] / N;
+      const double k3 = -rs * gs[0] / N + rs * rs * gs[1] * mu / N;
+      coef[((long long)b * C + c0 + c) * 4 + 0] = (float)k1;
+      coef[((long long)b * C + c0 + c) * 4 + 1] = (float)k2;
+      coef[((long long)b * C + c0 + c) * 4 + 2] = (float)k3;
     }
     __syncthreads();
   }
-  for (int k = 0; k < 2; ++k) {
-    const int c = threadIdx.x + 512 * k;
-    if (c < C) {   // acc_affine: a GroupNorm whose parameters serve two calls (WavUNetModel's reused blocks)
-      dgamma[c] = acc_affine ? dgamma[c] + (float)dg[k] : (float)dg[k];
-      dbeta[c] = acc_affine ? dbeta[c] + (float)db[k] : (float)db[k];
-    }
+  for (int c = t; c < cpg; c += 256) {
+    // acc_affine: a GroupNorm whose parameters serve two calls (WavUNetModel's reused blocks)
+    const int cc = c0 + c;
+    dgamma[cc] = acc_affine ? dgamma[cc] + (float)dG[c] : (float)dG[c];
+    dbeta[cc] = acc_affine ? dbeta[cc] + (float)dB[c] : (float)dB[c];
   }
 }
 
@@ -708,7 +696,7 @@ int cwdm::gn_silu_bwd_impl(const void* x0, int c0, const void* x1, int c1, const
          return CWDM_OK;
        })))
     return rc;
-  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(512), 0, s, pre_part ? pre_part : part,
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3((unsigned)groups), dim3(256), 0, s, pre_part ? pre_part : part,
                      pre_part ? pre_nblk : (int)nb, C, (int)B, gamma, mr, groups, V, coef, dgamma, dbeta, acc_affine);
   CWDM_LAUNCHED();
   // coef_out: reduce + finalize only; the caller fuses the apply into a
