@@ -563,10 +563,14 @@ int dispatch_mode(int mode, F&& f) {
 // voxel slots per workgroup) where that stays below 512 blocks -- the small
 // levels ran 1-8 workgroups looping over 512 voxels each (35-70 us per call at
 // 16^3 / 8^3, latency-bound) -- else 512 blocks
+// reduce-pass workgroups per batch entry: at most 1024 (R0's 64-channel
+// reduce at 2 M voxels: 132 us with 512 = 8 waves per CU, 114 us with 1024;
+// 2048 no better, profiles/r03/i_gnb_cap.txt)
 long long gn_bwd_blocks(int C, long long V) {
+  static const long long cap = [] { const char* e = std::getenv("CWDM_GNB_CAP"); return e ? std::atoll(e) : 1024LL; }();
   const long long slots = std::max(1, 256 / std::max(1, C / 8));
   long long nb = ceil_div(V, 4 * slots);
-  if (nb > 512) nb = 512;
+  if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;
   return nb;
 }
