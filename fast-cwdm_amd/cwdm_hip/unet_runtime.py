@@ -74,15 +74,23 @@ class UNetPlan:
     def packed_bytes(self):
         return int(lib().cwdm_unet_packed_bytes(self._h))
 
-    def pack(self, params, packed=None):
-        """params: fp32 contiguous device tensors in param_specs order."""
+    def pointer_array(self, params):
+        """ctypes array of the parameters' device pointers (param_specs order)."""
         if len(params) != len(self.param_specs):
             raise ValueError("parameter count mismatch")
-        _need_cuda(*params)
+        return (ctypes.c_void_p * len(params))(*[p.data_ptr() for p in params])
+
+    def pack(self, params, packed=None, arr=None):
+        """params: fp32 contiguous device tensors in param_specs order (arr: their
+        pointer_array, already checked, when the caller keeps one)."""
+        if len(params) != len(self.param_specs):
+            raise ValueError("parameter count mismatch")
         dev = params[0].device
         if packed is None:
             packed = torch.empty(self.packed_bytes, dtype=torch.uint8, device=dev)
-        arr = (ctypes.c_void_p * len(params))(*[p.data_ptr() for p in params])
+        if arr is None:
+            _need_cuda(*params)
+            arr = self.pointer_array(params)
         check(lib().cwdm_unet_pack(self._h, arr, ctypes.c_void_p(packed.data_ptr()), _stream()), "pack")
         return packed
 
@@ -154,13 +162,14 @@ class UNetPlan:
             n += k
         return n
 
-    def pack_bwd(self, params, packed_bwd=None):
+    def pack_bwd(self, params, packed_bwd=None, arr=None):
         """Transposed/flipped (dgrad) weight layouts; re-run after every update."""
-        _need_cuda(*params)
         if packed_bwd is None:
             packed_bwd = torch.empty(max(int(lib().cwdm_unet_packed_bwd_bytes(self._h)), 1), dtype=torch.uint8,
                                      device=params[0].device)
-        arr = (ctypes.c_void_p * len(params))(*[p.data_ptr() for p in params])
+        if arr is None:
+            _need_cuda(*params)
+            arr = self.pointer_array(params)
         check(lib().cwdm_unet_pack_bwd(self._h, arr, ctypes.c_void_p(packed_bwd.data_ptr()), _stream()), "pack_bwd")
         return packed_bwd
 

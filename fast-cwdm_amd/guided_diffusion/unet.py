@@ -140,6 +140,7 @@ class UNetModel(nn.Module):
         self._packed_key = None
         self._packed_bwd = None
         self._packed_bwd_key = None
+        self._src_ptrs = None      # (data_ptrs, ctypes pointer array) of the fp32 parameter views
         self._grad_hook = None       # called per backward segment (DDP bucket all-reduce)
         self._last_grad_flat = None
         # training forward keeps the DMA-staged convs' activated inputs (more
@@ -244,25 +245,42 @@ class UNetModel(nn.Module):
         params = list(self.parameters())
         key = self._weights_key()
         if self._packed is None or self._packed_key != key:
-            ops._need_cuda(*params)
-            flat = [p.detach().float().contiguous() for p in params]
+            arr = self._src_array(params, key)
+            flat = params if arr is not None else [p.detach().float().contiguous() for p in params]
             # re-pack in place (stream-ordered after earlier readers; a captured
             # sampling graph keeps a valid pointer; the plan's batched pack job
             # table stays cached when no pointer moved)
             old = self._packed if (self._packed is not None and self._packed.device == flat[0].device) else None
-            self._packed = self.plan.pack(flat, packed=old)
+            self._packed = self.plan.pack(flat, packed=old, arr=arr)
             self._packed_key = key
         return self._packed
+
+    def _src_array(self, params, key):
+        """The parameters' pointer array for the packs, cached while no pointer
+        moved: every training step re-packs, and building the per-parameter
+        views and the array each time cost ~1 ms of host time per step, during
+        which the GPU idled.  None when a parameter is not an fp32 contiguous
+        CUDA tensor (the pack then reads converted copies)."""
+        ptrs = tuple(k[0] for k in key[3:])
+        if self._src_ptrs is not None and self._src_ptrs[0] == ptrs:
+            return self._src_ptrs[1]
+        ops._need_cuda(*params)
+        if not all(p.dtype == th.float32 and p.is_contiguous() for p in params):
+            return None
+        arr = self.plan.pointer_array(params)
+        self._src_ptrs = (ptrs, arr)
+        return arr
 
     def packed_bwd_weights(self):
         """Transposed/flipped dgrad weight layouts for the native backward."""
         params = list(self.parameters())
         key = self._weights_key()
         if self._packed_bwd is None or self._packed_bwd_key != key:
-            ops._need_cuda(*params)
+            arr = self._src_array(params, key)
             old = self._packed_bwd if (self._packed_bwd is not None and
                                        self._packed_bwd.device == params[0].device) else None
-            self._packed_bwd = self.plan.pack_bwd([p.detach() for p in params], packed_bwd=old)
+            src = params if arr is not None else [p.detach() for p in params]
+            self._packed_bwd = self.plan.pack_bwd(src, packed_bwd=old, arr=arr)
             self._packed_bwd_key = key
         return self._packed_bwd
 
