@@ -112,7 +112,10 @@ class GradBucketReducer:
     def timeline(self):
         """(backward_end_ms, [(ready_ms, start_ms, end_ms) per bucket]) relative
         to the end of the first backward segment; synchronises.  A bucket whose
-        start precedes backward_end ran beside the backward."""
+        start precedes backward_end ran beside the backward.  None when no
+        backward was timed (timing off, or world size 1 without force)."""
+        if getattr(self, "_t0", None) is None or getattr(self, "_bwd_end", None) is None:
+            return None
         torch.cuda.synchronize()
         ms = lambda e: self._t0.elapsed_time(e)  # noqa: E731
         return ms(self._bwd_end), [(ms(r), ms(s), ms(e)) for r, s, e in self._events]

@@ -29,6 +29,9 @@ class FlatAdamW(torch.optim.Optimizer):
         if o != flat.numel():
             raise ValueError("FlatAdamW: flat buffer / parameter size mismatch")
         self._model = model
+        # the model's backward then hands its flat gradient buffer over as the
+        # parameters' .grad views (no per-parameter copies; flat_grad() is that buffer)
+        model.direct_grads = True
         self._flat = flat
         self._m = torch.zeros_like(flat)
         self._v = torch.zeros_like(flat)

@@ -86,7 +86,9 @@ class UNetPlan:
         if len(params) != len(self.param_specs):
             raise ValueError("parameter count mismatch")
         dev = params[0].device
-        if packed is None:
+        # a buffer passed in is reused only when it holds this plan's layout
+        # (the packed size depends on the compute dtype)
+        if packed is None or packed.numel() < self.packed_bytes:
             packed = torch.empty(self.packed_bytes, dtype=torch.uint8, device=dev)
         if arr is None:
             _need_cuda(*params)
@@ -162,11 +164,15 @@ class UNetPlan:
             n += k
         return n
 
+    @property
+    def packed_bwd_bytes(self):
+        return max(int(lib().cwdm_unet_packed_bwd_bytes(self._h)), 1)
+
     def pack_bwd(self, params, packed_bwd=None, arr=None):
         """Transposed/flipped (dgrad) weight layouts; re-run after every update."""
-        if packed_bwd is None:
-            packed_bwd = torch.empty(max(int(lib().cwdm_unet_packed_bwd_bytes(self._h)), 1), dtype=torch.uint8,
-                                     device=params[0].device)
+        need = self.packed_bwd_bytes
+        if packed_bwd is None or packed_bwd.numel() < need:
+            packed_bwd = torch.empty(need, dtype=torch.uint8, device=params[0].device)
         if arr is None:
             _need_cuda(*params)
             arr = self.pointer_array(params)

@@ -86,6 +86,9 @@ class TrainLoop:
             self.opt = FlatAdamW(self.model, lr=self.lr, weight_decay=self.weight_decay)
             self.reducer = GradBucketReducer() if self.world_size > 1 else None
             self.model._grad_hook = self.reducer
+            # gradients land as views of the flat buffer straight in .grad
+            # (FlatAdamW reads the flat buffer; autograd would clone each view)
+            self.model.direct_grads = True
         else:
             self.opt = th.optim.AdamW(self.model.parameters(), lr=self.lr, weight_decay=self.weight_decay)
             self.reducer = None
@@ -186,7 +189,10 @@ class TrainLoop:
         if self.grad_scaler.is_enabled():
             self.grad_scaler.step(self.opt)     # skipped when the unscaled gradients are not finite
             self.grad_scaler.update()
-            info["scale"] = self.grad_scaler.get_scale()
+            # the scale tensor itself: get_scale() reads it back (.item()), a host
+            # sync per step that the deferred finite check exists to avoid
+            sc = getattr(self.grad_scaler, "_scale", None)
+            info["scale"] = sc.detach().clone() if sc is not None else self.grad_scaler.get_scale()
         else:
             self.opt.step()
         self._anneal_lr()

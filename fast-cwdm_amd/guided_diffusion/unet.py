@@ -146,6 +146,10 @@ class UNetModel(nn.Module):
         # training forward keeps the DMA-staged convs' activated inputs (more
         # workspace, no GroupNorm+SiLU recompute in the weight gradients)
         self.keep_activations = True
+        # backward assigns .grad = views of the flat gradient buffer directly
+        # (TrainLoop turns it on); off, the views are returned to autograd, so
+        # torch.autograd.grad and backward(inputs=...) behave as usual
+        self.direct_grads = False
         self._flatten_params()
 
     # ---- flat parameter storage ---------------------------------------------
@@ -222,7 +226,9 @@ class UNetModel(nn.Module):
 
     def set_compute_dtype(self, dtype):
         self.compute_dtype = dtype
-        self._packed = None
+        # both packed layouts are per dtype (the plan's packed sizes differ)
+        self._packed = self._packed_bwd = None
+        self._packed_key = self._packed_bwd_key = None
         return self
 
     def mark_params_changed(self):
@@ -397,10 +403,10 @@ class _UNetTrain(th.autograd.Function):
             hook(None, grads, 0, grads.numel())
         del ws, gws
         model._last_grad_flat = grads
-        # a parameter without a gradient gets its view of the flat buffer as
-        # .grad directly (autograd would clone each returned view: ~230 copies per
-        # step); one that already has one (gradient accumulation) gets the view
-        # returned and added by autograd as usual
+        # with direct_grads, a parameter without a gradient gets its view of the
+        # flat buffer as .grad directly (autograd would clone each returned view:
+        # ~230 copies per step); otherwise (or with a gradient already there:
+        # accumulation) the view is returned and autograd handles it as usual
         out = []
         o = 0
         for p, (_, shape) in zip(model.parameters(), plan.param_specs):
@@ -409,7 +415,7 @@ class _UNetTrain(th.autograd.Function):
                 n *= s_
             view = grads[o:o + n].view(shape)
             o += n
-            if p.grad is None and p.requires_grad:
+            if model.direct_grads and p.grad is None and p.requires_grad:
                 p.grad = view
                 out.append(None)
             else:

@@ -457,6 +457,53 @@ def test_unet_backward_segments_and_hook():
         assert rel_err(p.grad, g_all[name]) < 1e-5, name
 
 
+def test_autograd_grad_returns_gradients():
+    """torch.autograd.grad over the native backward returns the gradients and
+    leaves .grad alone (direct .grad hand-over is TrainLoop / FlatAdamW's)."""
+    cfg, G = cases.C1_CFG, cases.C1_GROUPS
+    P = ou.random_params(seed=25, **cfg)
+    g = torch.Generator().manual_seed(26)
+    x = torch.randn(1, 32, 16, 16, 16, generator=g)
+    t = torch.tensor([17])
+    R = torch.randn(1, 8, 16, 16, 16, generator=g)
+    _, g_all, _ = _unet_grads(cfg, G, P, x, t, R, "fp32")
+    model = _product_model(cfg, G, P, "fp32")
+    names, params = zip(*model.named_parameters())
+    out = model(x.to(DEV), t.to(DEV))
+    grads = torch.autograd.grad((out * R.to(DEV)).sum(), params)
+    assert all(p.grad is None for p in params)
+    for n, gr in zip(names, grads):
+        assert gr is not None and rel_err(gr, g_all[n]) < 1e-5, n
+
+
+def test_train_switch_dtype_then_train_again():
+    """Packed buffers are per dtype: bf16 training, then fp32 training on the
+    same model re-packs into buffers of the fp32 size (no out-of-bounds pack)."""
+    from cwdm_hip.optim import FlatAdamW
+    cfg, G = cases.C1_CFG, cases.C1_GROUPS
+    P = ou.random_params(seed=27, **cfg)
+    g = torch.Generator().manual_seed(28)
+    x = torch.randn(1, 32, 16, 16, 16, generator=g).to(DEV)
+    t = torch.tensor([9]).to(DEV)
+    R = torch.randn(1, 8, 16, 16, 16, generator=g).to(DEV)
+    model = _product_model(cfg, G, P, "bf16")
+    opt = FlatAdamW(model, lr=1e-4, weight_decay=0.0)
+    for dt in ("bf16", "fp32"):
+        model.set_compute_dtype(dt)
+        opt.zero_grad()
+        (model(x, t) * R).sum().backward()
+        opt.step()
+        assert model._packed.numel() >= model.plan.packed_bytes
+        assert model._packed_bwd.numel() >= model.plan.packed_bwd_bytes
+    # the fp32 gradients after the switch match a fresh fp32 model at the same weights
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    opt.zero_grad()
+    (model(x, t) * R).sum().backward()
+    _, ref, _ = _unet_grads(cfg, G, sd, x.cpu(), t.cpu(), R.cpu(), "fp32")
+    for n, p in model.named_parameters():
+        assert rel_err(p.grad, ref[n]) < 1e-5, n
+
+
 def _c1_model_and_diffusion(P, dtype="fp32"):
     from guided_diffusion import script_util
     args = script_util.run_sh_model_args(num_channels=32, channel_mult="1,2", num_res_blocks=1, num_groups=8)
