@@ -108,7 +108,8 @@ int64_t src_voxels(const cwdm_conv3d_desc* d) {
 
 }  // namespace
 
-// kernel-path policy (cwdm_conv3d_set_path): 0 auto, 1 legacy only, 2 DMA kernel wherever the shape allows
+// kernel-path policy (cwdm_conv3d_set_path): 0 auto, 1 legacy only, 2 DMA kernels wherever the shape allows,
+// 3 as 2 without the warp-specialised kernel
 std::atomic<int> g_conv_path{[] {
   const char* e = std::getenv("CWDM_CONV_PATH");
   return e ? std::atoi(e) : 0;
@@ -126,6 +127,9 @@ int sg_ksplit(const cwdm_conv3d_desc* d);
 int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, void* partial, hipStream_t s);
 int sg_skip_ksplit(const cwdm_conv3d_desc* d);
 int64_t sg_sync_bytes(int ksplit);
+bool v5_eligible(const cwdm_conv3d_desc* d, bool gn);
+int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
+              const float* agn, const void* res, int rmode, hipStream_t s);
 
 int64_t v4_items(const cwdm_conv3d_desc* d) {
   return d->B * ((d->W + 31) / 32) * (d->H / 4) * (d->D / 4) * (d->cout / 64);
@@ -174,7 +178,7 @@ bool v4_eligible(const cwdm_conv3d_desc* d) {
   // work items: K slices, or (16-bit, no split, < 256 tiles) v4_launch's 32-channel tiles
   const int S = v4_ksplit(d);
   const int64_t items = nblk * S * (S == 1 && dtype_half(d->dtype) && nblk < 256 ? 2 : 1);
-  if (items < std::min<int64_t>(384, v4_ksplit_target()) && path != 2) return false;  // too few work items even K-split: the brick kernels
+  if (items < std::min<int64_t>(384, v4_ksplit_target()) && path < 2) return false;  // too few work items even K-split: the brick kernels
   const int esz = dtype_size(d->dtype);
   const int64_t sv = src_voxels(d);
   // the DMA range check works on 32-bit byte offsets per batch
@@ -255,6 +259,10 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   p.accumulate = d->accumulate;
   p.stamps = g_stamps.load(std::memory_order_relaxed);
   if (sg_eligible(d)) return sg_launch(p, d, partial, s);
+  // the warp-specialised kernel (conv3d_v5.hip) where it applies (not the
+  // backward's fused GroupNorm-reduce dgrad, not the stamps diagnostics build)
+  if (!p.stamps && !(g_gbwd && !g_gbwd->used) && v5_eligible(d, false))
+    return v5_launch(d, a0, c0, a1, c1, a0_cm, nullptr, res, rmode, s);
   const int S = v4_ksplit(d);
   p.ksplit = S;
   p.kper = (p.nch + S - 1) / S;
@@ -380,7 +388,11 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   int c0 = d->a_c0, c1 = d->a_c1;
   int a0_cm = 0;
   int rc;
-  if (d->a_gn) {
+  // GroupNorm + SiLU inside the warp-specialised conv (no activated copy):
+  // inference only -- the training forward keeps the activated input for wgrad
+  const float* agn = nullptr;
+  if (d->a_gn && !g_act_keep && !g_stamps.load(std::memory_order_relaxed) && v5_eligible(d, true)) agn = d->a_gn;
+  if (d->a_gn && !agn) {
     // the activated input: in the workspace, or (training) where the plan keeps
     // it for the backward's DMA-staged wgrad
     void* act = ws;
@@ -413,6 +425,7 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     }
     res = skip; rmode = 0;
   }
+  if (agn) return v5_launch(d, a0, c0, a1, c1, 0, agn, res, rmode, s);
   return v4_launch(d, a0, c0, a1, c1, a0_cm, res, rmode, v4_ksplit(d) > 1 ? ws : nullptr, s);
 }
 
@@ -595,7 +608,7 @@ extern "C" int cwdm_gn_apply(const void* x0, int c0, const void* x1, int c1, con
 }
 
 extern "C" int cwdm_conv3d_set_path(int path) {
-  CWDM_REQUIRE(path >= 0 && path <= 2, CWDM_E_INVALID, "cwdm_conv3d_set_path: path must be 0, 1 or 2");
+  CWDM_REQUIRE(path >= 0 && path <= 3, CWDM_E_INVALID, "cwdm_conv3d_set_path: path must be 0, 1, 2 or 3");
   return g_conv_path.exchange(path);
 }
 

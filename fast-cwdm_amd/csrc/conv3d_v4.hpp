@@ -77,6 +77,8 @@ struct V4Params {
   const void* gx0; const void* gx1; int gc0;
   const float* gss; const float* gmr; int ggroups;
   FastDiv gdiv;
+  // conv3d_v5: GroupNorm scale / shift [B][ac0 + ac1][2] of the raw sources, applied in LDS (null: none)
+  const float* agn;
 };
 
 

@@ -1,0 +1,487 @@
+// Conv3d 3x3x3 (stride 1, pad 1) implicit GEMM with the consumer's GroupNorm +
+// SiLU applied in LDS: the warp-specialised DMA conv for the wide U-Net levels
+// (16-bit, W >= 24, H % 4 == 0, D % 4 == 0, cout % 64 == 0, no K split).
+//
+// Why: the DMA conv of conv3d_v4.hpp stages an ALREADY activated input, so
+// every GroupNorm+SiLU'd conv input was written once and read back once by a
+// streaming pre-pass (cwdm_gn_apply: ~12 GB and 2.5 ms of a 128^3 bf16 step);
+// and its epilogue (residual loads, 64 KB of stores per tile) runs on the MFMA
+// waves.  Doing the transform on the MFMA waves instead cost more than the pass
+// (r02, DESIGN.md §3: the halo is 2.4x the tile and the SIMDs are MFMA-bound).
+//
+// Design (MI355X / gfx950), one 512-thread workgroup per CU, persistent:
+//   * waves 0-3 ("MFMA waves", s_setprio 2) run exactly v4's MFMA schedule on
+//     a 32(x) x 4(y) x 4(z) x 64-channel tile: 8 accumulators of 32 ch x 32 vox
+//     per wave, 216 v_mfma_f32_32x32x16 per 16-channel chunk, weights straight
+//     to VGPRs one group ahead.  They issue no halo DMA, no VALU epilogue and
+//     no global store;
+//   * waves 4-7 ("helper waves", one per SIMD beside an MFMA wave) own the
+//     data movement: per chunk k they issue the halo DMA of chunk k + 2 (and
+//     the chunk's 16 GroupNorm (scale, shift) pairs), wait for their OWN pieces
+//     of chunk k + 1, and apply SiLU(x sc + sh) to them in place (zero padding
+//     stays zero); the VALU issue slots an MFMA leaves free (24 of 32 cycles)
+//     absorb it.  Three 40 KB halo buffers rotate: read (k), transform (k + 1),
+//     DMA (k + 2).  One s_barrier per chunk for all 8 waves.
+//   * tile hand-off: after a tile's last chunk the MFMA waves write their
+//     accumulators as 16-bit values into LDS (rows = voxels, 128 B, 16-B column
+//     XOR row & 7: conflict-free) -- z-planes 0-1 into the halo buffer they just
+//     finished, planes 2-3 into a spare 32 KB -- and go straight on with the
+//     next tile.  During the next tile's first chunk the helpers drain it:
+//     + residual (prefetched a tile earlier into registers), per-channel
+//     (sum, sum^2) GroupNorm partials, 16-byte stores of whole 128-B rows.
+//     Helper h drains exactly the 1 KB blocks of the staging buffer that its
+//     own halo DMA of chunk k + 2 overwrites next, so no helper waits on
+//     another.  Partials reduce across the 4 helpers in a fixed order through
+//     LDS (deterministic).
+// The output is rounded to 16 bits before the residual add (v4 adds in fp32
+// and rounds once); without a residual the output is bit-identical to v4 on a
+// cwdm_gn_apply'd input.
+#include <atomic>
+#include <cstdlib>
+
+#include "conv3d_v4.hpp"
+
+namespace cwdm {
+
+struct V5Cfg {
+  static constexpr int HALO_B = V4Cfg::HALO_B;          // 40960: one halo buffer (2 quad planes x 1280 slots x 16 B)
+  static constexpr int STG1 = 3 * HALO_B;               // staging rows 256..511 (z-planes 2, 3): 32 KB
+  static constexpr int BIAS = STG1 + 32768;             // bias of tile parity s at + 256 s (64 fp32)
+  static constexpr int SCR = BIAS + 512;                // statistics partials [4 helper][64 ch][2] fp32
+  static constexpr int GSS = SCR + 2048;                // GroupNorm (sc, sh) [3 buffers][4 helpers][16 ch][2] fp32
+  static constexpr int CNT = GSS + 1536;                // statistics arrival counter
+  static constexpr int SMEM = CNT + 256;                // 162048 of the CU's 163840
+};
+static_assert(V5Cfg::SMEM <= 163840, "v5 LDS");
+
+template <typename T, int MODE, bool GN>
+__global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
+  using C = V4Cfg;
+  using T16 = T;
+  constexpr int NI = 10 + (GN ? 1 : 0);   // VMEM instructions per chunk of one helper wave
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[V5Cfg::SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, hh = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nblk = p.nblk;
+  const int ntile = (nblk - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  if (ntile <= 0) return;
+  auto tile_of = [&](int it) { return v4_tile_of(p, it); };
+  const int tiles = p.tx * p.ty * p.tz;
+
+  if (wv < 4) {
+    // ------------------------------------------------------------ MFMA waves
+    __builtin_amdgcn_s_setprio(2);
+    const int f = wv & 1, vg = wv >> 1, zb = 2 * vg;
+    const unsigned char* wlane = p.aw + f * 1024 + lr * 32 + ((hh ^ ((lr >> 3) & 1)) << 4);
+    auto load_w = [&](u32x4 (&w)[3], int ct, int c, int g) {
+      const unsigned char* src = wlane + ((long long)ct * p.nch + c) * 27 * 2048 + ((g / 3) * 9 + (g % 3)) * 2048;
+      v4_gload(w[0], src);
+      v4_gload(w[1], src + 3 * 2048);
+      v4_gload(w[2], src + 6 * 2048);
+    };
+    const int hlane = hh * (C::HVP * 16) + (zb * (C::HX * C::HY) + lr) * 16;
+    f32x16 acc[2][4];
+    u32x4 wr[3][3];
+    V4Tile cur = tile_of(0);
+    load_w(wr[0], cur.ct, cur.c0, 0);
+    __builtin_amdgcn_s_barrier();   // B0: chunk 0 transformed, bias 0 landed
+    int gch = 0;
+    for (int it = 0; it < ntile; ++it) {
+      const bool more = it + 1 < ntile;
+      const V4Tile nxt = more ? tile_of(it + 1) : cur;
+      {
+        float bia[16];
+        const float* bl = reinterpret_cast<const float*>(smem + V5Cfg::BIAS + (it & 1) * 256) + f * 32 + 4 * hh;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) bia[i] = p.bias ? bl[8 * (i >> 2) + (i & 3)] : 0.f;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[a][m][i] = bia[i];
+      }
+      auto chunk = [&](auto lastc, int c) {
+        constexpr bool LAST = decltype(lastc)::value;
+        const unsigned char* hb = smem + (gch % 3) * C::HALO_B + hlane;
+        u32x4 av[2][6];
+        v4_read_step<0>(av[0], hb);
+#define V5_STEP(K)                                                                                           \
+        {                                                                                                    \
+          constexpr int GI = (K) / 2, PL = (K) % 2, KN = (K) + 1, BC = (K) & 1;                              \
+          /* straight-line loads and counted waits only: a runtime branch between an asm load and its  */ \
+          /* wait lets the register allocator copy the destination before the data lands (the last tile */ \
+          /* reloads its own first group instead of skipping the load: nxt == cur there)               */ \
+          if (PL == 0) {                                                                                     \
+            if (GI + 1 < 9) load_w(wr[(GI + 1) % 3], cur.ct, c, GI + 1);                                     \
+            else if (!LAST) load_w(wr[0], cur.ct, c + 1, 0);                                                 \
+            else load_w(wr[0], nxt.ct, nxt.c0, 0);                                                           \
+          }                                                                                                  \
+          if (KN < 18) v4_read_step<KN % 18>(av[BC ^ 1], hb);                                                \
+          if (PL == 0) V4_WAIT_W(3, wr[GI % 3]);                                                             \
+          __builtin_amdgcn_sched_barrier(0);                                                                 \
+          _Pragma("unroll") for (int dy = 0; dy < 3; ++dy)                                                   \
+          _Pragma("unroll") for (int m = 0; m < 4; ++m)                                                      \
+            v4_mfma<T>(acc[PL][m], wr[GI % 3][dy], av[BC][m + dy]);                                          \
+          __builtin_amdgcn_sched_barrier(0);                                                                 \
+        }
+        V5_STEP(0) V5_STEP(1) V5_STEP(2) V5_STEP(3) V5_STEP(4) V5_STEP(5)
+        V5_STEP(6) V5_STEP(7) V5_STEP(8) V5_STEP(9) V5_STEP(10) V5_STEP(11)
+        V5_STEP(12) V5_STEP(13) V5_STEP(14) V5_STEP(15) V5_STEP(16) V5_STEP(17)
+#undef V5_STEP
+        __builtin_amdgcn_s_barrier();   // chunk k read; chunk k + 1 transformed
+        ++gch;
+      };
+      for (int c = cur.c0; c + 1 < cur.c1; ++c) chunk(std::false_type{}, c);
+      chunk(std::true_type{}, cur.c1 - 1);
+      // hand the tile to the helpers: 16-bit rows, planes 2 vg, 2 vg + 1 -> staging half vg
+      unsigned char* st = smem + (vg == 0 ? ((gch + 2) % 3) * C::HALO_B : V5Cfg::STG1);
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = acc[pl][m][8 * jj + k];
+            const unsigned p0 = pack2<T16>(v[0], v[1]), p1 = pack2<T16>(v[2], v[3]);
+            const unsigned p2 = pack2<T16>(v[4], v[5]), p3 = pack2<T16>(v[6], v[7]);
+            const auto t0 = __builtin_amdgcn_permlane32_swap(p0, p2, false, false);
+            const auto t1 = __builtin_amdgcn_permlane32_swap(p1, p3, false, false);
+            u32x4 w;
+            w[0] = t0[0]; w[1] = t1[0]; w[2] = t0[1]; w[3] = t1[1];
+            const int row = pl * 128 + m * 32 + lr;
+            const int q = 4 * f + 2 * jj + hh;
+            *reinterpret_cast<u32x4*>(st + row * 128 + ((q ^ (lr & 7)) << 4)) = w;
+          }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();   // B2: tile staged
+      cur = nxt;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2])::"memory");  // the dummy reload
+    return;
+  }
+
+  // -------------------------------------------------------------- helper waves
+  const int h = wv - 4;
+  const int r8 = lane >> 3, q = lane & 7;
+  unsigned* cnt = reinterpret_cast<unsigned*>(smem + V5Cfg::CNT);   // statistics arrivals (monotonic)
+  // chunk prefetch cursor (the next chunk to DMA)
+  int pit = 0;
+  V4Tile pt = tile_of(0);
+  int pc = pt.c0;
+  auto issue_next = [&](int buf) -> bool {
+    if (pit >= ntile) return false;
+    v4_issue_halo<T, MODE>(p, pt, pc, smem + buf * C::HALO_B, h, lane);
+    if constexpr (GN) {
+      if (lane < 32)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(p.agn + ((long long)pt.b * (p.ac0 + p.ac1) + pc * 16) * 2 + lane),
+            (__attribute__((address_space(3))) void*)(smem + V5Cfg::GSS + (buf * 4 + h) * 128), 4, 0, 0);
+    }
+    if (pc + 1 < pt.c1) ++pc;
+    else if (++pit < ntile) { pt = tile_of(pit); pc = pt.c0; }
+    return true;
+  };
+  // SiLU(x sc + sh) in place over this wave's pieces (voxel slots (h + 4 j) * 64 + lane, both
+  // quad planes) of the chunk in buffer buf; slots outside the volume stay zero
+  auto transform = [&](int x0, int y0, int z0, int buf) {
+    if constexpr (GN) {
+      unsigned char* hb = smem + buf * C::HALO_B;
+      const float* gs = reinterpret_cast<const float*>(smem + V5Cfg::GSS + (buf * 4 + h) * 128);
+      u32x4 x[2][5];
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+#pragma unroll
+        for (int qd = 0; qd < 2; ++qd)
+          x[qd][j] = *reinterpret_cast<const u32x4*>(hb + qd * (C::HVP * 16) + ((h + 4 * j) * 64 + lane) * 16);
+      float mk[5];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int hv = (h + 4 * j) * 64 + lane;
+        const int hx = hv % C::HX, hy = (hv / C::HX) % C::HY, hz = hv / (C::HX * C::HY);
+        const int ox = x0 + hx - 1, oy = y0 + hy - 1, oz = z0 + hz - 1;
+        mk[j] = (hv < C::HV && ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) ? 1.f : 0.f;
+      }
+#pragma unroll
+      for (int qd = 0; qd < 2; ++qd) {
+        float sc[8], sh[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { sc[e] = gs[2 * (8 * qd + e)]; sh[e] = gs[2 * (8 * qd + e) + 1]; }
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          float xv[8], y[8];
+          unpack<T>(x[qd][j], xv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y[e] = silu(xv[e] * sc[e] + sh[e]) * mk[j];
+          *reinterpret_cast<u32x4*>(hb + qd * (C::HVP * 16) + ((h + 4 * j) * 64 + lane) * 16) = pack<T>(y);
+        }
+      }
+    } else {
+      (void)x0; (void)y0; (void)z0; (void)buf;
+    }
+  };
+  const long long HW = (long long)p.H * p.W, V = (long long)p.D * HW;
+  const unsigned rowb = (unsigned)p.W * (unsigned)p.cout * 2u, planeb = (unsigned)HW * (unsigned)p.cout * 2u;
+  float s1[8], s2[8];   // this lane's statistics over both drain parts of a tile
+  // drain part `part` of staged tile tt: rows i = 8 part .. + 7 of this lane = voxels (x0 + 8 h + r8,
+  // y0 + (i & 3), z0 + (i >> 2)), channels tile + 8 q .. + 7; part 0 from halo buffer sb, part 1 from the spare
+  auto drain = [&](const V4Tile& tt, int part, int sb) {
+    const int ox = tt.x0 + 8 * h + r8;
+    const bool xin = ox < p.W;
+    const float xm = xin ? 1.f : 0.f;
+    u32x4 rq[8], sv[8];
+    if (p.rmode >= 0) {
+      const long long rV = p.rmode == 1 ? V / 8 : V;
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(reinterpret_cast<const T16*>(p.res) + (long long)tt.b * rV * p.cout), (short)0,
+          (int)(rV * p.cout * 2), 0x00020000);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = 8 * part + k;
+        const int oy = tt.y0 + (i & 3), oz = tt.z0 + (i >> 2);
+        unsigned rv = p.rmode == 1 ? (unsigned)(((oz >> 1) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1))
+                                   : (unsigned)((oz * p.H + oy) * p.W + ox);
+        rq[k] = __builtin_amdgcn_raw_buffer_load_b128(
+            rr, xin ? rv * (unsigned)p.cout * 2u + (unsigned)(tt.ct * 64 + 8 * q) * 2u : 0xFFFFFFF0u, 0, 0);
+      }
+    }
+    const unsigned char* base = smem + (part ? V5Cfg::STG1 : sb * C::HALO_B);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int row = 8 * (h + 4 * k) + r8;
+      sv[k] = *reinterpret_cast<const u32x4*>(base + row * 128 + ((q ^ r8) << 4));
+    }
+    if (part == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+    }
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<T16*>(p.out) + (long long)tt.b * V * p.cout, (short)0, (int)(V * p.cout * 2), 0x00020000);
+    const unsigned obase =
+        ((unsigned)((tt.z0 * p.H + tt.y0) * p.W) + (unsigned)ox) * (unsigned)p.cout * 2u + (unsigned)(tt.ct * 64 + 8 * q) * 2u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = 8 * part + k;
+      float v[8];
+      unpack<T>(sv[k], v);
+      if (p.rmode >= 0) {
+        float r[8];
+        unpack<T>(rq[k], r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += r[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float vv = v[e] * xm;
+        s1[e] += vv;
+        s2[e] += vv * vv;
+      }
+      const unsigned oo = obase + (unsigned)(i >> 2) * planeb + (unsigned)(i & 3) * rowb;
+      __builtin_amdgcn_raw_buffer_store_b128(pack<T>(v), ro, xin ? oo : 0xFFFFFFF0u, 0, 0);
+    }
+    if (part == 1 && p.stats) {
+      // sum over the 8 lanes of each channel block q (lanes q + 8 r8): xor 8 (DPP), 16 (swizzle), 32 (permlane)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float& sx = e < 8 ? s1[e] : s2[e - 8];
+        sx += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sx), 0x128, 0xF, 0xF, true));
+        sx += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, sx), 0x401F));
+        const unsigned u = __builtin_bit_cast(unsigned, sx);
+        const auto sw = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+        sx += __builtin_bit_cast(float, lane < 32 ? (unsigned)sw[1] : (unsigned)sw[0]);
+      }
+      // this helper's partial -> scratch [h][c][2]; the helper that arrives last sums the
+      // four in helper order (deterministic) and writes the tile's partial
+      // (one slot: consecutive part-1 drains are two barriers apart)
+      float* sc = reinterpret_cast<float*>(smem + V5Cfg::SCR) + (h * 64 + 8 * q) * 2;
+      if (lane < 8) {
+#pragma unroll
+        for (int e = 0; e < 8; e += 2)
+          *reinterpret_cast<float4*>(sc + 2 * e) = make_float4(s1[e], s2[e], s1[e + 1], s2[e + 1]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      unsigned old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+      old = __builtin_amdgcn_readfirstlane(old);
+      if ((old & 3u) == 3u) {
+        const float* s0 = reinterpret_cast<const float*>(smem + V5Cfg::SCR) + lane * 2;
+        float su = 0.f, sq = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { su += s0[k * 128]; sq += s0[k * 128 + 1]; }
+        const long long pidx = ((long long)tt.b * tiles + tt.sl) * p.cout + tt.ct * 64 + lane;
+        *reinterpret_cast<float2*>(p.stats + pidx * 2) = make_float2(su, sq);
+      }
+    }
+  };
+  auto issue_bias = [&](const V4Tile& tt, int slot) {
+    if (p.bias && h == 0)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(p.bias + (long long)tt.b * p.bias_bs + tt.ct * 64 + lane),
+          (__attribute__((address_space(3))) void*)(smem + V5Cfg::BIAS + slot * 256), 4, 0, 0);
+  };
+
+  // prologue: chunk 0 and tile 0's bias, chunk 1; transform chunk 0
+  V4Tile cur = tile_of(0);
+  if (h == 0 && lane == 0) *cnt = 0u;
+  issue_next(0);
+  issue_bias(cur, 0);
+  issue_next(1);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+  transform(cur.x0, cur.y0, cur.z0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // B0
+  int gch = 0;
+  int pend = 0;                   // drain parts of dt still to run (2: both, 1: part 1)
+  V4Tile dt = cur;
+  for (int it = 0; it < ntile; ++it) {
+    const bool more = it + 1 < ntile;
+    const V4Tile nxt = more ? tile_of(it + 1) : cur;
+    for (int c = cur.c0; c < cur.c1; ++c) {
+      const bool first = c == cur.c0, lastc = c + 1 == cur.c1;
+      // the drain part runs first: its residual wait (the compiler's) then also retires chunk
+      // k + 1's pieces, and part 0 frees this wave's blocks of the buffer chunk k + 2 goes to
+      const bool drained = pend > 0;
+      if (pend == 2) { drain(dt, 0, (gch + 2) % 3); pend = 1; }
+      else if (pend == 1) { drain(dt, 1, 0); pend = 0; }
+      if (drained) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const bool iss = issue_next((gch + 2) % 3);
+      if (!(lastc && !more)) {
+        // chunk k + 1 (the rest of this tile, or the next tile's first chunk): own pieces landed?
+        if (drained) {
+          if (iss) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + 8) : "memory");
+          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+          if (iss) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const V4Tile& t1 = lastc ? nxt : cur;
+        transform(t1.x0, t1.y0, t1.z0, (gch + 1) % 3);
+      }
+      if (first && more) issue_bias(nxt, (it + 1) & 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (lastc) {
+        __builtin_amdgcn_s_barrier();   // B2: the MFMA waves staged tile it
+        dt = cur;
+        pend = 2;
+      }
+      ++gch;
+    }
+    cur = nxt;
+  }
+  // the last tile (the MFMA waves have left)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  drain(dt, 0, (gch + 2) % 3);
+  drain(dt, 1, 0);
+}
+
+namespace {
+int v5_mode() {
+  static const int m = [] { const char* e = std::getenv("CWDM_V5"); return e ? std::atoi(e) : 2; }();
+  return m;
+}
+}  // namespace
+
+bool sg_eligible(const cwdm_conv3d_desc* d);
+int v4_ksplit(const cwdm_conv3d_desc* d);
+extern std::atomic<int> g_conv_path;
+std::atomic<int> g_v5_grid{0};
+int64_t v4_items(const cwdm_conv3d_desc* d);
+extern thread_local GbwdFuse* g_gbwd;
+
+// the warp-specialised kernel takes a conv of the DMA path when it is a 16-bit
+// fast-epilogue conv without K split and with at least two tiles per CU
+// (env CWDM_V5: 0 off, 1 GroupNorm'd inputs only, 2 every eligible conv)
+bool v5_eligible(const cwdm_conv3d_desc* d, bool gn) {
+  const int mode = v5_mode();
+  const int path = g_conv_path.load(std::memory_order_relaxed);
+  if (mode <= 0 || (mode == 1 && !gn) || path == 1 || path == 3) return false;
+  if (!dtype_half(d->dtype) || sg_eligible(d)) return false;
+  if (path != 2 && v4_ksplit(d) != 1) return false;   // (path 2: forced, no K split of its own)
+  if (d->out_dtype != d->dtype || d->accumulate || d->out1) return false;
+  if (d->a_mode != 0 && d->a_mode != 1) return false;
+  if (d->res_mode < -1 || d->res_mode > 1) return false;
+  if (d->W < kWideMinW || d->H % 4 || d->D % 4 || d->cout % 64) return false;
+  if (d->D * d->H * d->W * d->cout * 2 >= 0xFFFFE000LL) return false;
+  if (g_gbwd && !g_gbwd->used) return false;   // the backward's fused dgrad instance is v4's
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  return path == 2 || v4_items(d) >= 2LL * ncu;
+}
+
+// sources a0 (c0 channels; chunk-major if a0_cm) and a1 (c1, channels-last);
+// agn: [B][c0 + c1][2] GroupNorm scale / shift applied in LDS (null: none)
+int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
+              const float* agn, const void* res, int rmode, hipStream_t s) {
+  const int esz = dtype_size(d->dtype);
+  const int ck = 32 / esz;
+  const int64_t SV = d->a_mode == 1 ? d->D * d->H * d->W / 8 : d->D * d->H * d->W;
+  CWDM_REQUIRE(!agn || !a0_cm, CWDM_E_INVALID, "conv3d_v5: GroupNorm applies to raw channels-last sources only");
+  V4Params p{};
+  p.B = (int)d->B; p.D = (int)d->D; p.H = (int)d->H; p.W = (int)d->W;
+  p.tx = (p.W + 31) / 32; p.ty = p.H / 4; p.tz = p.D / 4;
+  p.cout = d->cout; p.nct = d->cout / 64;
+  p.nch0 = c0 / ck; p.nch = (c0 + c1) / ck;
+  p.a0 = a0; p.ac0 = c0; p.a1 = a1; p.ac1 = c1;
+  p.a0_bstride = SV * c0 * esz; p.a1_bstride = SV * c1 * esz;
+  p.a0_bytes = (unsigned)(SV * c0 * esz); p.a1_bytes = (unsigned)(SV * c1 * esz);
+  p.amode = d->a_mode;
+  p.a0_cm = a0_cm;
+  p.a0_cvox = (int)SV;
+  p.aw = reinterpret_cast<const unsigned char*>(d->a_w);
+  p.bias = d->bias; p.bias_bs = d->bias_bstride;
+  p.res = res; p.rmode = rmode;
+  p.out = d->out;
+  p.stats = d->stats;
+  p.ksplit = 1; p.kper = p.nch;
+  p.agn = agn;
+  const long long nblk = (long long)p.B * p.tx * p.ty * p.tz * p.nct;
+  p.nblk = (int)nblk;
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  const int cap = g_v5_grid.load(std::memory_order_relaxed);
+  const dim3 grid((unsigned)std::min<long long>(nblk, cap > 0 ? cap : ncu));
+  prof_begin(s);
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    if (agn) {
+      if (p.amode == 1) hipLaunchKernelGGL((conv3d_v5_kernel<T, 1, true>), grid, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((conv3d_v5_kernel<T, 0, true>), grid, dim3(512), 0, s, p);
+    } else {
+      if (p.amode == 1) hipLaunchKernelGGL((conv3d_v5_kernel<T, 1, false>), grid, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((conv3d_v5_kernel<T, 0, false>), grid, dim3(512), 0, s, p);
+    }
+  };
+  if (d->dtype == CWDM_BF16) go(bf16_t{});
+  else go(f16_t{});
+  prof_end(s, 2.0 * p.B * p.D * p.H * p.W * (double)p.cout * 27.0 * (c0 + c1));
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+template __global__ void conv3d_v5_kernel<bf16_t, 0, true>(V4Params);
+template __global__ void conv3d_v5_kernel<bf16_t, 1, true>(V4Params);
+template __global__ void conv3d_v5_kernel<bf16_t, 0, false>(V4Params);
+template __global__ void conv3d_v5_kernel<bf16_t, 1, false>(V4Params);
+template __global__ void conv3d_v5_kernel<f16_t, 0, true>(V4Params);
+template __global__ void conv3d_v5_kernel<f16_t, 1, true>(V4Params);
+template __global__ void conv3d_v5_kernel<f16_t, 0, false>(V4Params);
+template __global__ void conv3d_v5_kernel<f16_t, 1, false>(V4Params);
+
+}  // namespace cwdm
+
+extern "C" int cwdm_debug_v5_grid(int n) {
+  CWDM_REQUIRE(n >= 0, CWDM_E_INVALID, "cwdm_debug_v5_grid: n >= 0");
+  return cwdm::g_v5_grid.exchange(n);
+}

@@ -584,6 +584,7 @@ void build(cwdm_unet* u) {
 }  // namespace
 namespace cwdm {
 bool v4_eligible(const cwdm_conv3d_desc* d);
+bool v5_eligible(const cwdm_conv3d_desc* d, bool gn);
 bool apply_skip_ok(int dtype, int C, int cout, int64_t B, int64_t vpb);
 int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
                   const void* wskip, int cout, void* act, void* skip, hipStream_t s);
@@ -1073,7 +1074,16 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
     else { d.out = wb + L.t_off[cs.out]; d.out_dtype = u->cfg.dtype; }
     d.stats = (cs.stats && cs.out >= 0) ? reinterpret_cast<float*>(wb + L.s_off[cs.out]) : nullptr;
     if (u->profiling) cwdm::g_prof = &u->hooks[conv_i];
-    if (L.skip_fused[st.idx]) {
+    // a skip block's conv1 that applies GroupNorm in its own LDS (conv3d_v5,
+    // inference) reads x raw: the fused GroupNorm + 1x1-skip pass would only
+    // write an activated copy nobody reads; conv2 then runs the 1x1 skip itself
+    auto skip_pass_at = [&](int ci) {
+      if (!L.skip_fused[ci]) return false;
+      if (keep) return true;
+      const cwdm_conv3d_desc dc = conv_shape(u, u->convs[ci], B, D, H, W);
+      return !cwdm::v5_eligible(&dc, true);
+    };
+    if (skip_pass_at(st.idx)) {
       // conv1 of a skip block: SiLU(GN1(x)) for this conv and W_skip . x for conv2 in one pass
       const auto& c2 = u->convs[cs.skip_conv];
       const int64_t vpb = d.D * d.H * d.W;
@@ -1084,7 +1094,7 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
       void* part = wb + L.split + ((B * vpb * (d.a_c0 + d.a_c1) * es + 255) & ~(int64_t)255);
       if ((rc = cwdm::v4_launch(&d, act, d.a_c0 + d.a_c1, nullptr, 0, 1, d.res, d.res_mode, part, s))) return rc;
     } else {
-      if (cs.ws_p >= 0 && st.idx > 0 && L.skip_fused[st.idx - 1] && u->convs[st.idx - 1].skip_conv == st.idx) {
+      if (cs.ws_p >= 0 && st.idx > 0 && u->convs[st.idx - 1].skip_conv == st.idx && skip_pass_at(st.idx - 1)) {
         // the skip was computed in conv1's GroupNorm pass: a plain residual here
         d.b0 = d.b1 = nullptr; d.b_c0 = d.b_c1 = 0; d.b_w = nullptr;
         d.res = wb + L.skipbuf; d.res_mode = 0;

@@ -343,10 +343,18 @@ int cwdm_gn_silu_pool(const void* x, int C, const float* gn, int64_t B, int64_t 
                       int dtype, void* out_h, void* out_x, cwdm_stream_t stream);
 
 /* Conv kernel-path policy for cwdm_conv3d_forward (process-wide): 0 = auto
- * (DMA-staged kernel on wide grids with >= 512 tiles, brick/split-K kernels
- * elsewhere), 1 = brick kernels only, 2 = DMA-staged kernel wherever the shape
- * allows.  Returns the previous policy.  Initial value: env CWDM_CONV_PATH. */
+ * (DMA-staged kernels on wide grids with >= 512 tiles -- the warp-specialised
+ * kernel with GroupNorm+SiLU in LDS where it applies, conv3d_v5.hip -- brick /
+ * split-K kernels elsewhere), 1 = brick kernels only, 2 = DMA-staged kernels
+ * wherever the shape allows (the warp-specialised one first), 3 = as 2 but
+ * never the warp-specialised kernel.  Returns the previous policy.  Initial
+ * value: env CWDM_CONV_PATH. */
 int cwdm_conv3d_set_path(int path);
+
+/* Diagnostics / tests only: cap the persistent grid of the warp-specialised
+ * conv at n workgroups (many tiles per workgroup on small shapes); 0 = one per
+ * CU.  Returns the previous cap. */
+int cwdm_debug_v5_grid(int n);
 
 /* Diagnostics only: per-workgroup timestamps of the DMA-staged conv kernel
  * (24 x u64 per workgroup: s_memtime at start, after the prologue, after each of

@@ -74,6 +74,46 @@ def test_fullsize_denoising_step_fp32_vs_oracle():
     assert rel_err(sample, ref["sample"]) < 1e-3
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_fullsize_fused_head_step_bit_identical_to_unfused(dtype):
+    """The timed path at full size: the production U-Net at 128^3 with the
+    sampling step fused into its output head (cwdm_unet_forward_step: the path
+    every bench step runs) == cwdm_unet_forward + cwdm_sampler_step, bit for
+    bit, with tensor noise (reference gaussian_diffusion.py:335-354, :565-573)."""
+    from cwdm_hip import ops
+    P = ou.random_params(seed=5)
+    model, diffusion = _production(dtype, P)
+    cond, x_t, noise = _step_inputs()
+    B, d, h, w, C, cin = 1, N, N, N, 8, model.in_channels
+    V = d * h * w
+    coef = diffusion.coef_table(DEV)
+    t = torch.tensor([640], device=DEV)
+    x_t, noise = x_t.to(DEV), noise.to(DEV)
+    xin = torch.empty(B, d, h, w, cin, device=DEV, dtype=model.plan.torch_dtype)
+    xin[..., :C] = x_t.permute(0, 2, 3, 4, 1).to(xin.dtype)
+    xin[..., C:] = cond.to(DEV).permute(0, 2, 3, 4, 1).to(xin.dtype)
+    s = ops.ncdhw_strides(x_t)
+
+    def run(fused_path):
+        xi = xin.clone()
+        out_nd = torch.empty((B, d, h, w, C), device=DEV)
+        dst, pred = torch.empty_like(x_t), torch.empty_like(x_t)
+        kw = dict(clip_denoised=True, pred_xstart=pred, px_s=s, mirror=xi, mr_s=(V * cin, 1, cin))
+        a = (out_nd, (V * C, 1, C), x_t, s, dst, s, noise, s, coef, t, diffusion.num_timesteps, B, d, h, w)
+        if fused_path:
+            assert model.forward_step_ndhwc(xi, t.float(), ops.sampler_args(*a, **kw))
+        else:
+            model.forward_ndhwc(xi, t.float(), out_nd)
+            ops.sampler_step(*a, **kw)
+        torch.cuda.synchronize()
+        return dst, pred, xi
+
+    fused, ref = run(True), run(False)
+    for a, b, name in zip(fused, ref, ("x_prev", "pred_xstart", "mirror/input")):
+        assert torch.equal(a, b), name
+    assert torch.isfinite(fused[0]).all()
+
+
 def test_fullsize_half_step_close_to_fp32():
     P = ou.random_params(seed=5)
     cond, x_t, noise = _step_inputs()

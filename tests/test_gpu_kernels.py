@@ -356,18 +356,95 @@ V4_CASES = [
 ]
 
 
+@pytest.mark.parametrize("path", [3, 2], ids=["v4", "v5"])
 @pytest.mark.parametrize("dtype_name", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("case", V4_CASES, ids=[c[0] for c in V4_CASES])
-def test_conv3d_dma_kernel_vs_torch(case, dtype_name):
-    """The DMA-staged wide-grid kernel (conv3d_v4.hpp), forced on small shapes,
-    against F.conv3d; then the same call through the brick kernels must agree."""
+def test_conv3d_dma_kernel_vs_torch(case, dtype_name, path):
+    """The DMA-staged wide-grid kernels, forced on small shapes, against
+    F.conv3d: path 3 = conv3d_v4.hpp (GroupNorm pre-pass, K split), path 2 =
+    the warp-specialised conv3d_v5.hip for 16-bit shapes it takes (GroupNorm +
+    SiLU in LDS, helper-wave epilogue; fp32 stays on v4)."""
     from cwdm_hip._lib import lib
     L = lib()
-    prev = L.cwdm_conv3d_set_path(2)
+    prev = L.cwdm_conv3d_set_path(path)
     try:  # with a workspace: the GroupNorm pre-pass, the 1x1 skip and the K-split partials live there
         test_conv3d_fused_vs_torch(case, dtype_name, True)
     finally:
         L.cwdm_conv3d_set_path(prev)
+
+
+V5_CASES = [
+    # name, B, grid(out), c0, c1, cout, amode, gn, skip1x1, rmode  -- shapes with enough tiles for
+    # several per workgroup under a capped grid: the three-buffer halo rotation, the staged tile
+    # hand-off and the two-part drain across tiles of 2..12 chunks
+    ("v5_gn_res_2chunk", 2, (8, 8, 64), 32, 0, 64, 0, True, False, 0),
+    ("v5_gn_concat_c128", 1, (8, 12, 64), 64, 32, 128, 0, True, False, -1),
+    ("v5_up_res_up", 1, (8, 8, 64), 64, 0, 64, 1, True, False, 1),
+    ("v5_partial_x_res", 2, (4, 8, 56), 48, 16, 64, 0, True, False, 0),
+    ("v5_nogn_c192", 1, (4, 8, 96), 32, 32, 192, 0, False, False, -1),
+    ("v5_skip_c12", 1, (4, 4, 64), 128, 64, 64, 0, True, True, -1),
+    ("v5_w24_up_nogn", 2, (4, 8, 24), 32, 0, 64, 1, False, False, 1),
+]
+
+
+@pytest.mark.parametrize("cap", [1, 5, 0])
+@pytest.mark.parametrize("dtype_name", ["bf16", "fp16"])
+@pytest.mark.parametrize("case", V5_CASES, ids=[c[0] for c in V5_CASES])
+def test_conv3d_v5_kernel_vs_torch(case, dtype_name, cap):
+    """conv3d_v5.hip against F.conv3d with the persistent grid capped at 1 / 5
+    workgroups (every workgroup streams many tiles back to back) or uncapped."""
+    from cwdm_hip._lib import lib
+    L = lib()
+    prev, prevg = L.cwdm_conv3d_set_path(2), L.cwdm_debug_v5_grid(cap)
+    try:
+        _run_conv_case(case, dtype_name, True)
+    finally:
+        L.cwdm_conv3d_set_path(prev)
+        L.cwdm_debug_v5_grid(prevg)
+
+
+V5_EXACT_CASES = [
+    # >= 256 tiles of 64 channels: v4 runs them without K split or 32-channel tiles
+    ("v5x_gn_concat", 1, (16, 32, 128), 64, 32, 128, 0, True, False, -1),
+    ("v5x_up_gn", 1, (16, 32, 128), 64, 0, 128, 1, True, False, -1),
+    ("v5x_nogn_partial_x", 2, (16, 16, 120), 32, 0, 64, 0, False, False, -1),
+]
+
+
+@pytest.mark.parametrize("dtype_name", ["bf16", "fp16"])
+@pytest.mark.parametrize("case", V5_EXACT_CASES, ids=lambda c: c[0])
+def test_conv3d_v5_bitexact_vs_v4(case, dtype_name):
+    """Without a residual the warp-specialised conv (GroupNorm+SiLU in LDS) stores
+    exactly what v4 stores after the cwdm_gn_apply pre-pass: same transform, same
+    MFMA order per accumulator, one rounding."""
+    from cwdm_hip._lib import lib
+    L = lib()
+    name, B, grid, c0, c1, cout, amode, use_gn, skip, rmode = case
+    dtype, tdt = _DTN[dtype_name]
+    g = torch.Generator().manual_seed(9)
+    D, H, W = grid
+    sD, sH, sW = (D // 2, H // 2, W // 2) if amode == 1 else (D, H, W)
+    a0 = torch.randn(B, sD, sH, sW, c0, generator=g).to(DEV, tdt)
+    a1 = torch.randn(B, sD, sH, sW, c1, generator=g).to(DEV, tdt) if c1 else None
+    w = (torch.randn(cout, c0 + c1, 3, 3, 3, generator=g) / math.sqrt(27 * (c0 + c1))).to(DEV)
+    bias = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    gn = None
+    if use_gn:
+        gn = torch.stack([1 + 0.2 * torch.randn(B, c0 + c1, generator=g), 0.2 * torch.randn(B, c0 + c1, generator=g)],
+                         -1).contiguous().to(DEV)
+    outs = {}
+    for path in (3, 2):
+        prev, prevg = L.cwdm_conv3d_set_path(path), L.cwdm_debug_v5_grid(7)
+        try:
+            outs[path] = _conv_call(dtype, (B, D, H, W), a0, a1, amode, gn, w, bias)
+        finally:
+            L.cwdm_conv3d_set_path(prev)
+            L.cwdm_debug_v5_grid(prevg)
+    (o4, s4), (o5, s5) = outs[3], outs[2]
+    assert torch.equal(o4.view(torch.int16), o5.view(torch.int16)), name
+    # v4 sums the unrounded fp32 outputs, v5 the stored 16-bit ones (the tensor
+    # the next GroupNorm normalises): sums agree to the storage rounding
+    assert rel_err(s5.cpu(), s4.cpu()) < {"bf16": 2e-3, "fp16": 3e-4}[dtype_name], name
 
 
 SG_CASES = [

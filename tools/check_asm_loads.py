@@ -23,7 +23,8 @@ def main():
     path, sym = sys.argv[1], sys.argv[2]
     text = open(path).read().split('\n')
     start = next(i for i, l in enumerate(text) if l.startswith(sym + ':'))
-    end = next(i for i in range(start + 1, len(text)) if text[i].strip().startswith('s_endpgm'))
+    # the whole function (a kernel may end in several s_endpgm: warp-specialised roles)
+    end = next(i for i in range(start + 1, len(text)) if text[i].startswith('.Lfunc_end'))
     pending, bad = [], 0
     for i in range(start, end):
         s = text[i].strip()
