@@ -358,6 +358,8 @@ def main():
                     help="also time B volumes denoised together in one batched step (serving throughput; "
                          "0 = skip); reported beside, never as, the B=1 metric")
     ap.add_argument("--fp32", type=int, default=3, help="also time K steps of the fp32 parity mode (0 = skip)")
+    ap.add_argument("--fp32x", type=int, default=5, help="also time K steps of the accurate fast mode (fp32 storage, "
+                                                        "split-bf16 conv MFMAs; 0 = skip)")
     ap.add_argument("--train", type=int, default=5, help="config-3 train_ddp side figure: timed steps (0 = skip)")
     ap.add_argument("--wavunet", type=int, default=10, help="f4 side figure: WavUNetModel at 128^3, timed steps "
                                                             "(0 = skip)")
@@ -533,6 +535,22 @@ def main():
                 "steps": args.fp32, "mfma_frac_of_fp32_peak": round(step_flops * args.fp32 / tf / 1e12 / F32_PEAK_TFLOPS, 4)}
         torch.cuda.empty_cache()
 
+    # the accurate fast mode: fp32 activations, the wide-grid conv MFMAs on bf16
+    # hi/lo splits of both operands (compute_dtype "fp32x"; within the north star's
+    # 1e-3 of the reference, tests/test_gpu_fullsize.py)
+    split = None
+    if args.fp32x and args.dtype != "fp32x":
+        model.set_compute_dtype("fp32x")
+        lf = diffusion._native_loop(model, x_T, list(range(T))[::-1][:args.fp32x + 3], cond, True,
+                                    graph=bool(args.graph), fresh_outputs=False, need_pred=False)
+        tf = max_over_ranks(time_loop(lf, (1, args.fp32x), world, sync))
+        lf.close()
+        model.set_compute_dtype(args.dtype)
+        split = {"denoising_steps_per_s": round(world * args.fp32x / tf, 4), "ms_per_step": round(1000 * tf / args.fp32x, 2),
+                 "steps": args.fp32x, "mfma_frac_bf16_equiv": round(4 * step_flops * args.fp32x / tf / 1e12 / BF16_PEAK_TFLOPS, 4),
+                 "numerics": "fp32 storage; products hi.hi + hi.lo + lo.hi + lo.lo of bf16 splits, fp32 accumulation"}
+        torch.cuda.empty_cache()
+
     # fp16 mode: the same config-2 step with 16-bit IEEE half activations and
     # weights (fp32 accumulation, statistics and diffusion state), the
     # finer-mantissa alternative to bf16 at the same MFMA rate
@@ -608,6 +626,7 @@ def main():
         "fast_ddpm_sampled10": fast10,
         "batched_serving": batched,
         "fp32_parity_mode": fp32,
+        "split_bf16_mode": split,
         "fp16_mode": fp16,
         "train_ddp": train,
         "config5_224": config5,

@@ -188,6 +188,35 @@ __global__ void __launch_bounds__(256) pack_tile_kernel(const PackJob* __restric
   }
 }
 
+// Split-bf16 packing of an fp32 conv for the accurate fast mode (conv3d_v5.hip,
+// cwdm_conv3d_desc.a_w_split): the bf16 layout of a virtual conv with 4 cin
+// inputs -- per fp32 K chunk c (8 channels) two bf16 chunks: pass 0 = [hi(w) | hi(w)],
+// pass 1 = [lo(w) | lo(w)] over the (hi(x) | lo(x)) halo planes, hi = bf16(w),
+// lo = bf16(w - hi): hi.hi + hi.lo + lo.hi + lo.lo of every product, fp32-accumulated
+__global__ void __launch_bounds__(256) pack_split_kernel(const float* __restrict__ w, int cout, int cin, int NT,
+                                                         bf16_t* __restrict__ out, long long total) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int nch = cin / 4;  // virtual 16-channel chunks
+  const int e = (int)(i % 8);
+  long long r = i / 8;
+  r /= 2;  // quad (either plane carries the same 8 channels)
+  const int n = (int)(r % NT);
+  r /= NT;
+  const int tap = (int)(r % 27);
+  r /= 27;
+  const int chunk = (int)(r % nch);
+  const int ct = (int)(r / nch);
+  const int co = ct * NT + n, ci = (chunk >> 1) * 8 + e;
+  float v = 0.f;
+  if (co < cout) {
+    const float x = w[((long long)co * cin + ci) * 27 + tap];
+    const float hi = bf2f(f2bf(x));
+    v = (chunk & 1) ? x - hi : hi;
+  }
+  out[i] = f2bf(v);
+}
+
 template <typename T, int NF>
 int dispatch_brick(const ConvParams& p, const Brick& br, hipStream_t s) {
   if (br.bx == 32 && br.bz == 4) return launch_wide<T, NF>(p, s);
@@ -234,6 +263,23 @@ extern thread_local std::vector<PackJob>* g_pack_batch;
 extern "C" int cwdm_conv3d_pack(const float* w, int cout, int cin, int ksize, int dtype, void* packed,
                                 cwdm_stream_t stream) {
   return pack_impl(w, cout, cin, ksize, dtype, packed, 0, stream);
+}
+
+extern "C" int64_t cwdm_conv3d_packed_split_bytes(int cout, int cin) {
+  if (cout <= 0 || cout % 64 || cin <= 0 || cin % 8) return -1;
+  return cwdm_conv3d_packed_bytes(cout, 4 * cin, 3, CWDM_BF16);
+}
+
+extern "C" int cwdm_conv3d_pack_split(const float* w, int cout, int cin, void* packed, cwdm_stream_t stream) {
+  CWDM_REQUIRE(w && packed, CWDM_E_INVALID, "cwdm_conv3d_pack_split: null pointer");
+  CWDM_REQUIRE(cout > 0 && cout % 64 == 0 && cin > 0 && cin % 8 == 0, CWDM_E_UNSUPPORTED,
+               "cwdm_conv3d_pack_split: cout % 64 == 0, cin % 8 == 0");
+  const int NT = 64;
+  const long long total = (long long)(cout / NT) * (cin / 4) * 27 * NT * 16;
+  hipLaunchKernelGGL(pack_split_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, w,
+                     cout, cin, NT, reinterpret_cast<bf16_t*>(packed), total);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
 }
 
 extern "C" int cwdm_conv3d_pack_s2(const float* w, int cout, int cin, int dtype, void* packed, int transpose,
@@ -345,6 +391,7 @@ Plan1 plan_conv(const cwdm_conv3d_desc* d) {
 
 namespace cwdm {
 bool v4_eligible(const cwdm_conv3d_desc* d);
+bool v5_eligible(const cwdm_conv3d_desc* d, bool gn);
 int64_t v4_workspace_bytes(const cwdm_conv3d_desc* d);
 int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s);
 int legacy_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream);
@@ -357,7 +404,7 @@ int pw_forward(const cwdm_conv3d_desc* d, hipStream_t s);
 extern "C" int64_t cwdm_conv3d_workspace_bytes(const cwdm_conv3d_desc* d) {
   if (!d || d->B <= 0 || d->D <= 0 || d->H <= 0 || d->W <= 0 || d->cout <= 0) return -1;
   const int64_t legacy = plan_conv(d).ws;
-  return v4_eligible(d) ? std::max(legacy, v4_workspace_bytes(d)) : legacy;
+  return (v4_eligible(d) || (d->a_w_split && v5_eligible(d, false))) ? std::max(legacy, v4_workspace_bytes(d)) : legacy;
 }
 
 extern "C" int64_t cwdm_conv3d_parts(int dtype, int64_t D, int64_t H, int64_t W, int cout) {
@@ -388,7 +435,8 @@ extern "C" int cwdm_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stre
                "cwdm_conv3d_forward: output dtype must be fp32 or the compute dtype");
   if (head_eligible(d)) return head_conv_forward(d, (hipStream_t)stream);
   if (pw_eligible(d)) return pw_forward(d, (hipStream_t)stream);
-  if (v4_eligible(d)) {
+  // (the accurate fast mode's split-bf16 kernel takes fp32 shapes of any size: the same host path)
+  if (v4_eligible(d) || (d->a_w_split && v5_eligible(d, false))) {
     const int64_t need = v4_workspace_bytes(d);
     if (need == 0 || (d->workspace && d->ws_bytes >= need)) return conv3d_v4_forward(d, (hipStream_t)stream);
   }

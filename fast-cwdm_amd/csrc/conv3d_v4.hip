@@ -261,7 +261,7 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   if (sg_eligible(d)) return sg_launch(p, d, partial, s);
   // the warp-specialised kernel (conv3d_v5.hip) where it applies (not the
   // backward's fused GroupNorm-reduce dgrad, not the stamps diagnostics build)
-  if (!p.stamps && !(g_gbwd && !g_gbwd->used) && v5_eligible(d, false))
+  if (!(g_gbwd && !g_gbwd->used) && v5_eligible(d, false))
     return v5_launch(d, a0, c0, a1, c1, a0_cm, nullptr, res, rmode, s);
   const int S = v4_ksplit(d);
   p.ksplit = S;
@@ -391,7 +391,7 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   // GroupNorm + SiLU inside the warp-specialised conv (no activated copy):
   // inference only -- the training forward keeps the activated input for wgrad
   const float* agn = nullptr;
-  if (d->a_gn && !g_act_keep && !g_stamps.load(std::memory_order_relaxed) && v5_eligible(d, true)) agn = d->a_gn;
+  if (d->a_gn && !g_act_keep && v5_eligible(d, true)) agn = d->a_gn;
   if (d->a_gn && !agn) {
     // the activated input: in the workspace, or (training) where the plan keeps
     // it for the backward's DMA-staged wgrad

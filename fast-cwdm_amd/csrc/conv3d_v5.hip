@@ -13,7 +13,7 @@
 //   * waves 0-3 ("MFMA waves", s_setprio 2) run exactly v4's MFMA schedule on
 //     a 32(x) x 4(y) x 4(z) x 64-channel tile: 8 accumulators of 32 ch x 32 vox
 //     per wave, 216 v_mfma_f32_32x32x16 per 16-channel chunk, weights straight
-//     to VGPRs one group ahead.  They issue no halo DMA, no VALU epilogue and
+//     to VGPRs two groups ahead.  They issue no halo DMA, no VALU epilogue and
 //     no global store;
 //   * waves 4-7 ("helper waves", one per SIMD beside an MFMA wave) own the
 //     data movement: per chunk k they issue the halo DMA of chunk k + 2 (and
@@ -49,10 +49,23 @@ struct V5Cfg {
   static constexpr int BIAS = STG1 + 32768;             // bias of tile parity s at + 256 s (64 fp32)
   static constexpr int SCR = BIAS + 512;                // statistics partials [4 helper][64 ch][2] fp32
   static constexpr int GSS = SCR + 2048;                // GroupNorm (sc, sh) [3 buffers][4 helpers][16 ch][2] fp32
-  static constexpr int CNT = GSS + 1536;                // statistics arrival counter
+  static constexpr int CNT = GSS + 1536;                // statistics arrival counters
   static constexpr int SMEM = CNT + 256;                // 162048 of the CU's 163840
 };
 static_assert(V5Cfg::SMEM <= 163840, "v5 LDS");
+
+// diagnostics build (make STAMPS=1, tools/v5_stamps.py): per workgroup 64 u64 s_memtime stamps --
+// [0] start, [1] MFMA waves past B0, [2 + k] MFMA wave 0 at chunk k's barrier, [18 + k] released from it,
+// [34 + k] helper 0 at chunk k's barrier (k < 16), [50] / [51] s_memrealtime at start / end of MFMA wave 0,
+// [52] end of helper 0, [53] HW_ID, [54] XCC_ID
+#ifdef CWDM_CONV_STAMPS
+#define V5_STAMP(k, cond)                                                                        \
+  do {                                                                                           \
+    if (p.stamps && (cond)) p.stamps[(long long)blockIdx.x * 64 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define V5_STAMP(k, cond) do { } while (0)
+#endif
 
 template <typename T, int MODE, bool GN>
 __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
@@ -69,6 +82,14 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   auto tile_of = [&](int it) { return v4_tile_of(p, it); };
   const int tiles = p.tx * p.ty * p.tz;
 
+  V5_STAMP(0, tid == 0);
+#ifdef CWDM_CONV_STAMPS
+  if (p.stamps && tid == 0) {
+    p.stamps[(long long)blockIdx.x * 64 + 50] = __builtin_amdgcn_s_memrealtime();
+    p.stamps[(long long)blockIdx.x * 64 + 53] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+    p.stamps[(long long)blockIdx.x * 64 + 54] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+  }
+#endif
   if (wv < 4) {
     // ------------------------------------------------------------ MFMA waves
     __builtin_amdgcn_s_setprio(2);
@@ -85,7 +106,9 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
     u32x4 wr[3][3];
     V4Tile cur = tile_of(0);
     load_w(wr[0], cur.ct, cur.c0, 0);
+    load_w(wr[1], cur.ct, cur.c0, 1);
     __builtin_amdgcn_s_barrier();   // B0: chunk 0 transformed, bias 0 landed
+    V5_STAMP(1, tid == 0);
     int gch = 0;
     for (int it = 0; it < ntile; ++it) {
       const bool more = it + 1 < ntile;
@@ -113,13 +136,14 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
           /* straight-line loads and counted waits only: a runtime branch between an asm load and its  */ \
           /* wait lets the register allocator copy the destination before the data lands (the last tile */ \
           /* reloads its own first group instead of skipping the load: nxt == cur there)               */ \
+          /* weights two groups ahead (one MFMA wave per SIMD: nothing else hides an L2 round trip) */   \
           if (PL == 0) {                                                                                     \
-            if (GI + 1 < 9) load_w(wr[(GI + 1) % 3], cur.ct, c, GI + 1);                                     \
-            else if (!LAST) load_w(wr[0], cur.ct, c + 1, 0);                                                 \
-            else load_w(wr[0], nxt.ct, nxt.c0, 0);                                                           \
+            if (GI + 2 < 9) load_w(wr[(GI + 2) % 3], cur.ct, c, GI + 2);                                     \
+            else if (!LAST) load_w(wr[(GI + 2) % 3], cur.ct, c + 1, GI - 7);                                 \
+            else load_w(wr[(GI + 2) % 3], nxt.ct, nxt.c0, GI - 7);                                           \
           }                                                                                                  \
           if (KN < 18) v4_read_step<KN % 18>(av[BC ^ 1], hb);                                                \
-          if (PL == 0) V4_WAIT_W(3, wr[GI % 3]);                                                             \
+          if (PL == 0) V4_WAIT_W(6, wr[GI % 3]);                                                             \
           __builtin_amdgcn_sched_barrier(0);                                                                 \
           _Pragma("unroll") for (int dy = 0; dy < 3; ++dy)                                                   \
           _Pragma("unroll") for (int m = 0; m < 4; ++m)                                                      \
@@ -130,7 +154,9 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
         V5_STEP(6) V5_STEP(7) V5_STEP(8) V5_STEP(9) V5_STEP(10) V5_STEP(11)
         V5_STEP(12) V5_STEP(13) V5_STEP(14) V5_STEP(15) V5_STEP(16) V5_STEP(17)
 #undef V5_STEP
+        V5_STAMP(2 + gch, tid == 0 && gch < 16);
         __builtin_amdgcn_s_barrier();   // chunk k read; chunk k + 1 transformed
+        V5_STAMP(18 + gch, tid == 0 && gch < 16);
         ++gch;
       };
       for (int c = cur.c0; c + 1 < cur.c1; ++c) chunk(std::false_type{}, c);
@@ -160,7 +186,11 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
       __builtin_amdgcn_s_barrier();   // B2: tile staged
       cur = nxt;
     }
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2])::"memory");  // the dummy reload
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2]), "+v"(wr[1][0]), "+v"(wr[1][1]),
+                 "+v"(wr[1][2])::"memory");   // the dummy reloads of the last tile
+#ifdef CWDM_CONV_STAMPS
+    if (p.stamps && tid == 0) p.stamps[(long long)blockIdx.x * 64 + 51] = __builtin_amdgcn_s_memrealtime();
+#endif
     return;
   }
 
@@ -362,6 +392,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
       }
       if (first && more) issue_bias(nxt, (it + 1) & 1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      V5_STAMP(34 + gch, tid == 256 && gch < 16);
       __builtin_amdgcn_s_barrier();
       if (lastc) {
         __builtin_amdgcn_s_barrier();   // B2: the MFMA waves staged tile it
@@ -376,6 +407,302 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   drain(dt, 0, (gch + 2) % 3);
   drain(dt, 1, 0);
+  V5_STAMP(52, tid == 256);
+}
+
+
+// ---------------------------------------------------------------------------
+// The accurate fast mode: fp32 activations, conv MFMAs on bf16 hi/lo splits.
+// Same pipeline as conv3d_v5_kernel with three changes:
+//   * helpers convert every DMA'd fp32 chunk (8 channels, 32 B per voxel; the
+//     GroupNorm+SiLU applied first when agn is set) in place into two bf16
+//     planes: quad plane 0 = hi(x) of the 8 channels, plane 1 = lo(x) =
+//     bf16(x - hi(x)) -- the same 32 bytes per voxel slot;
+//   * the MFMA waves run two bf16 weight passes over each chunk
+//     (cwdm_conv3d_pack_split: [hi(w) | hi(w)] then [lo(w) | lo(w)]), i.e.
+//     hi.hi + hi.lo + lo.hi + lo.lo of every product, fp32-accumulated: a
+//     relative error ~2^-16 per product instead of 2^-8 (bf16) at 2x the bf16
+//     MFMA work per 8 fp32 channels (the exact-fp32 MFMA runs at 1/16 rate);
+//   * fp32 outputs leave from the accumulators (no 16-bit staging), with the
+//     (sum, sum^2) partials reduced across the two plane waves of a channel
+//     half through LDS (the second to arrive writes them: deterministic).
+// ---------------------------------------------------------------------------
+template <int MODE, bool GN>
+__global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
+  using C = V4Cfg;
+  constexpr int NI = 10 + (GN ? 1 : 0);
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[V5Cfg::SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, hh = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nblk = p.nblk;
+  const int ntile = (nblk - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  if (ntile <= 0) return;
+  auto tile_of = [&](int it) { return v4_tile_of(p, it); };
+  const int tiles = p.tx * p.ty * p.tz;
+  const int nchv = 2 * p.nch;   // bf16 weight chunks: two passes per fp32 chunk
+  unsigned* cnt = reinterpret_cast<unsigned*>(smem + V5Cfg::CNT);
+
+  if (wv < 4) {
+    // ------------------------------------------------------------ MFMA waves
+    __builtin_amdgcn_s_setprio(2);
+    const int f = wv & 1, vg = wv >> 1, zb = 2 * vg;
+    const unsigned char* wlane = p.aw + f * 1024 + lr * 32 + ((hh ^ ((lr >> 3) & 1)) << 4);
+    auto load_w = [&](u32x4 (&w)[3], int ct, int cv, int g) {
+      const unsigned char* src = wlane + ((long long)ct * nchv + cv) * 27 * 2048 + ((g / 3) * 9 + (g % 3)) * 2048;
+      v4_gload(w[0], src);
+      v4_gload(w[1], src + 3 * 2048);
+      v4_gload(w[2], src + 6 * 2048);
+    };
+    const int hlane = hh * (C::HVP * 16) + (zb * (C::HX * C::HY) + lr) * 16;
+    f32x16 acc[2][4];
+    u32x4 wr[3][3];
+    V4Tile cur = tile_of(0);
+    load_w(wr[0], cur.ct, 2 * cur.c0, 0);
+    load_w(wr[1], cur.ct, 2 * cur.c0, 1);
+    __builtin_amdgcn_s_barrier();   // B0
+    int gch = 0;
+    const long long HW = (long long)p.H * p.W, V = (long long)p.D * HW;
+    for (int it = 0; it < ntile; ++it) {
+      const bool more = it + 1 < ntile;
+      const V4Tile nxt = more ? tile_of(it + 1) : cur;
+      {
+        float bia[16];
+        const float* bl = reinterpret_cast<const float*>(smem + V5Cfg::BIAS + (it & 1) * 256) + f * 32 + 4 * hh;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) bia[i] = bl[8 * (i >> 2) + (i & 3)];
+        const float bm = p.bias ? 1.f : 0.f;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[a][m][i] = bia[i] * bm;
+      }
+      // one bf16 weight pass (virtual chunk cv) over the halo at hb; LASTV: the tile's last pass
+      auto vpass = [&](auto lastc, int cv, const unsigned char* hb) {
+        constexpr bool LASTV = decltype(lastc)::value;
+        u32x4 av[2][6];
+        v4_read_step<0>(av[0], hb);
+#define V5S_STEP(K)                                                                                          \
+        {                                                                                                    \
+          constexpr int GI = (K) / 2, PL = (K) % 2, KN = (K) + 1, BC = (K) & 1;                              \
+          if (PL == 0) {                                                                                     \
+            if (GI + 2 < 9) load_w(wr[(GI + 2) % 3], cur.ct, cv, GI + 2);                                    \
+            else if (!LASTV) load_w(wr[(GI + 2) % 3], cur.ct, cv + 1, GI - 7);                               \
+            else load_w(wr[(GI + 2) % 3], nxt.ct, 2 * nxt.c0, GI - 7);                                       \
+          }                                                                                                  \
+          if (KN < 18) v4_read_step<KN % 18>(av[BC ^ 1], hb);                                                \
+          if (PL == 0) V4_WAIT_W(6, wr[GI % 3]);                                                             \
+          __builtin_amdgcn_sched_barrier(0);                                                                 \
+          _Pragma("unroll") for (int dy = 0; dy < 3; ++dy)                                                   \
+          _Pragma("unroll") for (int m = 0; m < 4; ++m)                                                      \
+            v4_mfma<bf16_t>(acc[PL][m], wr[GI % 3][dy], av[BC][m + dy]);                                     \
+          __builtin_amdgcn_sched_barrier(0);                                                                 \
+        }
+        V5S_STEP(0) V5S_STEP(1) V5S_STEP(2) V5S_STEP(3) V5S_STEP(4) V5S_STEP(5)
+        V5S_STEP(6) V5S_STEP(7) V5S_STEP(8) V5S_STEP(9) V5S_STEP(10) V5S_STEP(11)
+        V5S_STEP(12) V5S_STEP(13) V5S_STEP(14) V5S_STEP(15) V5S_STEP(16) V5S_STEP(17)
+#undef V5S_STEP
+      };
+      for (int c = cur.c0; c + 1 < cur.c1; ++c) {
+        const unsigned char* hb = smem + (gch % 3) * C::HALO_B + hlane;
+        vpass(std::false_type{}, 2 * c, hb);
+        vpass(std::false_type{}, 2 * c + 1, hb);
+        __builtin_amdgcn_s_barrier();   // chunk k read; chunk k + 1 split
+        ++gch;
+      }
+      {
+        const int c = cur.c1 - 1;
+        const unsigned char* hb = smem + (gch % 3) * C::HALO_B + hlane;
+        vpass(std::false_type{}, 2 * c, hb);
+        vpass(std::true_type{}, 2 * c + 1, hb);
+        __builtin_amdgcn_s_barrier();
+        ++gch;
+      }
+      // fp32 epilogue from the accumulators: + residual, store, (sum, sum^2) partials
+      {
+        const int c0w = cur.ct * 64 + f * 32, cl = c0w + 4 * hh;
+        const int ox = cur.x0 + lr;
+        const bool xin = ox < p.W;
+        const float xm = xin ? 1.f : 0.f;
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<float*>(p.out) + (long long)cur.b * V * p.cout, (short)0, (int)(V * p.cout * 4), 0x00020000);
+        const long long rV = p.rmode == 1 ? V / 8 : V;
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(reinterpret_cast<const float*>(p.res) + (long long)cur.b * rV * p.cout), (short)0,
+            (int)(rV * p.cout * 4), 0x00020000);
+        float ssum[16], ssq[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { ssum[i] = 0.f; ssq[i] = 0.f; }
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const int oy = cur.y0 + m, oz = cur.z0 + zb + pl;
+            const unsigned vo = (unsigned)((oz * p.H + oy) * p.W + ox);
+            const unsigned rvo = p.rmode == 1 ? (unsigned)(((oz >> 1) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1)) : vo;
+            float4 rq[4];
+            if (p.rmode >= 0) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(
+                    rr, xin ? (rvo * (unsigned)p.cout + (unsigned)(cl + 8 * j)) * 4u : 0xFFFFFFF0u, 0, 0);
+                rq[j] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
+                                    __uint_as_float(q[3]));
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              float v[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) v[k] = acc[pl][m][4 * j + k];
+              if (p.rmode >= 0) { v[0] += rq[j].x; v[1] += rq[j].y; v[2] += rq[j].z; v[3] += rq[j].w; }
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                ssum[4 * j + k] += v[k] * xm;
+                ssq[4 * j + k] += v[k] * v[k] * xm;
+              }
+              u32x4 w;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) w[k] = __float_as_uint(v[k]);
+              __builtin_amdgcn_raw_buffer_store_b128(w, ro, xin ? (vo * (unsigned)p.cout + (unsigned)(cl + 8 * j)) * 4u
+                                                               : 0xFFFFFFF0u, 0, 0);
+            }
+          }
+        if (p.stats) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            ssum[i] = row16_sum(ssum[i]);
+            ssq[i] = row16_sum(ssq[i]);
+            ssum[i] += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, ssum[i]), 0x401F));
+            ssq[i] += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, ssq[i]), 0x401F));
+          }
+          // this wave's partial: scratch [f][vg][2 halves][16] sums, then squares at + 256
+          float* sc = reinterpret_cast<float*>(smem + V5Cfg::SCR) + (f * 2 + vg) * 32 + hh * 16;
+          if (lr == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { sc[i] = ssum[i]; sc[256 + i] = ssq[i]; }
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          unsigned old = 0;
+          if (lane == 0) old = __hip_atomic_fetch_add(cnt + f, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+          old = __builtin_amdgcn_readfirstlane(old);
+          if (old & 1u) {   // the second of the channel half's two plane waves
+            if (lane < 32) {
+              const int h2 = (lane >> 2) & 1, i = 4 * (lane >> 3) + (lane & 3);
+              const float* s0 = reinterpret_cast<const float*>(smem + V5Cfg::SCR) + f * 64 + h2 * 16 + i;
+              const float su = s0[0] + s0[32], sq = s0[256] + s0[256 + 32];
+              const long long pidx = ((long long)cur.b * tiles + cur.sl) * p.cout + c0w + lane;
+              *reinterpret_cast<float2*>(p.stats + pidx * 2) = make_float2(su, sq);
+            }
+          }
+        }
+      }
+      cur = nxt;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(wr[0][0]), "+v"(wr[0][1]), "+v"(wr[0][2]), "+v"(wr[1][0]), "+v"(wr[1][1]),
+                 "+v"(wr[1][2])::"memory");
+    return;
+  }
+
+  // -------------------------------------------------------------- helper waves
+  const int h = wv - 4;
+  int pit = 0;
+  V4Tile pt = tile_of(0);
+  int pc = pt.c0;
+  auto issue_next = [&](int buf) -> bool {
+    if (pit >= ntile) return false;
+    v4_issue_halo<float, MODE>(p, pt, pc, smem + buf * C::HALO_B, h, lane);
+    if constexpr (GN) {
+      if (lane < 16)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(p.agn + ((long long)pt.b * (p.ac0 + p.ac1) + pc * 8) * 2 + lane),
+            (__attribute__((address_space(3))) void*)(smem + V5Cfg::GSS + (buf * 4 + h) * 128), 4, 0, 0);
+    }
+    if (pc + 1 < pt.c1) ++pc;
+    else if (++pit < ntile) { pt = tile_of(pit); pc = pt.c0; }
+    return true;
+  };
+  // fp32 chunk at buffer buf, this wave's voxel slots (h + 4 j) * 64 + lane: (GroupNorm + SiLU,)
+  // then plane 0 <- hi, plane 1 <- lo of the 8 channels
+  auto split = [&](int x0, int y0, int z0, int buf) {
+    unsigned char* hb = smem + buf * C::HALO_B;
+    u32x4 x[2][5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+      for (int qd = 0; qd < 2; ++qd)
+        x[qd][j] = *reinterpret_cast<const u32x4*>(hb + qd * (C::HVP * 16) + ((h + 4 * j) * 64 + lane) * 16);
+    float sc[8], sh[8], mk[5];
+    if constexpr (GN) {
+      const float* gs = reinterpret_cast<const float*>(smem + V5Cfg::GSS + (buf * 4 + h) * 128);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sc[e] = gs[2 * e]; sh[e] = gs[2 * e + 1]; }
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int hv = (h + 4 * j) * 64 + lane;
+        const int hx = hv % C::HX, hy = (hv / C::HX) % C::HY, hz = hv / (C::HX * C::HY);
+        const int ox = x0 + hx - 1, oy = y0 + hy - 1, oz = z0 + hz - 1;
+        mk[j] = (hv < C::HV && ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) ? 1.f : 0.f;
+      }
+    } else {
+      (void)x0; (void)y0; (void)z0;
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[e] = __uint_as_float(x[0][j][e]); v[4 + e] = __uint_as_float(x[1][j][e]); }
+      if constexpr (GN) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = silu(v[e] * sc[e] + sh[e]) * mk[j];
+      }
+      u32x4 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hi[e] = pack2<bf16_t>(v[2 * e], v[2 * e + 1]);
+        lo[e] = pack2<bf16_t>(v[2 * e] - lo2f<bf16_t>(hi[e]), v[2 * e + 1] - hi2f<bf16_t>(hi[e]));
+      }
+      *reinterpret_cast<u32x4*>(hb + ((h + 4 * j) * 64 + lane) * 16) = hi;
+      *reinterpret_cast<u32x4*>(hb + C::HVP * 16 + ((h + 4 * j) * 64 + lane) * 16) = lo;
+    }
+  };
+  auto issue_bias = [&](const V4Tile& tt, int slot) {
+    if (p.bias && h == 0)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(p.bias + (long long)tt.b * p.bias_bs + tt.ct * 64 + lane),
+          (__attribute__((address_space(3))) void*)(smem + V5Cfg::BIAS + slot * 256), 4, 0, 0);
+  };
+  V4Tile cur = tile_of(0);
+  if (h == 0 && lane < 2) cnt[lane] = 0u;
+  issue_next(0);
+  issue_bias(cur, 0);
+  issue_next(1);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+  split(cur.x0, cur.y0, cur.z0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // B0
+  int gch = 0;
+  for (int it = 0; it < ntile; ++it) {
+    const bool more = it + 1 < ntile;
+    const V4Tile nxt = more ? tile_of(it + 1) : cur;
+    for (int c = cur.c0; c < cur.c1; ++c) {
+      const bool first = c == cur.c0, lastc = c + 1 == cur.c1;
+      const bool iss = issue_next((gch + 2) % 3);
+      if (!(lastc && !more)) {
+        if (iss) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const V4Tile& t1 = lastc ? nxt : cur;
+        split(t1.x0, t1.y0, t1.z0, (gch + 1) % 3);
+      }
+      if (first && more) issue_bias(nxt, (it + 1) & 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      ++gch;
+    }
+    cur = nxt;
+  }
 }
 
 namespace {
@@ -388,17 +715,34 @@ int v5_mode() {
 bool sg_eligible(const cwdm_conv3d_desc* d);
 int v4_ksplit(const cwdm_conv3d_desc* d);
 extern std::atomic<int> g_conv_path;
+extern std::atomic<unsigned long long*> g_stamps;
 std::atomic<int> g_v5_grid{0};
 int64_t v4_items(const cwdm_conv3d_desc* d);
 extern thread_local GbwdFuse* g_gbwd;
 
 // the warp-specialised kernel takes a conv of the DMA path when it is a 16-bit
 // fast-epilogue conv without K split and with at least two tiles per CU
-// (env CWDM_V5: 0 off, 1 GroupNorm'd inputs only, 2 every eligible conv)
+// (env CWDM_V5: 0 off, 1 GroupNorm'd inputs only, 2 every eligible conv, 3 every
+// eligible conv with the GroupNorm applied by the cwdm_gn_apply pre-pass)
 bool v5_eligible(const cwdm_conv3d_desc* d, bool gn) {
   const int mode = v5_mode();
   const int path = g_conv_path.load(std::memory_order_relaxed);
+  if (d->dtype == CWDM_F32) {
+    // the accurate fast mode (conv3d_v5s_kernel): wherever the split weights are
+    // given and the shape tiles (no minimum work: it is 8x the exact-fp32 MFMA rate)
+    if (!d->a_w_split || path == 1 || path == 3) return false;
+    if (d->out_dtype != CWDM_F32 || d->accumulate || d->out1) return false;
+    if (d->a_mode != 0 && d->a_mode != 1) return false;
+    if (d->res_mode < -1 || d->res_mode > 1) return false;
+    if (d->W < kWideMinW || d->H % 4 || d->D % 4 || d->cout % 64) return false;
+    if (d->D * d->H * d->W * d->cout * 4 >= 0xFFFFE000LL) return false;
+    return !(gn && d->a_mode == 1);
+  }
   if (mode <= 0 || (mode == 1 && !gn) || path == 1 || path == 3) return false;
+  // GroupNorm+SiLU in LDS: not for an upsampling conv (its halo repeats every
+  // source voxel 8x: the pre-pass at the half resolution is 8x cheaper), and
+  // not in mode 3 (pre-pass + this kernel on the activated copy)
+  if (gn && (d->a_mode == 1 || mode == 3)) return false;
   if (!dtype_half(d->dtype) || sg_eligible(d)) return false;
   if (path != 2 && v4_ksplit(d) != 1) return false;   // (path 2: forced, no K split of its own)
   if (d->out_dtype != d->dtype || d->accumulate || d->out1) return false;
@@ -442,6 +786,7 @@ int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   p.stats = d->stats;
   p.ksplit = 1; p.kper = p.nch;
   p.agn = agn;
+  p.stamps = g_stamps.load(std::memory_order_relaxed);
   const long long nblk = (long long)p.B * p.tx * p.ty * p.tz * p.nct;
   p.nblk = (int)nblk;
   static const int ncu = [] {
@@ -463,8 +808,20 @@ int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
       else hipLaunchKernelGGL((conv3d_v5_kernel<T, 0, false>), grid, dim3(512), 0, s, p);
     }
   };
-  if (d->dtype == CWDM_BF16) go(bf16_t{});
-  else go(f16_t{});
+  if (d->dtype == CWDM_F32) {
+    p.aw = reinterpret_cast<const unsigned char*>(d->a_w_split);
+    if (agn) {
+      if (p.amode == 1) hipLaunchKernelGGL((conv3d_v5s_kernel<1, true>), grid, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((conv3d_v5s_kernel<0, true>), grid, dim3(512), 0, s, p);
+    } else {
+      if (p.amode == 1) hipLaunchKernelGGL((conv3d_v5s_kernel<1, false>), grid, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((conv3d_v5s_kernel<0, false>), grid, dim3(512), 0, s, p);
+    }
+  } else if (d->dtype == CWDM_BF16) {
+    go(bf16_t{});
+  } else {
+    go(f16_t{});
+  }
   prof_end(s, 2.0 * p.B * p.D * p.H * p.W * (double)p.cout * 27.0 * (c0 + c1));
   CWDM_LAUNCHED();
   return CWDM_OK;
@@ -478,6 +835,10 @@ template __global__ void conv3d_v5_kernel<f16_t, 0, true>(V4Params);
 template __global__ void conv3d_v5_kernel<f16_t, 1, true>(V4Params);
 template __global__ void conv3d_v5_kernel<f16_t, 0, false>(V4Params);
 template __global__ void conv3d_v5_kernel<f16_t, 1, false>(V4Params);
+template __global__ void conv3d_v5s_kernel<0, true>(V4Params);
+template __global__ void conv3d_v5s_kernel<1, true>(V4Params);
+template __global__ void conv3d_v5s_kernel<0, false>(V4Params);
+template __global__ void conv3d_v5s_kernel<1, false>(V4Params);
 
 }  // namespace cwdm
 

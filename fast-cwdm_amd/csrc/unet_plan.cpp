@@ -80,6 +80,7 @@ struct ConvStep {
   int level;                    // output level
   bool stats;
   int skip_conv = -1;           // conv1 of a block with a 1x1 skip: index of the block's conv2
+  int64_t wsplit_off = -1;      // accurate fast mode: split-bf16 packed weights (cwdm_conv3d_pack_split), -1 none
   int s2 = 0;                   // stride-2 conv (Downsample.op) over a space-to-depth input: cin_a = 8 x its channels
 };
 
@@ -555,6 +556,8 @@ void build(cwdm_unet* u) {
   u->off_emb_b = take((int64_t)u->R * 4);
   for (auto& cs : u->convs) {
     cs.w_off = take(cwdm_conv3d_packed_bytes(cs.cout, cs.cin_a, 3, c.dtype));
+    if (c.mfma_split && c.dtype == CWDM_F32 && !cs.s2 && cs.cout % 64 == 0 && cs.cin_a % 8 == 0)
+      cs.wsplit_off = take(cwdm_conv3d_packed_split_bytes(cs.cout, cs.cin_a));
     if (cs.ws_p >= 0) cs.wsk_off = take(cwdm_conv3d_packed_bytes(cs.cout, cs.cin_b, 1, c.dtype));
     if (cs.bias_kind == 0) cs.bias_off = take((int64_t)cs.cout * 4);
   }
@@ -653,6 +656,7 @@ cwdm_conv3d_desc conv_shape(const cwdm_unet* u, const ConvStep& cs, int64_t B, i
   }
   d.res_mode = cs.rmode;
   d.out_dtype = cs.out < 0 ? CWDM_F32 : u->cfg.dtype;
+  if (cs.wsplit_off >= 0) d.a_w_split = reinterpret_cast<const void*>(1);   // presence flag only
   return d;
 }
 
@@ -908,6 +912,9 @@ extern "C" int cwdm_unet_pack(const cwdm_unet* uc, const float* const* P, void* 
       } else if ((rc = cwdm_conv3d_pack(P[cs.w_p], cs.cout, cs.cin_a, 3, u->cfg.dtype, base + cs.w_off, stream))) {
         return rc;
       }
+      if (cs.wsplit_off >= 0 &&
+          (rc = cwdm_conv3d_pack_split(P[cs.w_p], cs.cout, cs.cin_a, base + cs.wsplit_off, stream)))
+        return rc;
       if (cs.ws_p >= 0 &&
           (rc = cwdm_conv3d_pack(P[cs.ws_p], cs.cout, cs.cin_b, 1, u->cfg.dtype, base + cs.wsk_off, stream)))
         return rc;
@@ -1062,6 +1069,7 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
     d.ws_bytes = L.split_bytes;
     d.a_gn = cs.gn >= 0 ? reinterpret_cast<const float*>(wb + L.ss_off[cs.gn]) : nullptr;
     d.a_w = pk + cs.w_off;
+    d.a_w_split = cs.wsplit_off >= 0 ? pk + cs.wsplit_off : nullptr;
     if (cs.ws_p >= 0) {
       d.b0 = tptr(cs.sb0); d.b_c0 = u->tensors[cs.sb0].channels;
       d.b1 = tptr(cs.sb1); d.b_c1 = cs.sb1 >= 0 ? u->tensors[cs.sb1].channels : 0;

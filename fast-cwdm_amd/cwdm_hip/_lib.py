@@ -64,6 +64,7 @@ class ConvDesc(ctypes.Structure):
         ("workspace", vp), ("ws_bytes", i64),
         ("out1", vp), ("out_c0", ctypes.c_int),
         ("accumulate", ctypes.c_int),
+        ("a_w_split", vp),
     ]
 
 
@@ -90,6 +91,7 @@ class UNetConfig(ctypes.Structure):
         ("num_levels", ctypes.c_int), ("channel_mult", ctypes.c_int * 8),
         ("num_groups", ctypes.c_int), ("dtype", ctypes.c_int),
         ("resblock_updown", ctypes.c_int), ("use_freq", ctypes.c_int),
+        ("mfma_split", ctypes.c_int),
     ]
 
 
@@ -132,6 +134,8 @@ _PROTOS = {
                                   i64, i64, i64, vp]),
     "cwdm_conv3d_packed_bytes": (i64, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "cwdm_conv3d_pack": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]),
+    "cwdm_conv3d_packed_split_bytes": (i64, [ctypes.c_int, ctypes.c_int]),
+    "cwdm_conv3d_pack_split": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, vp, vp]),
     "cwdm_conv3d_pack_dgrad": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]),
     "cwdm_conv3d_parts": (i64, [ctypes.c_int, i64, i64, i64, ctypes.c_int]),
     "cwdm_space_to_depth": (ctypes.c_int, [vp, ctypes.c_int, i64, i64, i64, i64, ctypes.c_int, vp, ctypes.c_int,

@@ -13,7 +13,10 @@ from ._lib import CWDM_BF16, CWDM_F16, CWDM_F32, check, lib
 from .ops import _need_cuda, _stream
 
 _DTYPES = {"fp32": CWDM_F32, "float32": CWDM_F32, "bf16": CWDM_BF16, "bfloat16": CWDM_BF16,
-           "fp16": CWDM_F16, "float16": CWDM_F16}
+           "fp16": CWDM_F16, "float16": CWDM_F16,
+           # the accurate fast mode: fp32 storage, wide-grid conv MFMAs on bf16 hi/lo splits
+           "fp32x": CWDM_F32}
+SPLIT_DTYPES = ("fp32x",)
 TORCH_DT = {CWDM_F32: torch.float32, CWDM_BF16: torch.bfloat16, CWDM_F16: torch.float16}
 
 
@@ -21,7 +24,7 @@ def parse_dtype(d):
     if isinstance(d, torch.dtype):
         d = {torch.float32: "fp32", torch.bfloat16: "bf16", torch.float16: "fp16"}.get(d, str(d))
     if d not in _DTYPES:
-        raise ValueError(f"compute dtype must be fp32, bf16 or fp16, got {d!r}")
+        raise ValueError(f"compute dtype must be fp32, fp32x, bf16 or fp16, got {d!r}")
     return _DTYPES[d]
 
 
@@ -37,6 +40,7 @@ class UNetPlan:
             cfg.channel_mult[i] = int(m)
         cfg.num_groups = num_groups
         cfg.dtype = parse_dtype(dtype)
+        cfg.mfma_split = 1 if (isinstance(dtype, str) and dtype in SPLIT_DTYPES) else 0
         cfg.resblock_updown = 1 if resblock_updown else 0
         cfg.use_freq = 1 if use_freq else 0
         self.use_freq = bool(use_freq)

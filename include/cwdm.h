@@ -290,8 +290,15 @@ typedef struct {
   void* out1; int out_c0;   /* optional second output: channels >= out_c0 (the two halves of a
                                concat input's gradient) */
   int accumulate;           /* out += result instead of out = result */
+  const void* a_w_split;    /* fp32 convs (optional): cwdm_conv3d_pack_split weights -- the accurate fast
+                               mode: the conv MFMAs run on bf16 hi/lo splits of the fp32 operands (every
+                               product hi.hi + hi.lo + lo.hi + lo.lo, fp32 accumulation) where the shape
+                               takes the warp-specialised kernel; fp32 in, fp32 out */
 } cwdm_conv3d_desc;
 int64_t cwdm_conv3d_packed_bytes(int cout, int cin, int ksize, int dtype);
+/* Split-bf16 weights of a 3x3x3 fp32 conv (cout % 64 == 0) for cwdm_conv3d_desc.a_w_split. */
+int64_t cwdm_conv3d_packed_split_bytes(int cout, int cin);
+int cwdm_conv3d_pack_split(const float* w_oidhw, int cout, int cin, void* packed, cwdm_stream_t stream);
 int cwdm_conv3d_pack(const float* w_oidhw, int cout, int cin, int ksize, int dtype,
                      void* packed, cwdm_stream_t stream);
 /* Packs the input-gradient (dgrad) conv of a (cin -> cout) conv: a (cout -> cin)
@@ -458,6 +465,9 @@ typedef struct {
                           conv / Upsample(use_conv=True) nearest + conv (unet.py:40-100, conv_resample) */
   int use_freq;        /* 1: WavUNetModel (guided_diffusion/wunet.py, script_util.py:268-292): DWT/IDWT
                           resampling with high-band skips, wavelet input pyramid; forward only */
+  int mfma_split;      /* fp32 plans: 1 = the accurate fast mode -- the wide-grid 3x3x3 convs run their MFMAs on
+                          bf16 hi/lo splits of the fp32 operands (cwdm_conv3d_pack_split, conv3d_v5.hip); fp32
+                          storage and everything else unchanged */
 } cwdm_unet_config;
 
 int cwdm_unet_create(const cwdm_unet_config* cfg, cwdm_unet** plan);

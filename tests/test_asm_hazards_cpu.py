@@ -25,8 +25,9 @@ def test_v5_async_weight_loads_have_no_early_uses(tmp_path):
                     os.path.join(CSRC, "conv3d_v5.hip"), "-o", str(out)], check=True, capture_output=True)
     text = out.read_text()
     syms = sorted({l.split(":")[0] for l in text.split("\n")
-                   if l.startswith("_ZN4cwdm16conv3d_v5_kernel") and l.split()[0].endswith(":")})
-    assert len(syms) == 8, syms
+                   if l.startswith(("_ZN4cwdm16conv3d_v5_kernel", "_ZN4cwdm17conv3d_v5s_kernel"))
+                   and l.split()[0].endswith(":")})
+    assert len(syms) == 12, syms
     for sym in syms:
         r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_asm_loads.py"), str(out), sym],
                            capture_output=True, text=True)

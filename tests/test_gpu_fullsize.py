@@ -74,6 +74,25 @@ def test_fullsize_denoising_step_fp32_vs_oracle():
     assert rel_err(sample, ref["sample"]) < 1e-3
 
 
+def test_fullsize_denoising_step_accurate_fast_mode_vs_oracle():
+    """The accurate fast mode (compute_dtype "fp32x": fp32 storage, split-bf16
+    conv MFMAs) at BASELINE's full size: one whole denoising step within 1e-3 of
+    the CPU oracle (x_hat_0 and the sample), the north star's bound."""
+    P = ou.random_params(seed=5)
+    model, diffusion = _production("fp32x", P)
+    cond, x_t, noise = _step_inputs()
+    t = 640
+    sample, pred = _native_step(model, diffusion, cond, x_t, noise, t)
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"))
+    torch.set_num_threads(16)
+    with torch.no_grad():
+        ref = od.p_sample(tab, ou.OracleUNet(P), x_t, torch.tensor([t]), cond, noise)
+    e_pred, e_samp = rel_err(pred, ref["pred_xstart"]), rel_err(sample, ref["sample"])
+    print(f"fp32x vs oracle at 128^3: pred_xstart {e_pred:.3e}, sample {e_samp:.3e}")
+    assert e_pred < 1e-3
+    assert e_samp < 1e-3
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 def test_fullsize_fused_head_step_bit_identical_to_unfused(dtype):
     """The timed path at full size: the production U-Net at 128^3 with the

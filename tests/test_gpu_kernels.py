@@ -171,7 +171,7 @@ def test_ddim_step_vs_oracle(eta):
 
 # --------------------------------------------------------------------------- conv3d
 def _conv_call(dtype, out_grid, a0, a1, amode, gn, w, bias, bvec_bstride=0, b0=None, b1=None, wb=None, res=None,
-               rmode=-1, out_f32=False, stats=True, split=True):
+               rmode=-1, out_f32=False, stats=True, split=True, wsplit=False):
     """Run cwdm_conv3d_forward on NDHWC tensors; returns (out, stats)."""
     from cwdm_hip import _lib
     from cwdm_hip._lib import check, lib
@@ -208,6 +208,12 @@ def _conv_call(dtype, out_grid, a0, a1, amode, gn, w, bias, bvec_bstride=0, b0=N
     d.res, d.res_mode = (res.data_ptr() if res is not None else None), rmode
     d.out, d.out_dtype = out.data_ptr(), (_lib.CWDM_F32 if out_f32 else dtype)
     d.stats = st.data_ptr() if st is not None else None
+    psplit = None
+    if wsplit:   # the accurate fast mode's split-bf16 weights (fp32 convs)
+        psplit = torch.empty(L.cwdm_conv3d_packed_split_bytes(cout, w.shape[1]), dtype=torch.uint8, device=DEV)
+        check(L.cwdm_conv3d_pack_split(ctypes.c_void_p(w.to(DEV).contiguous().data_ptr()), cout, w.shape[1],
+                                       ctypes.c_void_p(psplit.data_ptr()), None))
+        d.a_w_split = psplit.data_ptr()
     nws = L.cwdm_conv3d_workspace_bytes(ctypes.byref(d))
     ws = None
     if nws > 0 and split:
@@ -401,6 +407,69 @@ def test_conv3d_v5_kernel_vs_torch(case, dtype_name, cap):
     finally:
         L.cwdm_conv3d_set_path(prev)
         L.cwdm_debug_v5_grid(prevg)
+
+
+SPLIT_CASES = [
+    # name, B, grid(out), c0, c1, cout, amode, gn, skip1x1, rmode (fp32, cout % 64 == 0, W >= 24)
+    ("x_gn_res", 2, (8, 8, 64), 32, 0, 64, 0, True, False, 0),
+    ("x_gn_concat_c128", 1, (8, 12, 64), 64, 32, 128, 0, True, False, -1),
+    ("x_up_gnpre_res_up", 1, (8, 8, 64), 64, 0, 64, 1, True, False, 1),
+    ("x_partial_x_nogn", 2, (4, 8, 56), 48, 16, 64, 0, False, False, 0),
+    ("x_skip", 1, (4, 4, 64), 128, 64, 64, 0, True, True, -1),
+    ("x_w24_up_nogn", 2, (4, 8, 24), 32, 0, 64, 1, False, False, 1),
+]
+
+
+@pytest.mark.parametrize("cap", [3, 0])
+@pytest.mark.parametrize("case", SPLIT_CASES, ids=[c[0] for c in SPLIT_CASES])
+def test_conv3d_split_bf16_accurate_mode_vs_torch(case, cap):
+    """The accurate fast mode (conv3d_v5s_kernel): fp32 in / out, MFMAs on bf16
+    hi/lo splits of both operands (hi.hi + hi.lo + lo.hi + lo.lo) -- within 2e-5
+    of fp32 F.conv3d on the UNquantised fp32 operands (bf16 is ~1e-2)."""
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import lib
+    L = lib()
+    name, B, grid, c0, c1, cout, amode, use_gn, skip, rmode = case
+    g = torch.Generator().manual_seed(17)
+    D, H, W = grid
+    sD, sH, sW = (D // 2, H // 2, W // 2) if amode == 1 else (D, H, W)
+    cin = c0 + c1
+    x = torch.randn(B, cin, sD, sH, sW, generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)
+    bias = torch.randn(cout, generator=g) * 0.1
+    gn = None
+    h = x
+    if use_gn:
+        scale = 1 + 0.2 * torch.randn(B, cin, generator=g)
+        shift = 0.2 * torch.randn(B, cin, generator=g)
+        gn = torch.stack([scale, shift], -1).contiguous()
+        h = F.silu(x * scale[:, :, None, None, None] + shift[:, :, None, None, None])
+    if amode == 1:
+        h = F.interpolate(h, scale_factor=2, mode="nearest")
+    ref = F.conv3d(h.double(), w.double(), bias.double(), padding=1)
+    wb = None
+    if skip:
+        wb = torch.randn(cout, cin, 1, 1, 1, generator=g) / math.sqrt(cin)
+        ref = ref + F.conv3d(x.double(), wb.double())
+    res = None
+    if rmode >= 0:
+        res = torch.randn(B, cout, *((D, H, W) if rmode == 0 else (D // 2, H // 2, W // 2)), generator=g)
+        ref = ref + (res if rmode == 0 else F.interpolate(res, scale_factor=2, mode="nearest")).double()
+    prev, prevg = L.cwdm_conv3d_set_path(0), L.cwdm_debug_v5_grid(cap)
+    try:
+        out, st = _conv_call(_lib.CWDM_F32, (B, D, H, W), _nd(x[:, :c0]).to(DEV), _nd(x[:, c0:]).to(DEV) if c1 else None,
+                             amode, gn.to(DEV) if gn is not None else None, w.to(DEV), bias.to(DEV),
+                             b0=_nd(x[:, :c0]).to(DEV) if skip else None,
+                             b1=_nd(x[:, c0:]).to(DEV) if (skip and c1) else None,
+                             wb=wb.to(DEV) if skip else None, res=_nd(res).to(DEV) if res is not None else None,
+                             rmode=rmode, wsplit=True)
+    finally:
+        L.cwdm_conv3d_set_path(prev)
+        L.cwdm_debug_v5_grid(prevg)
+    got = _nc(out.cpu()).double()
+    assert rel_err(got, ref) < 2e-5, name
+    s = st.sum(1).cpu().double()
+    assert torch.allclose(s[..., 0], ref.sum(dim=(2, 3, 4)), rtol=1e-4, atol=1e-5 * ref.abs().max().item() * D * H * W)
 
 
 V5_EXACT_CASES = [

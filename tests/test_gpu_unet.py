@@ -91,6 +91,25 @@ def test_production_unet_forward_dma_kernel(grid):
         lib().cwdm_conv3d_set_path(prev)
 
 
+@pytest.mark.parametrize("grid", [(16, 16, 32), (32, 32, 64)])
+def test_production_unet_accurate_fast_mode_vs_oracle(grid):
+    """compute_dtype "fp32x" (fp32 storage, the wide-grid conv MFMAs on bf16
+    hi/lo splits, conv3d_v5s_kernel): the 81.5 M production U-Net within the
+    north star's 1e-3 of the oracle, and within 2e-5 of the exact-fp32 plan."""
+    P = ou.random_params(seed=14)
+    cfg = dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4))
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(1, 32, *grid, generator=g)
+    t = torch.tensor([300])
+    with torch.no_grad():
+        mx = _product_model(cfg, 32, P, "fp32x")
+        out = mx(x.to(DEV), t.to(DEV))
+        ref = ou.unet_forward(P, x, t)
+        assert rel_err(out, ref) < 1e-3
+        m32 = _product_model(cfg, 32, P, "fp32")
+        assert rel_err(out, m32(x.to(DEV), t.to(DEV))) < 2e-5
+
+
 @pytest.mark.parametrize("half,tol", [("bf16", 6e-2), ("fp16", 1e-2)])
 def test_production_unet_half_close_to_fp32(half, tol):
     P = ou.random_params(seed=12)

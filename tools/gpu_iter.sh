@@ -13,7 +13,7 @@ i=0
 for rep in 1 2; do
 for cfg in "$@"; do
   i=$((i+1))
-  env $cfg timeout -k 10 240 python -u bench.py --cpu-baseline 0 --train 0 --fp32 0 --batched 0 --respaced 0 --fp16 0 --config5 0 --wavunet 0 --train5 0 --steps 30 > $O/ab_$i.json 2> $O/ab_$i.err || { tail -20 $O/ab_$i.err; exit 1; }
+  env $cfg timeout -k 10 240 python -u bench.py --cpu-baseline 0 --train 0 --fp32 0 --fp32x 0 --batched 0 --respaced 0 --fp16 0 --config5 0 --wavunet 0 --train5 0 --steps 30 > $O/ab_$i.json 2> $O/ab_$i.err || { tail -20 $O/ab_$i.err; exit 1; }
   python3 -c "import json; d=json.loads(open('$O/ab_$i.json').read().strip().splitlines()[-1]); print('$cfg', d['value'], d['ms_per_step'], d['roofline']['frac'])"
 done
 done

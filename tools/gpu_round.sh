@@ -17,7 +17,7 @@ timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err && timeout 
 tail -1 $O/bench.json | cut -c1-300
 timeout -k 10 300 python -u tools/train_bench.py --steps 5 > $O/train_bench.json 2> $O/train_bench.err
 tail -1 $O/train_bench.json
-SIDE="--cpu-baseline 0 --respaced 0 --batched 0 --train 0 --fp32 0 --fp16 0 --config5 0 --wavunet 0 --train5 0"
+SIDE="--cpu-baseline 0 --respaced 0 --batched 0 --train 0 --fp32 0 --fp32x 0 --fp16 0 --config5 0 --wavunet 0 --train5 0"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 $SIDE > $O/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_train -o run --output-format csv -- python3 $R/tools/train_bench.py --steps 3 --warmup 1 > $O/trace_train.log 2>&1
