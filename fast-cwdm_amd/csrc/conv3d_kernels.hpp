@@ -62,6 +62,20 @@ __device__ __forceinline__ float silu(float v) {
   return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.4426950408889634f));
 }
 
+// SiLU(x sc + sh) with the affine folded into exp2's argument: a = -sc log2(e),
+// b = -sh log2(e) (silu_aff_coef), t = x a + b = -z log2(e), and
+// z / (1 + 2^t) = t / (-log2(e) (1 + 2^t)): fma, exp2, fma, rcp, mul -- 5 VALU
+// (2 transcendental) instead of 6.  The GroupNorm pre-pass (cwdm_gn_apply) and
+// the warp-specialised conv's in-LDS transform both use it: bit-identical.
+__device__ __forceinline__ void silu_aff_coef(float sc, float sh, float& a, float& b) {
+  a = sc * -1.4426950408889634f;
+  b = sh * -1.4426950408889634f;
+}
+__device__ __forceinline__ float silu_aff(float x, float a, float b) {
+  const float t = __builtin_fmaf(x, a, b);
+  return t * __builtin_amdgcn_rcpf(__builtin_fmaf(__builtin_amdgcn_exp2f(t), -1.4426950408889634f, -1.4426950408889634f));
+}
+
 // 16-byte quad <-> floats
 template <typename T>
 __device__ __forceinline__ void unpack(const u32x4& q, float* f);

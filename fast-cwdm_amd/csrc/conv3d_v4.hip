@@ -81,13 +81,14 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x0,
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float4 t = g4[e];  // (sc, sh) of channels c + 2e, c + 2e + 1
-        sc[2 * e] = t.x; sh[2 * e] = t.y; sc[2 * e + 1] = t.z; sh[2 * e + 1] = t.w;
+        silu_aff_coef(t.x, t.y, sc[2 * e], sh[2 * e]);
+        silu_aff_coef(t.z, t.w, sc[2 * e + 1], sh[2 * e + 1]);
       }
       bprev = b;
     }
     float y[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) y[e] = silu(xv[k][e] * sc[e] + sh[e]);
+    for (int e = 0; e < 8; ++e) y[e] = silu_aff(xv[k][e], sc[e], sh[e]);
     T* dst = cm ? out + ((size_t)(b * (unsigned)(C / CK) + (unsigned)(c / CK)) * dvpb.d + (v - b * dvpb.d)) * CK + (c % CK)
                 : out + (size_t)v * C + c;
     if constexpr (sizeof(T) == 2) {

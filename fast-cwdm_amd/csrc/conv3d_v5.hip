@@ -235,17 +235,24 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
         const int ox = x0 + hx - 1, oy = y0 + hy - 1, oz = z0 + hz - 1;
         mk[j] = (hv < C::HV && ox >= 0 && oy >= 0 && oz >= 0 && ox < p.W && oy < p.H && oz < p.D) ? 1.f : 0.f;
       }
+      // interior tiles (the halo inside the volume: most of them) skip the masks
+      const bool inner = x0 >= 1 && y0 >= 1 && z0 >= 1 && x0 + C::HX - 1 <= p.W && y0 + C::HY - 1 <= p.H &&
+                         z0 + C::HZ - 1 <= p.D;
 #pragma unroll
       for (int qd = 0; qd < 2; ++qd) {
-        float sc[8], sh[8];
+        float sa[8], sb[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { sc[e] = gs[2 * (8 * qd + e)]; sh[e] = gs[2 * (8 * qd + e) + 1]; }
+        for (int e = 0; e < 8; ++e) silu_aff_coef(gs[2 * (8 * qd + e)], gs[2 * (8 * qd + e) + 1], sa[e], sb[e]);
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
           float xv[8], y[8];
           unpack<T>(x[qd][j], xv);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) y[e] = silu(xv[e] * sc[e] + sh[e]) * mk[j];
+          for (int e = 0; e < 8; ++e) y[e] = silu_aff(xv[e], sa[e], sb[e]);
+          if (!inner) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] *= mk[j];
+          }
           *reinterpret_cast<u32x4*>(hb + qd * (C::HVP * 16) + ((h + 4 * j) * 64 + lane) * 16) = pack<T>(y);
         }
       }
@@ -638,7 +645,7 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
     if constexpr (GN) {
       const float* gs = reinterpret_cast<const float*>(smem + V5Cfg::GSS + (buf * 4 + h) * 128);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { sc[e] = gs[2 * e]; sh[e] = gs[2 * e + 1]; }
+      for (int e = 0; e < 8; ++e) silu_aff_coef(gs[2 * e], gs[2 * e + 1], sc[e], sh[e]);
 #pragma unroll
       for (int j = 0; j < 5; ++j) {
         const int hv = (h + 4 * j) * 64 + lane;
@@ -656,7 +663,7 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
       for (int e = 0; e < 4; ++e) { v[e] = __uint_as_float(x[0][j][e]); v[4 + e] = __uint_as_float(x[1][j][e]); }
       if constexpr (GN) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = silu(v[e] * sc[e] + sh[e]) * mk[j];
+        for (int e = 0; e < 8; ++e) v[e] = silu_aff(v[e], sc[e], sh[e]) * mk[j];
       }
       u32x4 hi, lo;
 #pragma unroll
@@ -707,7 +714,7 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
 
 namespace {
 int v5_mode() {
-  static const int m = [] { const char* e = std::getenv("CWDM_V5"); return e ? std::atoi(e) : 2; }();
+  static const int m = [] { const char* e = std::getenv("CWDM_V5"); return e ? std::atoi(e) : 3; }();
   return m;
 }
 }  // namespace
@@ -722,8 +729,10 @@ extern thread_local GbwdFuse* g_gbwd;
 
 // the warp-specialised kernel takes a conv of the DMA path when it is a 16-bit
 // fast-epilogue conv without K split and with at least two tiles per CU
-// (env CWDM_V5: 0 off, 1 GroupNorm'd inputs only, 2 every eligible conv, 3 every
-// eligible conv with the GroupNorm applied by the cwdm_gn_apply pre-pass)
+// (env CWDM_V5: 0 off, 1 GroupNorm'd inputs only, 2 every eligible conv, 3 (default)
+// every eligible conv with the GroupNorm applied by the cwdm_gn_apply pre-pass: the
+// in-LDS transform costs the helper waves more issue cycles than the MFMA waves
+// leave them -- measured 611 vs 588 us on the 64->64 128^3-subband conv)
 bool v5_eligible(const cwdm_conv3d_desc* d, bool gn) {
   const int mode = v5_mode();
   const int path = g_conv_path.load(std::memory_order_relaxed);

@@ -1,0 +1,9 @@
+#!/bin/bash
+# full GPU parity suite, then smoke()
+# usage: tools/gpu_full.sh TAG [pytest -k filter]
+set -e -o pipefail
+T=${1:-full}; K=${2:-}
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/$T; mkdir -p $O; cd $R
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread ${K:+-k "$K"} > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
+tail -3 $O/pytest_gpu.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -2 $O/smoke.log
