@@ -212,6 +212,18 @@ int legacy_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream);
 // V4Params::gx0); taken only by the 16-bit fast epilogue without K split
 thread_local GbwdFuse* g_gbwd = nullptr;
 
+// the backward's dgrad conv whose epilogue may take the GroupNorm-backward
+// reduce (v4 only): only where the conv leaves VALU room -- at 128^3 the
+// epilogue's ~13 VALU + 2 transcendentals per output element cost the
+// MFMA-bound kernel more (+30 %) than the separate reduce pass it saves; at
+// 64^3 / 32^3 it is a net win (same-box kernel traces; env
+// CWDM_GBWD_MAXW, default 64).  Elsewhere the dgrad is an ordinary conv (v5 may take it).
+bool gbwd_grid_ok(const cwdm_conv3d_desc* d) {
+  static const int gb_maxw = [] { const char* e = std::getenv("CWDM_GBWD_MAXW"); return e ? std::atoi(e) : 64; }();
+  return g_gbwd && !g_gbwd->used && dtype_half(d->dtype) && d->W <= gb_maxw && d->a_mode == 0 && d->res_mode < 0 &&
+         !d->stats;
+}
+
 int gn_apply(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
              void* out, hipStream_t s, int cm = 0) {
   constexpr int VPT = 4;
@@ -262,7 +274,7 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   if (sg_eligible(d)) return sg_launch(p, d, partial, s);
   // the warp-specialised kernel (conv3d_v5.hip) where it applies (not the
   // backward's fused GroupNorm-reduce dgrad, not the stamps diagnostics build)
-  if (!(g_gbwd && !g_gbwd->used) && v5_eligible(d, false))
+  if (v5_eligible(d, false))   // (refuses the dgrad that takes the fused GroupNorm-backward reduce)
     return v5_launch(d, a0, c0, a1, c1, a0_cm, nullptr, res, rmode, s);
   const int S = v4_ksplit(d);
   p.ksplit = S;
@@ -317,13 +329,8 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
       else hipLaunchKernelGGL((conv3d_v4_kernel<T, 0, false>), grid, dim3(256), 0, s, p);
     }
   };
-  // (only where the conv leaves VALU room: at 128^3 the epilogue's ~13 VALU + 2
-  // transcendentals per output element cost the MFMA-bound kernel more (+30 %)
-  // than the separate reduce pass it saves; at 64^3 / 32^3 it is a net win --
-  // same-box kernel traces, DESIGN.md §3b.  Env CWDM_GBWD_MAXW, default 64)
-  static const int gb_maxw = [] { const char* e = std::getenv("CWDM_GBWD_MAXW"); return e ? std::atoi(e) : 64; }();
-  if (g_gbwd && !g_gbwd->used && dtype_half(d->dtype) && (ct32 || fast) && S == 1 && rmode < 0 && !p.stats &&
-      p.amode == 0 && p.W <= gb_maxw) {
+  // (gbwd_grid_ok: where the fused reduce pays)
+  if (gbwd_grid_ok(d) && (ct32 || fast) && S == 1 && rmode < 0 && !p.stats && p.amode == 0) {
     GbwdFuse& g = *g_gbwd;
     const int nc = ct32 ? 32 : 64;
     const int C = d->cout;

@@ -725,7 +725,7 @@ extern std::atomic<int> g_conv_path;
 extern std::atomic<unsigned long long*> g_stamps;
 std::atomic<int> g_v5_grid{0};
 int64_t v4_items(const cwdm_conv3d_desc* d);
-extern thread_local GbwdFuse* g_gbwd;
+bool gbwd_grid_ok(const cwdm_conv3d_desc* d);
 
 // the warp-specialised kernel takes a conv of the DMA path when it is a 16-bit
 // fast-epilogue conv without K split and with at least two tiles per CU
@@ -759,7 +759,7 @@ bool v5_eligible(const cwdm_conv3d_desc* d, bool gn) {
   if (d->res_mode < -1 || d->res_mode > 1) return false;
   if (d->W < kWideMinW || d->H % 4 || d->D % 4 || d->cout % 64) return false;
   if (d->D * d->H * d->W * d->cout * 2 >= 0xFFFFE000LL) return false;
-  if (g_gbwd && !g_gbwd->used) return false;   // the backward's fused dgrad instance is v4's
+  if (gbwd_grid_ok(d)) return false;   // the backward's fused dgrad instance is v4's
   static const int ncu = [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)

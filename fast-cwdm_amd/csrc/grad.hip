@@ -394,9 +394,7 @@ __global__ void __launch_bounds__(256) resample_add_kernel(T* __restrict__ dst, 
 
 template <typename T>
 __global__ void __launch_bounds__(256) channel_sum_kernel(const T* __restrict__ src, long long V, int C, int cs,
-                                                         long long vpb, float* __restrict__ out_bc,
-                                                         long long bc_stride, float* __restrict__ out_c,
-                                                         float* __restrict__ out_c2, float* __restrict__ part) {
+                                                         long long vpb, float* __restrict__ part) {
   __shared__ float red[256 * 8];
   const int ncg = (C + 7) >> 3, nslots = 256 / ncg;
   const int b = blockIdx.y, blk = blockIdx.x;
@@ -420,13 +418,8 @@ __global__ void __launch_bounds__(256) channel_sum_kernel(const T* __restrict__ 
   for (int c = threadIdx.x; c < C; c += 256) {
     float s = 0.f;
     for (int k = 0; k < nslots; ++k) s += red[(k * ncg + (c >> 3)) * 8 + (c & 7)];
-    if (part) {   // deterministic: [B][gridDim.x][C] partials, chs_reduce_kernel finishes
-      part[((long long)b * gridDim.x + blk) * C + c] = s;
-      continue;
-    }
-    if (out_bc) atomicAdd(out_bc + (long long)b * bc_stride + c, s);
-    if (out_c) atomicAdd(out_c + c, s);
-    if (out_c2) atomicAdd(out_c2 + c, s);
+    // [B][gridDim.x][C] partials; chs_reduce_kernel adds them in workgroup order
+    part[((long long)b * gridDim.x + blk) * C + c] = s;
   }
 }
 
@@ -473,23 +466,25 @@ __global__ void __launch_bounds__(256) emb_bwd_w_kernel(const float* __restrict_
   }
 }
 
-// dsil[b][e] += sum_r W[r][e] * dEb[b][r]: 64 e x 4 row groups per block,
-// row chunks of 32 over grid.z, fp32 atomics
-__global__ void __launch_bounds__(256) emb_bwd_x_kernel(const float* __restrict__ dEb, int R, int n,
-                                                       const float* __restrict__ W, int E,
-                                                       float* __restrict__ dsil) {
-  __shared__ float red[256];
+// dsil[b][e] += sum_r W[r][e] * dEb[b][r]: one 1024-thread block per (16 e, b),
+// 64 row groups over all n rows, the group sums added in group order -- one
+// writer per element, a fixed summation order (no atomics: deterministic)
+__global__ void __launch_bounds__(1024) emb_bwd_x_kernel(const float* __restrict__ dEb, int R, int n,
+                                                        const float* __restrict__ W, int E,
+                                                        float* __restrict__ dsil) {
+  __shared__ float red[1024];
   const int b = blockIdx.y;
-  const int e = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
-  const int r0 = blockIdx.z * 32;
+  const int e = blockIdx.x * 16 + (threadIdx.x & 15), rg = threadIdx.x >> 4;
   float s = 0.f;
   if (e < E)
-    for (int r = r0 + rg; r < r0 + 32 && r < n; r += 4) s += W[(long long)r * E + e] * dEb[(long long)b * R + r];
+    for (int r = rg; r < n; r += 64) s += W[(long long)r * E + e] * dEb[(long long)b * R + r];
   red[threadIdx.x] = s;
   __syncthreads();
-  if (rg == 0 && e < E)
-    atomicAdd(dsil + (long long)b * E + e, red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] +
-                                              red[threadIdx.x + 192]);
+  if (rg == 0 && e < E) {
+    float t = 0.f;
+    for (int q = 0; q < 64; ++q) t += red[threadIdx.x + 16 * q];
+    dsil[(long long)b * E + e] += t;
+  }
 }
 
 // time_embed MLP backward (unet.py:534-539): one workgroup, batch looped.
@@ -582,8 +577,7 @@ int launch_emb_bwd(const float* dEb, int R, int n, int B, const float* temb, int
   hipLaunchKernelGGL(emb_bwd_w_kernel, dim3((unsigned)ceil_div((long long)n * E, 256)), dim3(256), 0, s, dEb, R, n,
                      B, temb, E, dw, db, dcb, acc);
   CWDM_LAUNCHED();
-  hipLaunchKernelGGL(emb_bwd_x_kernel, dim3((unsigned)ceil_div(E, 64), B, (unsigned)ceil_div(n, 32)), dim3(256), 0, s,
-                     dEb, R, n, W, E, dsil);
+  hipLaunchKernelGGL(emb_bwd_x_kernel, dim3((unsigned)ceil_div(E, 16), B), dim3(1024), 0, s, dEb, R, n, W, E, dsil);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }
@@ -804,8 +798,8 @@ extern "C" int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V
   CWDM_REQUIRE(C > 0 && cs >= ((C + 7) / 8) * 8 && cs % 8 == 0 && cs <= 2048, CWDM_E_UNSUPPORTED,
                "cwdm_channel_sum: stride must be a multiple of 8 covering C (<= 2048)");
   CWDM_REQUIRE(B > 0 && B < 65536 && V > 0, CWDM_E_SHAPE, "cwdm_channel_sum: empty input");
-  CWDM_REQUIRE(!workspace || ws_bytes >= cwdm_channel_sum_workspace_bytes(B, V, C), CWDM_E_WORKSPACE,
-               "cwdm_channel_sum: workspace too small");
+  CWDM_REQUIRE(workspace && ws_bytes >= cwdm_channel_sum_workspace_bytes(B, V, C), CWDM_E_WORKSPACE,
+               "cwdm_channel_sum: workspace (cwdm_channel_sum_workspace_bytes) missing or too small");
   const long long nb = channel_sum_blocks(V, C);
   const long long vpb = ceil_div(V, nb);
   dim3 grid((unsigned)nb, (unsigned)B);
@@ -813,16 +807,13 @@ extern "C" int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V
   float* part = reinterpret_cast<float*>(workspace);
   dispatch_dtype(dtype, [&](auto tag) -> int {
     using T = decltype(tag);
-    hipLaunchKernelGGL(channel_sum_kernel<T>, grid, dim3(256), 0, s, (const T*)src, (long long)V, C, cs, vpb,
-                       out_bc, (long long)bc_stride, out_c, out_c2, part);
+    hipLaunchKernelGGL(channel_sum_kernel<T>, grid, dim3(256), 0, s, (const T*)src, (long long)V, C, cs, vpb, part);
     return CWDM_OK;
   });
   CWDM_LAUNCHED();
-  if (part) {
-    hipLaunchKernelGGL(chs_reduce_kernel, dim3((unsigned)ceil_div(C, 64)), dim3(1024), 0, s, part, (int)nb, C, out_bc,
-                       (long long)bc_stride, out_c, out_c2, (int)B);
-    CWDM_LAUNCHED();
-  }
+  hipLaunchKernelGGL(chs_reduce_kernel, dim3((unsigned)ceil_div(C, 64)), dim3(1024), 0, s, part, (int)nb, C, out_bc,
+                     (long long)bc_stride, out_c, out_c2, (int)B);
+  CWDM_LAUNCHED();
   return CWDM_OK;
 }
 

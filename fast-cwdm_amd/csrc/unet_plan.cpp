@@ -596,7 +596,6 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
 extern thread_local unsigned* g_sg_sync;
 int64_t sg_sync_bytes(int ksplit);
 bool head_eligible(const cwdm_conv3d_desc* d);
-extern thread_local int g_wgrad_ws_zeroed;  // wgrad.hip
 extern thread_local std::vector<PackJob>* g_pack_batch;  // conv3d.hip
 int pack_batch_run(std::vector<PackJob>& jobs, int dtype, PackJob* table, std::vector<PackJob>& cache, hipStream_t s);
 // conv3d_v4.hip: where conv3d_v4_forward's GroupNorm pre-pass writes the
@@ -1383,12 +1382,6 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
   // (every call: a caller may run segments on a fresh grad workspace)
   CWDM_HIP(hipMemsetAsync(gb + G.sync, 0, cwdm::sg_sync_bytes(2), s));
   SgSyncScope sync_scope(gb + G.sync);
-  // the wgrad scratch: zeroed once here, each wgrad's finishing pass leaves it zeroed
-  CWDM_HIP(hipMemsetAsync(gb + G.wgws, 0, G.wgws_bytes, s));
-  struct WgZeroScope {
-    WgZeroScope() { cwdm::g_wgrad_ws_zeroed = 1; }
-    ~WgZeroScope() { cwdm::g_wgrad_ws_zeroed = 0; }
-  } wg_zero_scope;
   auto P = [&](int64_t off) { return reinterpret_cast<const float*>(pk + off); };
   auto GR = [&](int pi) { return grads + u->goff[pi]; };
   auto act = [&](int id) -> const void* {

@@ -14,7 +14,10 @@
 // so each wave holds its 7 taps x 64 x 32 fp32 accumulators in AGPRs):
 //   * tile = 32*MC output channels x 32 input channels x all taps; K is walked
 //     in bricks of 16x4x4 voxels (a range of bricks per workgroup, split over
-//     the grid; partial tiles are combined with fp32 atomics).
+//     the grid).  Every (brick range, tile) unit stores its partial tile into
+//     the range's slab of the workspace; wg_reduce_kernel then adds the slabs
+//     into dw in range order -- the result does not depend on which workgroup
+//     finishes first (no fp32 atomics: two runs are bitwise identical).
 //   * per brick: the halo of the two 16-channel input chunks (one LDS image
 //     each, 32-B rows) and the brick's dY rows [voxel][co] are committed from
 //     registers that were loaded while the previous brick's MFMAs ran.
@@ -37,7 +40,7 @@ struct WgradParams {
   ConvParams cp;          // grid + U sources (a* for 3x3x3, b* for 1x1)
   const void* dy;
   int dy_cs, cout, cin, taps;
-  float* dw;
+  float* part;            // [S = gridDim.x][taps][cout][cin] partial slabs
   int tx, ty, tz;         // bricks per axis
   long long nbricks;      // B * tx * ty * tz
   long long per;          // bricks per workgroup
@@ -157,11 +160,11 @@ __device__ __forceinline__ void wg_brick_mfma(const unsigned char* halo, const u
   mfmas(fa1, fb1);
 }
 
-// combine: fp32 atomics into the [tap][co][ci] scratch -- one accumulator
-// register is two 128-B row segments (ci contiguous), the full-rate atomic
-// shape; OIDHW order would scatter the 64 lanes over 64 rows (~17x slower)
+// the unit's partial tile -> its slab [tap][co][ci] (plain stores: one
+// accumulator register is two 128-B row segments, ci contiguous; OIDHW order
+// would scatter the 64 lanes over 64 rows); wg_reduce_kernel transposes
 template <int MC, int TAPS>
-__device__ __forceinline__ void wg_combine(float* dw, const f32x16 (&acc)[TAPS == 27 ? 7 : 1][MC], int cout, int cin,
+__device__ __forceinline__ void wg_combine(float* slab, const f32x16 (&acc)[TAPS == 27 ? 7 : 1][MC], int cout, int cin,
                                            int co0, int ci0, int ntap, int wv, int lane) {
   constexpr int NT = TAPS == 27 ? 7 : 1;
   const int ci = ci0 + (lane & 31);
@@ -174,7 +177,7 @@ __device__ __forceinline__ void wg_combine(float* dw, const f32x16 (&acc)[TAPS =
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int co = co0 + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-          if (co < cout && ci < cin) atomicAdd(dw + ((long long)tap * cout + co) * cin + ci, acc[k][m][i]);
+          if (co < cout && ci < cin) slab[((long long)tap * cout + co) * cin + ci] = acc[k][m][i];
         }
     }
   }
@@ -294,7 +297,29 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradParams p) {
     }
   }
 
-  wg_combine<MC, TAPS>(p.dw, acc, p.cout, p.cin, co0, ci0, ntap, wv, lane);
+  if constexpr (TAPS == 1) {
+    // 1x1: the four waves hold partial sums of the same tile (they split the
+    // K-steps): waves 1-3 hand theirs over through LDS and wave 0 adds them in
+    // wave order before the store
+    __syncthreads();   // the last brick's operand reads are done
+    float* xs = reinterpret_cast<float*>(smem);
+    if (wv > 0) {
+#pragma unroll
+      for (int m = 0; m < MC; ++m)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) xs[(((wv - 1) * MC + m) * 16 + i) * 64 + lane] = acc[0][m][i];
+    }
+    __syncthreads();
+    if (wv > 0) return;
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+#pragma unroll
+      for (int m = 0; m < MC; ++m)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[0][m][i] += xs[((w * MC + m) * 16 + i) * 64 + lane];
+  }
+  wg_combine<MC, TAPS>(p.part + (long long)blockIdx.x * p.taps * p.cout * p.cin, acc, p.cout, p.cin, co0, ci0, ntap,
+                       wv, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -315,7 +340,7 @@ struct WgDmaParams {
   int units, upx;              // (brick range, channel tile) units; units per XCD
   const unsigned char* act; long long act_bs;  // per-batch bytes of U (cin * SV * esz)
   const unsigned char* dy; long long dy_bs;    // per-batch bytes of dY (V * dy_cs * esz)
-  float* dw;
+  float* part;                 // [S][cout][cin][27] partial slabs (dw's OIDHW order), one per brick range
 };
 
 // One LDS-DMA of 16 B per lane (lane l -> lds + 16 l), issued by inline asm so
@@ -435,11 +460,11 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
     if (bi + 1 < be) issue(bi + 1, smem + ((bi - bb + 1) & 1) * BUF);
     wg_brick_mfma<T, MC, 27>(cur, cur + C::DY_OFF, acc, toff, ntap, wv, lane);
   }
-  // combine straight into dw (OIDHW, fp32): per 32-channel half m of the tile the
-  // four waves' taps meet in LDS as [co 32][ci 32][tap 27] (the stages are
-  // free now), then every row co -- 32 ci x 27 taps = 864 contiguous floats of
-  // dw -- goes out as coalesced atomics.  No scratch, no memset, no
-  // transposing pass.
+  // the partial tile -> the brick range's slab in dw's OIDHW order: per 32-channel
+  // half m of the tile the four waves' taps meet in LDS as [co 32][ci 32][tap 27]
+  // (the stages are free now), then every row co -- 32 ci x 27 taps = 864
+  // contiguous floats -- goes out as coalesced stores (wg_reduce_kernel adds the
+  // slabs in range order: deterministic)
   float* T3 = reinterpret_cast<float*>(smem);
   const int cil = lane & 31;
 #pragma unroll
@@ -458,9 +483,10 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
     }
     __syncthreads();
     const int ncol = min(32, p.cout - co0 - 32 * m), nci = min(32, p.cin - ci0);
+    float* slab = p.part + sx * ((long long)p.cout * p.cin * 27);
     for (int r = 0; r < ncol; ++r) {
-      float* row = p.dw + ((long long)(co0 + 32 * m + r) * p.cin + ci0) * 27;
-      for (int e = tid; e < nci * 27; e += 256) atomicAdd(row + e, T3[r * 864 + e]);
+      float* row = slab + ((long long)(co0 + 32 * m + r) * p.cin + ci0) * 27;
+      for (int e = tid; e < nci * 27; e += 256) row[e] = T3[r * 864 + e];
     }
   }
 }
@@ -477,7 +503,7 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
 // U (16 channels, 32-B rows) + the 64 dY rows -- lands in LDS by LDS-DMA,
 // double-buffered, and feeds the transposed-read MFMA operands of the 3x3x3
 // kernels (tap offset 0).  Wave w owns input channels [32 w, +32) of the tile.
-// Partial tiles go straight into dw (OIDHW) as full-rate fp32 atomics.
+// Partial tiles go to the stage range's slab; wg_reduce_kernel adds the slabs.
 struct Wg1Params {
   const unsigned char* u0; const unsigned char* u1;
   int c0, c1, cin;
@@ -487,7 +513,7 @@ struct Wg1Params {
   long long per;    // stages per unit
   int nco, nci;     // 64-channel co tiles x 128-channel ci tiles
   int units, upx;   // (stage range, tile) units; units per XCD
-  float* dw;
+  float* part;      // [S][cout][cin] partial slabs, one per stage range
 };
 constexpr int W1_NV = 64;
 constexpr int W1_IMG = W1_NV * 32 + 128;         // one 16-channel chunk image (+128 B: complementary banks)
@@ -584,8 +610,79 @@ __global__ void __launch_bounds__(256) wgrad1_kernel(Wg1Params p) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int co = co0 + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-      if (co < p.cout) atomicAdd(p.dw + (long long)co * p.cin + ci, acc[m][i]);
+      if (co < p.cout) p.part[(sr * p.cout + co) * p.cin + ci] = acc[m][i];
     }
+}
+
+// dw += sum over the S partial slabs, in slab order.  A 256-thread block is
+// (256 / R) columns x R row groups; column c owns 4 consecutive slab elements
+// (16-byte loads), row group r sums slabs r, r + R, ... in increasing order (8
+// loads in flight), and the R group sums are added in group order -- the same
+// sum on every run for a given S.  R = min(16, ceil(S / 8)) (host): few slabs
+// (the small levels) -> one row group and 1024 elements per block; many (the
+// 128^3 level's 128) -> 16 groups of 8 slabs.  perm: the slabs are
+// [taps][cout][cin] (wgrad_kernel) and dw is OIDHW.
+template <int R>
+__global__ void __launch_bounds__(256) wg_reduce_kernel(const float* __restrict__ part, int S, long long n,
+                                                       float* __restrict__ dw, int cout, int cin, int taps, int perm) {
+  constexpr int NC = 256 / R;
+  const int c = threadIdx.x % NC, r = threadIdx.x / NC;
+  const long long j = ((long long)blockIdx.x * NC + c) * 4;   // n % 4 == 0 (cin % 32 == 0)
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (j < n) {
+    const float* p = part + j;
+    int k = r;
+    for (; k + 7 * R < S; k += 8 * R) {
+      float4 u[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) u[e] = *reinterpret_cast<const float4*>(p + (long long)(k + e * R) * n);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a.x += u[e].x; a.y += u[e].y; a.z += u[e].z; a.w += u[e].w; }
+    }
+    for (; k < S; k += R) {
+      const float4 u = *reinterpret_cast<const float4*>(p + (long long)k * n);
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    }
+  }
+  if constexpr (R > 1) {
+    __shared__ float4 red[256];
+    red[threadIdx.x] = a;
+    __syncthreads();
+    if (r) return;
+#pragma unroll
+    for (int q = 1; q < R; ++q) {
+      const float4 u = red[q * NC + c];
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    }
+  }
+  if (j >= n) return;
+  const float t[4] = {a.x, a.y, a.z, a.w};
+  const long long cc = (long long)cout * cin;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long long jj = j + e;
+    const long long o = perm ? (jj % cc) * taps + jj / cc : jj;   // [tap][co][ci] -> [co][ci][tap]
+    dw[o] += t[e];
+  }
+}
+
+int launch_wg_reduce(const float* part, long long S, long long n, float* dw, int cout, int cin, int taps, bool perm,
+                     hipStream_t s) {
+  CWDM_REQUIRE(S > 0 && S < (1LL << 31) && n % 4 == 0, CWDM_E_SHAPE, "cwdm_conv3d_wgrad: bad partial slab count");
+  const int R = S >= 128 ? 16 : S >= 64 ? 8 : S >= 32 ? 4 : S >= 16 ? 2 : 1;
+  const long long nb = ceil_div(n / 4, (long long)(256 / R));
+  CWDM_REQUIRE(nb < (1LL << 31), CWDM_E_SHAPE, "cwdm_conv3d_wgrad: weight gradient too large");
+  const int pm = perm ? 1 : 0;
+  const dim3 g((unsigned)nb), b(256);
+  switch (R) {
+    case 16: hipLaunchKernelGGL(wg_reduce_kernel<16>, g, b, 0, s, part, (int)S, n, dw, cout, cin, taps, pm); break;
+    case 8: hipLaunchKernelGGL(wg_reduce_kernel<8>, g, b, 0, s, part, (int)S, n, dw, cout, cin, taps, pm); break;
+    case 4: hipLaunchKernelGGL(wg_reduce_kernel<4>, g, b, 0, s, part, (int)S, n, dw, cout, cin, taps, pm); break;
+    case 2: hipLaunchKernelGGL(wg_reduce_kernel<2>, g, b, 0, s, part, (int)S, n, dw, cout, cin, taps, pm); break;
+    default: hipLaunchKernelGGL(wg_reduce_kernel<1>, g, b, 0, s, part, (int)S, n, dw, cout, cin, taps, pm); break;
+  }
+  CWDM_LAUNCHED();
+  return CWDM_OK;
 }
 
 template <typename T>
@@ -607,13 +704,13 @@ int launch_wg1(const cwdm_wgrad_desc* d, hipStream_t s) {
   S = ceil_div(q.nst, q.per);
   q.units = (int)(S * ntiles);
   q.upx = (q.units + 7) / 8;
-  q.dw = d->dw;
+  q.part = reinterpret_cast<float*>(d->workspace);
   constexpr int smem = 2 * W1_BUF;
   auto k = wgrad1_kernel<T>;
   CWDM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, smem));
   hipLaunchKernelGGL(k, dim3((unsigned)(8LL * q.upx)), dim3(256), smem, s, q);
   CWDM_LAUNCHED();
-  return CWDM_OK;
+  return launch_wg_reduce(q.part, S, (long long)q.cout * q.cin, d->dw, q.cout, q.cin, 1, false, s);
 }
 
 // the 1x1 kernel's shapes: 16-bit, source boundary on a 16-channel chunk, < 2 GB per stage row block
@@ -621,21 +718,6 @@ bool wg1_eligible(const cwdm_wgrad_desc* d) {
   if (d->ksize != 1 || !dtype_half(d->dtype) || d->u_gn || d->u_mode != 0 || d->u_cm) return false;
   if (d->u_c0 % 16 || (d->u_c0 + d->u_c1) % 32 || d->dy_cs % 8) return false;
   return d->B * d->D * d->H * d->W * (int64_t)(d->u_c0 + d->u_c1) * 2 < (1LL << 40);
-}
-
-// dW[co][ci][tap] += scratch[tap][co][ci]
-// (rezero: leave the scratch zeroed for the next call -- the plan's backward
-// zeroes it once per call instead of once per conv)
-__global__ void __launch_bounds__(256) wgrad_finish_kernel(float* __restrict__ scr, float* __restrict__ dw,
-                                                          int cout, int cin, int taps, int rezero) {
-  const long long n = (long long)cout * cin * taps;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const int tap = (int)(i % taps);
-  const long long oc = i / taps;  // co * cin + ci
-  const long long si = (long long)tap * cout * cin + oc;
-  dw[i] += scr[si];
-  if (rezero) scr[si] = 0.f;
 }
 
 template <typename T, int MC, int MODE, bool GN, int TAPS>
@@ -675,10 +757,6 @@ int launch_wg_dma(const WgDmaParams& p, dim3, hipStream_t s) {
 
 using namespace cwdm;
 
-namespace cwdm {
-thread_local int g_wgrad_ws_zeroed = 0;  // the plan's backward: the scratch is zero on entry, leave it zero
-}
-
 extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream) {
   CWDM_REQUIRE(d, CWDM_E_INVALID, "cwdm_conv3d_wgrad: null desc");
   CWDM_REQUIRE(d->u0 && d->dy && d->dw, CWDM_E_INVALID, "cwdm_conv3d_wgrad: null pointer");
@@ -708,7 +786,7 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
     c.b0 = d->u0; c.bc0 = d->u_c0; c.b1 = d->u1; c.bc1 = d->u_c1;
   }
   p.dy = d->dy; p.dy_cs = d->dy_cs; p.cout = d->cout; p.cin = cin; p.taps = d->ksize == 3 ? 27 : 1;
-  p.dw = reinterpret_cast<float*>(d->workspace);
+  p.part = reinterpret_cast<float*>(d->workspace);
   p.tx = (int)ceil_div(d->W, WBX); p.ty = (int)ceil_div(d->H, WBY); p.tz = (int)ceil_div(d->D, WBZ);
   p.nbricks = d->B * (long long)p.tx * p.ty * p.tz;
   const int mc = d->cout > 32 ? 2 : 1;
@@ -726,7 +804,6 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
   hipStream_t s = (hipStream_t)stream;
   const bool gn = d->u_gn != nullptr;
   const long long nw = (long long)d->cout * cin * p.taps;
-  const int zeroed = g_wgrad_ws_zeroed;
   int rc;
   static const bool wg1_on = !std::getenv("CWDM_WG1_OFF");   // A/B knob: the brick kernel for 1x1
   if (wg1_on && wg1_eligible(d)) {
@@ -746,7 +823,7 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
     const long long sv = (long long)q.SD * q.SH * q.SW, V = d->D * d->H * d->W;
     q.act = reinterpret_cast<const unsigned char*>(d->u0); q.act_bs = sv * cin * 2;
     q.dy = reinterpret_cast<const unsigned char*>(d->dy); q.dy_bs = V * d->dy_cs * 2;
-    q.dw = d->dw;  // accumulated into directly (OIDHW)
+    q.part = p.part;
     CWDM_REQUIRE(q.act_bs < (1LL << 31) && q.dy_bs < (1LL << 31), CWDM_E_UNSUPPORTED,
                  "cwdm_conv3d_wgrad: u_cm sources above 2 GB per batch");
     rc = d->dtype == CWDM_F16
@@ -754,21 +831,27 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
                         : (d->u_mode ? launch_wg_dma<f16_t, 1, 1>(q, grid, s) : launch_wg_dma<f16_t, 1, 0>(q, grid, s)))
              : (mc == 2 ? (d->u_mode ? launch_wg_dma<bf16_t, 2, 1>(q, grid, s) : launch_wg_dma<bf16_t, 2, 0>(q, grid, s))
                         : (d->u_mode ? launch_wg_dma<bf16_t, 1, 1>(q, grid, s) : launch_wg_dma<bf16_t, 1, 0>(q, grid, s)));
-    return rc;
+    if (rc) return rc;
+    return launch_wg_reduce(p.part, S, nw, d->dw, d->cout, cin, 27, false, s);
   }
-  if (!zeroed) CWDM_HIP(hipMemsetAsync(d->workspace, 0, nw * 4, s));
   rc = dispatch_dtype(d->dtype, [&](auto tag) -> int {
     using T = decltype(tag);
     return mc == 2 ? dispatch_wg<T, 2>(p, d->u_mode, gn, grid, s) : dispatch_wg<T, 1>(p, d->u_mode, gn, grid, s);
   });
   if (rc) return rc;
-  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)ceil_div(nw, 256)), dim3(256), 0, s,
-                     reinterpret_cast<float*>(d->workspace), d->dw, d->cout, cin, p.taps, zeroed);
-  CWDM_LAUNCHED();
-  return CWDM_OK;
+  return launch_wg_reduce(p.part, S, nw, d->dw, d->cout, cin, p.taps, true, s);
 }
 
+// the partial slabs: at most S_max brick / stage ranges of cout x cin x ksize^3
+// fp32 each (the launch code's S never exceeds these bounds)
 extern "C" int64_t cwdm_conv3d_wgrad_workspace_bytes(int cout, int cin, int ksize) {
   if (cout <= 0 || cin <= 0 || (ksize != 1 && ksize != 3)) return -1;
-  return (int64_t)cout * cin * ksize * ksize * ksize * 4;
+  const int mc = cout > 32 ? 2 : 1;
+  const int64_t tiles = ceil_div((int64_t)cout, 32 * mc) * ceil_div((int64_t)cin, 32);
+  int64_t smax = std::max<int64_t>(1, 256 / tiles);                      // wgrad_kernel / wgrad_dma_kernel
+  if (ksize == 1) {
+    const int64_t t1 = ceil_div((int64_t)cout, 64) * ceil_div((int64_t)cin, 128);
+    smax = std::max(smax, std::max<int64_t>(1, 768 / t1));                // wgrad1_kernel
+  }
+  return smax * cout * cin * ksize * ksize * ksize * 4;
 }

@@ -386,8 +386,10 @@ int cwdm_gn_apply(const void* x0, int c0, const void* x1, int c1, const float* s
  * forward staged it (concat of u0/u1, optional GroupNorm scale/shift + SiLU,
  * optional nearest-x2 upsample of a half-resolution source).  dw is fp32 OIDHW
  * and is accumulated into (dw += dW).  workspace: fp32 scratch of
- * cwdm_conv3d_wgrad_workspace_bytes (zeroed by the call; partial tiles meet
- * there with full-rate atomics before one transposing pass into dw).
+ * cwdm_conv3d_wgrad_workspace_bytes: every (K range, channel tile) unit stores
+ * its partial tile into its range's slab, and one pass adds the slabs into dw
+ * in range order -- no atomics, two calls on the same inputs are bitwise
+ * identical.  Nothing in it needs zeroing or survives the call.
  * ksize 1: the 1x1 skip conv. */
 typedef struct {
   int dtype;
@@ -432,10 +434,9 @@ int cwdm_resample_add(void* dst, const void* src, int C, int64_t B, int64_t d, i
 
 /* Per-channel sums of src [B][V][cs] (first C channels): out_bc[b*bc_stride+c]
  * += sum_v, out_c[c] += sum_{b,v}, out_c2 likewise (each may be NULL).  Bias
- * gradients and the emb-projection gradient.  With a workspace of
- * cwdm_channel_sum_workspace_bytes the per-workgroup sums are added in a fixed
- * order (bitwise repeatable); workspace NULL adds them with fp32 atomics
- * (arrival order: not repeatable). */
+ * gradients and the emb-projection gradient.  workspace (required): fp32
+ * partials of cwdm_channel_sum_workspace_bytes; the per-workgroup sums are
+ * added in a fixed order (bitwise repeatable; no atomics). */
 int64_t cwdm_channel_sum_workspace_bytes(int64_t B, int64_t V, int C);
 int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V, int C, int cs,
                      float* out_bc, int64_t bc_stride, float* out_c, float* out_c2,
