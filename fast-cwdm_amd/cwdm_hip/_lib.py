@@ -150,6 +150,7 @@ _PROTOS = {
     "cwdm_gn_apply": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, vp, i64, i64, ctypes.c_int, vp, vp]),
     "cwdm_conv3d_set_path": (ctypes.c_int, [ctypes.c_int]),
     "cwdm_debug_v5_grid": (ctypes.c_int, [ctypes.c_int]),
+    "cwdm_debug_head2": (ctypes.c_int, [ctypes.c_int]),
     "cwdm_debug_conv_stamps": (ctypes.c_int, [vp]),
     "cwdm_conv3d_wgrad": (ctypes.c_int, [ctypes.POINTER(WgradDesc), vp]),
     "cwdm_conv3d_wgrad_workspace_bytes": (i64, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),

@@ -363,6 +363,14 @@ int cwdm_conv3d_set_path(int path);
  * CU.  Returns the previous cap. */
 int cwdm_debug_v5_grid(int n);
 
+/* Diagnostics / tests only: which output-head kernel runs -- 0 = the
+ * second-generation head wherever its shape holds (64 input channels,
+ * W % 16, H % 4, D % 4; default), -1 = the first head only, n > 0 = the
+ * second head with its persistent grid capped at n workgroups (several z
+ * columns per workgroup on small shapes).  Returns the previous setting.
+ * Initial value: env CWDM_HEAD2=0 -> -1, else 0. */
+int cwdm_debug_head2(int mode);
+
 /* Diagnostics only: per-workgroup timestamps of the DMA-staged conv kernel
  * (24 x u64 per workgroup: s_memtime at start, after the prologue, after each of
  * the first 16 chunks, at the end; [22] HW_ID, [23] XCC_ID) into the device

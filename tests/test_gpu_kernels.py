@@ -550,11 +550,24 @@ def test_conv3d_small_grid_kernel_vs_torch(case, dtype_name):
     _run_conv_case(case, dtype_name, True)
 
 
+HEAD_CASES = [((4, 4, 32), 1, 64), ((8, 8, 64), 2, 64), ((4, 8, 32), 1, 32),
+              # second head: W % 16 only, partial z segments, several columns per workgroup
+              ((12, 8, 48), 1, 64), ((100, 32, 64), 1, 64), ((8, 128, 128), 2, 64)]
+
+
+@pytest.mark.parametrize("gen", [-1, 0, 3], ids=["head1", "head2", "head2_grid3"])
 @pytest.mark.parametrize("dtype_name", ["bf16", "fp16"])
-@pytest.mark.parametrize("grid,B,cin", [((4, 4, 32), 1, 64), ((8, 8, 64), 2, 64), ((4, 8, 32), 1, 32)])
-def test_output_head_kernel_vs_torch(grid, B, cin, dtype_name):
-    """The narrow-output head kernel (conv3d_head.hip: GN+SiLU fused, 16x16x32
-    MFMA, 8 of 16 output lanes real): bf16 / fp16 operands, fp32 output, vs F.conv3d."""
+@pytest.mark.parametrize("grid,B,cin", HEAD_CASES)
+def test_output_head_kernel_vs_torch(grid, B, cin, dtype_name, gen):
+    """The narrow-output head kernels (conv3d_head.hip: GN+SiLU fused, 16x16x32
+    MFMA, 8 of 16 output lanes real; the second one a z-rolling ring of halo
+    planes filled by helper waves): bf16 / fp16 operands, fp32 output, vs
+    F.conv3d; the two heads agree to fp32 rounding where both run."""
+    from cwdm_hip._lib import lib
+    if gen == -1 and grid[2] % 32:
+        pytest.skip("the first head needs W % 32")
+    if gen == 3 and (cin != 64 or grid[0] * grid[1] * grid[2] > 300000):
+        pytest.skip("grid cap: the second head's larger cases")
     dtype, tdt = _DTN[dtype_name]
     g = torch.Generator().manual_seed(11)
     D, H, W = grid
@@ -567,8 +580,18 @@ def test_output_head_kernel_vs_torch(grid, B, cin, dtype_name):
     gn = torch.stack([scale, shift], -1).contiguous()
     h = F.silu(x * scale[:, :, None, None, None] + shift[:, :, None, None, None]).to(tdt).float()
     ref = F.conv3d(h, w, bias, padding=1)
-    out, _ = _conv_call(dtype, (B, D, H, W), _nd(x).to(DEV, tdt), None, 0, gn.to(DEV),
-                        w.to(DEV), bias.to(DEV), out_f32=True, stats=False)
+    prev = lib().cwdm_debug_head2(gen)
+    try:
+        out, _ = _conv_call(dtype, (B, D, H, W), _nd(x).to(DEV, tdt), None, 0, gn.to(DEV),
+                            w.to(DEV), bias.to(DEV), out_f32=True, stats=False)
+        if gen != -1 and grid[2] % 32 == 0:
+            lib().cwdm_debug_head2(-1)
+            out1, _ = _conv_call(dtype, (B, D, H, W), _nd(x).to(DEV, tdt), None, 0, gn.to(DEV),
+                                 w.to(DEV), bias.to(DEV), out_f32=True, stats=False)
+            # the same products; the second head adds the two 32-channel halves' sums at the end
+            assert rel_err(out, out1) < 1e-5
+    finally:
+        lib().cwdm_debug_head2(prev)
     assert rel_err(_nc(out.float().cpu()), ref) < (1e-2 if dtype_name == "bf16" else 1e-3)
 
 
