@@ -37,7 +37,7 @@ for _p in (os.path.join(ROOT, "fast-cwdm_amd"), ROOT):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r03", "r02", "r01")]
+TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r04", "r03", "r02", "r01")]
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3
 
@@ -637,7 +637,8 @@ def main():
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_unit": "HBM bytes per step of those launches (2 x FETCH_SIZE + WRITE_SIZE, "
                                      f"{traffic_src})",
-                     "kernel": f"implicit-GEMM MFMA conv kernels (conv3d_v4 DMA-staged, conv3d_sg small-grid, brick, output head: "
+                     "kernel": f"implicit-GEMM MFMA conv kernels (conv3d_v5 warp-specialised, conv3d_v4 DMA-staged, conv3d_sg "
+                               f"small-grid, brick, head2 output head: "
                                f"{n_conv} launches per step, {conv_ms:.2f} ms, {conv_flops / 1e12:.2f} TFLOP)"},
     }
     if cpu_state is not None:

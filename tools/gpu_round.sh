@@ -4,13 +4,13 @@
 # the training step (train_bench line + its kernel-trace stats).
 # usage: tools/gpu_round.sh TAG [skip-tests]
 set -e -o pipefail
-TAG=${1:-r02}
+TAG=${1:-r04}
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
 if [ "$2" != "skip-tests" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1
   tail -3 $O/pytest_gpu.log
 fi
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err && timeout -k 10 200 python -u tools/volume_bench.py > $O/volume_bench.json 2>&1
@@ -24,4 +24,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_train -o run --ou
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o pmc --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 $SIDE > $O/pmc_fetch.log 2>&1
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o pmc --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 $SIDE > $O/pmc_write.log 2>&1
 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_MFMA -d $O/pmc_mfma -o pmc --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 $SIDE > $O/pmc_mfma.log 2>&1
+cd $R
+python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write $O/pmc_traffic.json
+python3 tools/trace_step.py $O/trace --last > $O/step_timeline.txt
+python3 tools/trace_step.py $O/trace_train --last > $O/train_timeline.txt
 echo done

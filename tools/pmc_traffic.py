@@ -17,8 +17,9 @@ import glob
 import json
 import sys
 
-CONV_FAMILY = ("conv3d_v4_kernel", "conv3d_sg_kernel", "conv3d_kernel", "conv3d_wide_kernel", "conv3d_reduce_kernel",
-               "splitk_sum_kernel", "gn_apply_kernel", "gn_apply_skip_kernel", "head_conv_kernel")
+CONV_FAMILY = ("conv3d_v5_kernel", "conv3d_v4_kernel", "conv3d_sg_kernel", "conv3d_kernel", "conv3d_wide_kernel",
+               "conv3d_reduce_kernel", "splitk_sum_kernel", "gn_apply_kernel", "gn_apply_skip_kernel", "head_conv_kernel",
+               "head2_kernel")
 
 
 def last_step(d, counter):
@@ -31,7 +32,8 @@ def last_step(d, counter):
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     idx = [i for i, r in enumerate(rows) if "time_embed_kernel" in r["Kernel_Name"]]
     steps = [rows[a:b] for a, b in zip(idx[:-1], idx[1:])
-             if any("conv3d_v4_kernel<unsigned short" in r["Kernel_Name"] for r in rows[a:b])]
+             if any(("conv3d_v4_kernel<unsigned short" in r["Kernel_Name"] or "conv3d_v5_kernel<unsigned short" in r["Kernel_Name"])
+                    for r in rows[a:b])]
     if steps:
         return steps[-2] if len(steps) > 1 else steps[-1]   # not the last: side-leg setup may follow it
     raise SystemExit("no complete bf16 step in " + d)
@@ -64,7 +66,8 @@ def main():
         e[0] += 1
         e[1] += rb
         e[2] += wb
-    mfma = ("conv3d_v4_kernel", "conv3d_sg_kernel", "conv3d_kernel", "conv3d_wide_kernel", "head_conv_kernel")
+    mfma = ("conv3d_v5_kernel", "conv3d_v4_kernel", "conv3d_sg_kernel", "conv3d_kernel", "conv3d_wide_kernel",
+            "head_conv_kernel", "head2_kernel")
     mk = {k: v for k, v in per.items() if k in mfma}
     res = {"scope": "conv family of one 128^3 bf16 denoising step (bench.py)", "launches": n,
            "mfma_conv_kernels": {"kernels": sorted(mk), "launches": sum(v[0] for v in mk.values()),
