@@ -14,3 +14,5 @@ for c in L0_64_8_out L0_64_8_out_nogn; do
   CWDM_HEAD2=1 CWDM_LIB=ablib/libcwdm_stamps.so CWDM_ALLOW_STALE_LIB=1 timeout -k 10 120 python -u tools/head_stamps.py $c 2>/dev/null > $O/st_$c.txt
   cat $O/st_$c.txt
 done
+CWDM_LIB=ablib/libcwdm_stamps.so CWDM_ALLOW_STALE_LIB=1 timeout -k 10 200 python -u tools/head_step_stamps.py 2>&1 | grep -v amdgpu.ids > $O/st_step.txt
+cat $O/st_step.txt

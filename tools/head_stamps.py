@@ -30,6 +30,10 @@ def main():
     conv_bench.run_case(case, spec, 1, 1)
     torch.cuda.synchronize()
     lib().cwdm_debug_conv_stamps(None)
+    report(case, buf, nwg)
+
+
+def report(case, buf, nwg):
     st = [r for r in buf.view(nwg, 64).cpu().tolist() if r[0] != 0]
     mean = lambda v: sum(v) / max(len(v), 1)  # noqa: E731
     print(f"{case}: {len(st)} workgroups; cycles from the previous tile barrier, mean (min / max)")
