@@ -173,4 +173,24 @@ struct GapplyFuse {
   bool used;
 };
 extern thread_local GapplyFuse* g_gapply;
+
+// The U-Net plan's forward: a GroupNorm finalize (statistics partials -> scale /
+// shift, cwdm_gn_finalize) offered to the consumer conv.  Where the conv's
+// GroupNorm+SiLU pre-pass runs at a small grid it computes the finalize itself
+// (gn_fin_apply, conv3d_v4.hip: each workgroup reduces the partials of its 16
+// channels); any other route runs cwdm_gn_finalize first (gnfin_flush).  Either
+// way ss / mr are written for later readers (the backward).
+struct GnFinFuse {
+  const float* s0; long long p0; int c0;
+  const float* s1; long long p1; int c1;
+  const float* gamma; const float* beta;
+  int groups; long long voxels; float eps;
+  float* ss;   // [B][C][2] -- the a_gn pointer of the consumer conv
+  float* mr;   // [B][groups][2]
+  long long B;
+  bool used;
+};
+extern thread_local GnFinFuse* g_gnfin;
+// run the offered finalize now if it is pending for d (d->a_gn == its ss)
+int gnfin_flush(const cwdm_conv3d_desc* d, hipStream_t s);
 }  // namespace cwdm

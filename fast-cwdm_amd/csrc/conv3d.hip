@@ -433,13 +433,23 @@ extern "C" int cwdm_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stre
   CWDM_REQUIRE(d->res_mode < 0 || d->res, CWDM_E_INVALID, "cwdm_conv3d_forward: residual pointer missing");
   CWDM_REQUIRE(d->out_dtype == CWDM_F32 || d->out_dtype == d->dtype, CWDM_E_INVALID,
                "cwdm_conv3d_forward: output dtype must be fp32 or the compute dtype");
-  if (head_eligible(d)) return head_conv_forward(d, (hipStream_t)stream);
-  if (pw_eligible(d)) return pw_forward(d, (hipStream_t)stream);
+  // (an offered GroupNorm finalize, GnFinFuse, runs first on every route but the
+  // DMA-staged one, whose pre-pass may take it)
+  int rc;
+  if (head_eligible(d)) {
+    if ((rc = gnfin_flush(d, (hipStream_t)stream))) return rc;
+    return head_conv_forward(d, (hipStream_t)stream);
+  }
+  if (pw_eligible(d)) {
+    if ((rc = gnfin_flush(d, (hipStream_t)stream))) return rc;
+    return pw_forward(d, (hipStream_t)stream);
+  }
   // (the accurate fast mode's split-bf16 kernel takes fp32 shapes of any size: the same host path)
   if (v4_eligible(d) || (d->a_w_split && v5_eligible(d, false))) {
     const int64_t need = v4_workspace_bytes(d);
     if (need == 0 || (d->workspace && d->ws_bytes >= need)) return conv3d_v4_forward(d, (hipStream_t)stream);
   }
+  if ((rc = gnfin_flush(d, (hipStream_t)stream))) return rc;
   return legacy_conv3d_forward(d, stream);
 }
 

@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(512) head2_kernel(HeadParams p, Head2Geo g) {
       __syncthreads();   // B_tz0: the prologue planes are in
       for (int tz = tz0; tz < tz1; ++tz) {
         const int z0 = tz * 4;
-        const int ks = tz - tz0;
+        [[maybe_unused]] const int ks = tz - tz0;
         H2_STAMP(1 + 3 * ks, tid == 0 && ks < 8 && u == u0);
         // SAMP: the previous tile's sampler step runs after this tile's MFMAs (the
         // MFMA waves wait for the fill there)
@@ -623,7 +623,7 @@ __global__ void __launch_bounds__(512) head2_kernel(HeadParams p, Head2Geo g) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __syncthreads();   // B_tz0
       for (int tz = tz0; tz < tz1; ++tz) {
-        const int ks = tz - tz0;
+        [[maybe_unused]] const int ks = tz - tz0;
         // under tile tz's MFMAs: fetch and transform tile tz + 2's planes (issuing
         // them one tile earlier, after the stores, measured slower: 271 vs 227 us
         // in the step -- they queue behind the epilogue's stores)

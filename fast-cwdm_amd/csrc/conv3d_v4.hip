@@ -100,6 +100,93 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x0,
   }
 }
 
+// GroupNorm finalize + SiLU(GN(x)) pre-pass in one launch (small grids,
+// GnFinFuse): workgroup (16-channel chunk j, voxel block, batch entry) first
+// reduces the statistics partials of its 16 channels -- parts x 16 (sum, sum^2)
+// pairs, 128 contiguous bytes per part -- in fp64 (thread (part slice r,
+// channel cl) over parts r, r + 16, ..., then the 16 slices and the group's
+// channels in order), derives (scale, shift) as gn_finalize does, and applies
+// them to its voxels, writing the chunk-major layout (32 bytes of the chunk per
+// voxel).  Workgroups of voxel block 0 also write ss / mr for later readers.
+// 16-bit types; a chunk lies in one source (c0 % 16 == 0); cpg divides 16.
+struct GnFinApplyArgs {
+  const void* x0; int c0; const void* x1; int c1;
+  const float* s0; long long p0; const float* s1; long long p1;
+  const float* gamma; const float* beta; int groups; double n; float eps;
+  float* ss; float* mr; void* out;
+  int V, vblk;   // voxels per batch entry, voxels per workgroup
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) gn_fin_apply_kernel(GnFinApplyArgs a) {
+  const int j = blockIdx.x, vb = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
+  const int C = a.c0 + a.c1, cpg = C / a.groups, c16 = 16 * j;
+  const bool first = c16 < a.c0;
+  const int cs = first ? a.c0 : a.c1, cl0 = first ? c16 : c16 - a.c0;
+  const long long P = first ? a.p0 : a.p1;
+  const float2* part = reinterpret_cast<const float2*>(first ? a.s0 : a.s1) + (long long)b * P * cs + cl0;
+  __shared__ double r1[256], r2[256];
+  __shared__ float tab[32];
+  {
+    const int cl = t & 15, r = t >> 4;
+    double s = 0.0, q = 0.0;
+    for (long long k = r; k < P; k += 16) {
+      const float2 u = part[k * cs + cl];
+      s += (double)u.x;
+      q += (double)u.y;
+    }
+    r1[t] = s;
+    r2[t] = q;
+  }
+  __syncthreads();
+  if (t < 16) {
+    double s = 0.0, q = 0.0;
+    for (int r = 0; r < 16; ++r) { s += r1[r * 16 + t]; q += r2[r * 16 + t]; }
+    r1[t] = s;   // (slot t of slice 0 is read only by this thread)
+    r2[t] = q;
+  }
+  __syncthreads();
+  if (t < 16) {
+    const int g0 = (t / cpg) * cpg;   // the group's first channel within the chunk
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < cpg; ++k) { s += r1[g0 + k]; q += r2[g0 + k]; }
+    const double mean = s / a.n;
+    double var = q / a.n - mean * mean;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + (double)a.eps));
+    const float meanf = (float)mean;
+    const int c = c16 + t;
+    const float sc = a.gamma[c] * rstd;
+    const float sh = a.beta[c] - meanf * sc;
+    tab[2 * t] = sc;
+    tab[2 * t + 1] = sh;
+    if (vb == 0) {
+      a.ss[((long long)b * C + c) * 2] = sc;
+      a.ss[((long long)b * C + c) * 2 + 1] = sh;
+      if (t % cpg == 0 && a.mr) {
+        const int g = c / cpg;
+        a.mr[((long long)b * a.groups + g) * 2] = meanf;
+        a.mr[((long long)b * a.groups + g) * 2 + 1] = rstd;
+      }
+    }
+  }
+  __syncthreads();
+  const int h = t & 1, vs = t >> 1;
+  float sa[8], sb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) silu_aff_coef(tab[2 * (8 * h + e)], tab[2 * (8 * h + e) + 1], sa[e], sb[e]);
+  const T* xs = reinterpret_cast<const T*>(first ? a.x0 : a.x1) + (long long)b * a.V * cs + cl0 + 8 * h;
+  T* out = reinterpret_cast<T*>(a.out) + (((long long)b * (C / 16) + j) * a.V) * 16 + 8 * h;
+  const int v0 = vb * a.vblk, v1 = min(a.V, v0 + a.vblk);
+  for (int v = v0 + vs; v < v1; v += 128) {
+    float f[8];
+    unpack<T>(*reinterpret_cast<const u32x4*>(xs + (long long)v * cs), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = silu_aff(f[e], sa[e], sb[e]);
+    *reinterpret_cast<u32x4*>(out + (long long)v * 16) = pack<T>(f);
+  }
+}
+
 inline int64_t align256(int64_t n) { return (n + 255) & ~(int64_t)255; }
 
 int64_t src_voxels(const cwdm_conv3d_desc* d) {
@@ -211,6 +298,49 @@ int legacy_conv3d_forward(const cwdm_conv3d_desc* d, cwdm_stream_t stream);
 // backward that follows this dgrad conv into its epilogue (GbwdFuse, conv3d_v4.hpp
 // V4Params::gx0); taken only by the 16-bit fast epilogue without K split
 thread_local GbwdFuse* g_gbwd = nullptr;
+thread_local GnFinFuse* g_gnfin = nullptr;
+
+int gnfin_flush(const cwdm_conv3d_desc* d, hipStream_t s) {
+  GnFinFuse* f = g_gnfin;
+  if (!f || f->used || !d->a_gn || f->ss != d->a_gn) return CWDM_OK;
+  f->used = true;
+  return cwdm_gn_finalize(f->s0, f->p0, f->c0, f->s1, f->p1, f->c1, f->gamma, f->beta, f->groups, f->B, f->voxels,
+                          f->eps, f->ss, f->mr, s);
+}
+
+namespace {
+// the fused finalize + pre-pass applies: 16-bit, every 16-channel chunk in one
+// source and whole groups, few partials per chunk (the small grids: <= 256 parts)
+bool gn_fin_fusable(const GnFinFuse& f, int dtype, int c0, int c1) {
+  const int C = c0 + c1;
+  if (!dtype_half(dtype) || C % 16 || c0 % 16 || f.c0 != c0 || f.c1 != c1 || f.groups <= 0 || C % f.groups) return false;
+  const int cpg = C / f.groups;
+  return cpg <= 16 && 16 % cpg == 0 && f.p0 <= 256 && (c1 == 0 || f.p1 <= 256);
+}
+
+int gn_fin_apply(const GnFinFuse& f, const void* x0, int c0, const void* x1, int c1, int64_t B, int64_t V, int dtype,
+                 void* out, hipStream_t s) {
+  GnFinApplyArgs a{};
+  a.x0 = x0; a.c0 = c0; a.x1 = x1; a.c1 = c1;
+  a.s0 = f.s0; a.p0 = f.p0; a.s1 = f.s1; a.p1 = f.p1;
+  a.gamma = f.gamma; a.beta = f.beta; a.groups = f.groups;
+  a.n = (double)((c0 + c1) / f.groups) * (double)f.voxels; a.eps = f.eps;
+  a.ss = f.ss; a.mr = f.mr; a.out = out;
+  CWDM_REQUIRE(V < (1LL << 31) && V * (c0 + c1) < (1LL << 31), CWDM_E_UNSUPPORTED, "gn_fin_apply: grid too large");
+  a.V = (int)V;
+  // ~512 workgroups in all
+  const int nchunk = (c0 + c1) / 16;
+  long long nvb = std::max<long long>(1, 512 / (nchunk * B));
+  a.vblk = (int)std::max<long long>(128, ceil_div(V, nvb));
+  nvb = ceil_div(V, (long long)a.vblk);
+  CWDM_REQUIRE(B < 65536 && nvb < 65536, CWDM_E_UNSUPPORTED, "gn_fin_apply: grid too large");
+  const dim3 grid((unsigned)nchunk, (unsigned)nvb, (unsigned)B);
+  if (dtype == CWDM_F16) hipLaunchKernelGGL(gn_fin_apply_kernel<f16_t>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(gn_fin_apply_kernel<bf16_t>, grid, dim3(256), 0, s, a);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+}  // namespace
 
 // the backward's dgrad conv whose epilogue may take the GroupNorm-backward
 // reduce (v4 only): only where the conv leaves VALU room -- at 128^3 the
@@ -400,6 +530,12 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   // inference only -- the training forward keeps the activated input for wgrad
   const float* agn = nullptr;
   if (d->a_gn && !g_act_keep && v5_eligible(d, true)) agn = d->a_gn;
+  // an offered GroupNorm finalize (GnFinFuse): fused into the pre-pass below where it fits, else run now
+  GnFinFuse* fin = (g_gnfin && !g_gnfin->used && d->a_gn && g_gnfin->ss == d->a_gn) ? g_gnfin : nullptr;
+  if (fin && (agn || !gn_fin_fusable(*fin, d->dtype, c0, c1))) {
+    if ((rc = gnfin_flush(d, s))) return rc;
+    fin = nullptr;
+  }
   if (d->a_gn && !agn) {
     // the activated input: in the workspace, or (training) where the plan keeps
     // it for the backward's DMA-staged wgrad
@@ -410,7 +546,12 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     } else {
       ws += align256(d->B * SV * (c0 + c1) * esz);
     }
-    if ((rc = gn_apply(a0, c0, a1, c1, d->a_gn, d->B, SV, d->dtype, act, s, 1))) return rc;
+    if (fin) {
+      fin->used = true;
+      if ((rc = gn_fin_apply(*fin, a0, c0, a1, c1, d->B, SV, d->dtype, act, s))) return rc;
+    } else if ((rc = gn_apply(a0, c0, a1, c1, d->a_gn, d->B, SV, d->dtype, act, s, 1))) {
+      return rc;
+    }
     a0 = act; c0 = c0 + c1; a1 = nullptr; c1 = 0;
     a0_cm = 1;
   }

@@ -1011,7 +1011,35 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
       for (int k = 0; k < 4; ++k) u->hooks[i].ev[k >> 1][k & 1] = u->ev[4 * i + k];
     u->ev_used = 0;
   }
+  // GroupNorm finalize offered to its consumer conv (cwdm::GnFinFuse: at the
+  // small grids the conv's pre-pass computes it; any other route runs it
+  // first).  A pending one whose consumer is not the next step runs on its own.
+  // Env CWDM_GNFIN=0: every finalize as its own launch (A/B switch).
+  static const bool fin_on = [] { const char* e = std::getenv("CWDM_GNFIN"); return !(e && e[0] == '0'); }();
+  int fin_pend = -1;
+  auto fin_args = [&](int gi, cwdm::GnFinFuse& f) {
+    const auto& g = u->gns[gi];
+    f.s0 = reinterpret_cast<const float*>(wb + L.s_off[g.src0]); f.p0 = L.s_parts[g.src0];
+    f.c0 = u->tensors[g.src0].channels;
+    f.s1 = g.src1 >= 0 ? reinterpret_cast<const float*>(wb + L.s_off[g.src1]) : nullptr;
+    f.p1 = g.src1 >= 0 ? L.s_parts[g.src1] : 0; f.c1 = g.src1 >= 0 ? u->tensors[g.src1].channels : 0;
+    f.gamma = P(g.gamma_off); f.beta = P(g.beta_off); f.groups = u->cfg.num_groups;
+    f.voxels = (D >> g.level) * (H >> g.level) * (W >> g.level); f.eps = 1e-5f;
+    f.ss = reinterpret_cast<float*>(wb + L.ss_off[g.ss_id]); f.mr = reinterpret_cast<float*>(wb + L.mr_off[g.ss_id]);
+    f.B = B;
+    f.used = false;
+  };
+  auto flush_fin = [&]() -> int {
+    if (fin_pend < 0) return CWDM_OK;
+    cwdm::GnFinFuse f{};
+    fin_args(fin_pend, f);
+    fin_pend = -1;
+    return cwdm_gn_finalize(f.s0, f.p0, f.c0, f.s1, f.p1, f.c1, f.gamma, f.beta, f.groups, B, f.voxels, f.eps, f.ss,
+                            f.mr, stream);
+  };
   for (const auto& st : u->steps) {
+    if (fin_pend >= 0 && !(st.kind == 1 && u->convs[st.idx].gn == u->gns[fin_pend].ss_id) && (rc = flush_fin()))
+      return rc;
     if (st.kind == 2) {
       const auto& ps = u->pools[st.idx];
       const int lv = ps.level_out;
@@ -1048,16 +1076,8 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
       continue;
     }
     if (st.kind == 0) {
-      const auto& g = u->gns[st.idx];
-      const int lv = g.level;
-      const int64_t vox = (D >> lv) * (H >> lv) * (W >> lv);
-      const int c0 = u->tensors[g.src0].channels, c1 = g.src1 >= 0 ? u->tensors[g.src1].channels : 0;
-      if ((rc = cwdm_gn_finalize(reinterpret_cast<const float*>(wb + L.s_off[g.src0]), L.s_parts[g.src0], c0,
-                                 g.src1 >= 0 ? reinterpret_cast<const float*>(wb + L.s_off[g.src1]) : nullptr,
-                                 g.src1 >= 0 ? L.s_parts[g.src1] : 0, c1, P(g.gamma_off), P(g.beta_off),
-                                 u->cfg.num_groups, B, vox, 1e-5f, reinterpret_cast<float*>(wb + L.ss_off[g.ss_id]),
-                                 reinterpret_cast<float*>(wb + L.mr_off[g.ss_id]), stream)))
-        return rc;
+      fin_pend = st.idx;
+      if (!fin_on && (rc = flush_fin())) return rc;
       continue;
     }
     const auto& cs = u->convs[st.idx];
@@ -1095,6 +1115,7 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
       const auto& c2 = u->convs[cs.skip_conv];
       const int64_t vpb = d.D * d.H * d.W;
       void* act = keep && L.keep_off[st.idx] >= 0 ? wb + L.keep_off[st.idx] : wb + L.split;
+      if ((rc = flush_fin())) return rc;
       if ((rc = cwdm::gn_apply_skip(d.a0, d.a_c0, d.a1, d.a_c1, d.a_gn, B, vpb, u->cfg.dtype, pk + c2.wsk_off,
                                     c2.cout, act, wb + L.skipbuf, s)))
         return rc;
@@ -1107,11 +1128,25 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
         d.res = wb + L.skipbuf; d.res_mode = 0;
       }
       if (samp && cs.out < 0 && cwdm::head_sampler_eligible(&d, samp)) {
+        if ((rc = flush_fin())) return rc;
         if ((rc = cwdm::head_sampler_forward(&d, samp, s))) return rc;
         if (fused) *fused = 1;
       } else {
         cwdm::ActKeepScope ks(keep && L.keep_off[st.idx] >= 0 ? wb + L.keep_off[st.idx] : nullptr);
-        if ((rc = cwdm_conv3d_forward(&d, stream))) return rc;
+        cwdm::GnFinFuse ff{};
+        const bool offer = fin_pend >= 0 && d.a_gn == reinterpret_cast<const float*>(wb + L.ss_off[u->gns[fin_pend].ss_id]);
+        if (offer) {
+          fin_args(fin_pend, ff);
+          fin_pend = -1;
+          cwdm::g_gnfin = &ff;
+        } else if ((rc = flush_fin())) {
+          return rc;
+        }
+        rc = cwdm_conv3d_forward(&d, stream);
+        cwdm::g_gnfin = nullptr;
+        if (rc) return rc;
+        CWDM_REQUIRE(!offer || ff.used, CWDM_E_INVALID,
+                     "cwdm_unet_forward: conv " + std::to_string(st.idx) + " did not take its GroupNorm finalize");
         CWDM_REQUIRE(!ks.ptr || ks.used(), CWDM_E_INVALID,
                      "cwdm_unet_forward: conv " + std::to_string(st.idx) + " did not keep its activated input");
       }
@@ -1122,7 +1157,7 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
     }
     ++conv_i;
   }
-  return CWDM_OK;
+  return flush_fin();
 }
 
 extern "C" int cwdm_unet_forward(cwdm_unet* u, const void* packed, const void* x, const float* t, float* out,
