@@ -31,6 +31,8 @@ CASES = {
     "L0_192_64_cat_nogn": (128, 128, 64, 64, 0, False, 0, -1),
     "L1_128_128_gn": (64, 128, 0, 128, 0, True, 0, -1),
     "L1_128_128_nogn": (64, 128, 0, 128, 0, False, 0, -1),
+    "L1_64_64_nogn": (64, 64, 0, 64, 0, False, 0, -1),
+    "L0_128_64_nogn": (128, 128, 0, 64, 0, False, 0, -1),
     "L2_128_128_gn": (32, 128, 0, 128, 0, True, 0, -1),
     "L3_256_256_gn": (16, 256, 0, 256, 0, True, 0, -1),
     "L3_256_256_res": (16, 256, 0, 256, 0, False, 0, 0),
