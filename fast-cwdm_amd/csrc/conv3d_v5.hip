@@ -263,28 +263,36 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   const long long HW = (long long)p.H * p.W, V = (long long)p.D * HW;
   const unsigned rowb = (unsigned)p.W * (unsigned)p.cout * 2u, planeb = (unsigned)HW * (unsigned)p.cout * 2u;
   float s1[8], s2[8];   // this lane's statistics over both drain parts of a tile
+  // the residual rows of drain part `part` of tile tt (this lane's rows i = 8 part .. + 7): loaded
+  // one chunk ahead of their drain (part 0 under the tile's last chunk, part 1 under part 0's
+  // chunk), so their latency is not on the helper's path at the tile seam
+  u32x4 rq[8];
+  auto drain_load = [&](const V4Tile& tt, int part) {
+    if (p.rmode < 0) return;
+    const int ox = tt.x0 + 8 * h + r8;
+    const bool xin = ox < p.W;
+    const long long rV = p.rmode == 1 ? V / 8 : V;
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(reinterpret_cast<const T16*>(p.res) + (long long)tt.b * rV * p.cout), (short)0,
+        (int)(rV * p.cout * 2), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = 8 * part + k;
+      const int oy = tt.y0 + (i & 3), oz = tt.z0 + (i >> 2);
+      unsigned rv = p.rmode == 1 ? (unsigned)(((oz >> 1) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1))
+                                 : (unsigned)((oz * p.H + oy) * p.W + ox);
+      rq[k] = __builtin_amdgcn_raw_buffer_load_b128(
+          rr, xin ? rv * (unsigned)p.cout * 2u + (unsigned)(tt.ct * 64 + 8 * q) * 2u : 0xFFFFFFF0u, 0, 0);
+    }
+  };
   // drain part `part` of staged tile tt: rows i = 8 part .. + 7 of this lane = voxels (x0 + 8 h + r8,
-  // y0 + (i & 3), z0 + (i >> 2)), channels tile + 8 q .. + 7; part 0 from halo buffer sb, part 1 from the spare
+  // y0 + (i & 3), z0 + (i >> 2)), channels tile + 8 q .. + 7; part 0 from halo buffer sb, part 1 from the
+  // spare; the residual rows are in rq (drain_load)
   auto drain = [&](const V4Tile& tt, int part, int sb) {
     const int ox = tt.x0 + 8 * h + r8;
     const bool xin = ox < p.W;
     const float xm = xin ? 1.f : 0.f;
-    u32x4 rq[8], sv[8];
-    if (p.rmode >= 0) {
-      const long long rV = p.rmode == 1 ? V / 8 : V;
-      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(reinterpret_cast<const T16*>(p.res) + (long long)tt.b * rV * p.cout), (short)0,
-          (int)(rV * p.cout * 2), 0x00020000);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int i = 8 * part + k;
-        const int oy = tt.y0 + (i & 3), oz = tt.z0 + (i >> 2);
-        unsigned rv = p.rmode == 1 ? (unsigned)(((oz >> 1) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1))
-                                   : (unsigned)((oz * p.H + oy) * p.W + ox);
-        rq[k] = __builtin_amdgcn_raw_buffer_load_b128(
-            rr, xin ? rv * (unsigned)p.cout * 2u + (unsigned)(tt.ct * 64 + 8 * q) * 2u : 0xFFFFFFF0u, 0, 0);
-      }
-    }
+    u32x4 sv[8];
     const unsigned char* base = smem + (part ? V5Cfg::STG1 : sb * C::HALO_B);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -381,13 +389,18 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
       // the drain part runs first: its residual wait (the compiler's) then also retires chunk
       // k + 1's pieces, and part 0 frees this wave's blocks of the buffer chunk k + 2 goes to
       const bool drained = pend > 0;
-      if (pend == 2) { drain(dt, 0, (gch + 2) % 3); pend = 1; }
+      // (part 0 is followed by part 1's residual loads: 8 stores + 8 loads in flight before the DMA)
+      const bool d0 = pend == 2 && p.rmode >= 0;
+      if (pend == 2) { drain(dt, 0, (gch + 2) % 3); drain_load(dt, 1); pend = 1; }
       else if (pend == 1) { drain(dt, 1, 0); pend = 0; }
       if (drained) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const bool iss = issue_next((gch + 2) % 3);
       if (!(lastc && !more)) {
         // chunk k + 1 (the rest of this tile, or the next tile's first chunk): own pieces landed?
-        if (drained) {
+        if (d0) {
+          if (iss) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + 16) : "memory");
+          else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        } else if (drained) {
           if (iss) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + 8) : "memory");
           else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         } else {
@@ -397,6 +410,8 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
         const V4Tile& t1 = lastc ? nxt : cur;
         transform(t1.x0, t1.y0, t1.z0, (gch + 1) % 3);
       }
+      // the finishing tile's part-0 residual rows, under its last chunk
+      if (lastc) drain_load(cur, 0);
       if (first && more) issue_bias(nxt, (it + 1) & 1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       V5_STAMP(34 + gch, tid == 256 && gch < 16);
@@ -410,9 +425,10 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
     }
     cur = nxt;
   }
-  // the last tile (the MFMA waves have left)
+  // the last tile (the MFMA waves have left; its part-0 residual rows were loaded under its last chunk)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   drain(dt, 0, (gch + 2) % 3);
+  drain_load(dt, 1);
   drain(dt, 1, 0);
   V5_STAMP(52, tid == 256);
 }
@@ -759,6 +775,7 @@ bool v5_eligible(const cwdm_conv3d_desc* d, bool gn) {
   if (d->res_mode < -1 || d->res_mode > 1) return false;
   if (d->W < kWideMinW || d->H % 4 || d->D % 4 || d->cout % 64) return false;
   if (d->D * d->H * d->W * d->cout * 2 >= 0xFFFFE000LL) return false;
+  if (d->a_c0 + d->a_c1 < 32) return false;   // >= 2 chunks per tile: a tile's drain spans two chunks
   if (gbwd_grid_ok(d)) return false;   // the backward's fused dgrad instance is v4's
   static const int ncu = [] {
     int dev = 0, n = 0;
@@ -766,7 +783,10 @@ bool v5_eligible(const cwdm_conv3d_desc* d, bool gn) {
       return 256;
     return n > 0 ? n : 256;
   }();
-  return path == 2 || v4_items(d) >= 2LL * ncu;
+  // tiles per CU below which v4 (two workgroups per CU) keeps the conv (env
+  // CWDM_V5_MIN_TPC, A/B knob)
+  static const double min_tpc = [] { const char* e = std::getenv("CWDM_V5_MIN_TPC"); return e ? std::atof(e) : 2.0; }();
+  return path == 2 || (double)v4_items(d) >= min_tpc * ncu;
 }
 
 // sources a0 (c0 channels; chunk-major if a0_cm) and a1 (c1, channels-last);
