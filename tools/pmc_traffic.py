@@ -18,8 +18,8 @@ import json
 import sys
 
 CONV_FAMILY = ("conv3d_v5_kernel", "conv3d_v4_kernel", "conv3d_sg_kernel", "conv3d_kernel", "conv3d_wide_kernel",
-               "conv3d_reduce_kernel", "splitk_sum_kernel", "gn_apply_kernel", "gn_apply_skip_kernel", "head_conv_kernel",
-               "head2_kernel")
+               "conv3d_reduce_kernel", "splitk_sum_kernel", "gn_apply_kernel", "gn_apply_skip_kernel", "gn_fin_apply_kernel",
+               "head_conv_kernel", "head2_kernel")
 
 
 def last_step(d, counter):
