@@ -227,7 +227,9 @@ int64_t v4_items(const cwdm_conv3d_desc* d) {
 int64_t v4_ksplit_target() {
   static const int64_t t = [] {
     const char* e = std::getenv("CWDM_V4_KSPLIT_TARGET");
-    return e ? (int64_t)std::atoll(e) : (int64_t)128;
+    // 64 (r04; was 128): config 5's 28^3 64-channel down-block convs (49 tiles)
+    // then run unsplit on 32-channel tiles: 44 -> 19 us against the split legacy path
+    return e ? (int64_t)std::atoll(e) : (int64_t)64;
   }();
   return t;
 }

@@ -744,7 +744,7 @@ int64_t v4_items(const cwdm_conv3d_desc* d);
 bool gbwd_grid_ok(const cwdm_conv3d_desc* d);
 
 // the warp-specialised kernel takes a conv of the DMA path when it is a 16-bit
-// fast-epilogue conv without K split and with at least two tiles per CU
+// fast-epilogue conv without K split and with at least one tile per CU (CWDM_V5_MIN_TPC)
 // (env CWDM_V5: 0 off, 1 GroupNorm'd inputs only, 2 every eligible conv, 3 (default)
 // every eligible conv with the GroupNorm applied by the cwdm_gn_apply pre-pass: the
 // in-LDS transform costs the helper waves more issue cycles than the MFMA waves
@@ -784,8 +784,9 @@ bool v5_eligible(const cwdm_conv3d_desc* d, bool gn) {
     return n > 0 ? n : 256;
   }();
   // tiles per CU below which v4 (two workgroups per CU) keeps the conv (env
-  // CWDM_V5_MIN_TPC, A/B knob)
-  static const double min_tpc = [] { const char* e = std::getenv("CWDM_V5_MIN_TPC"); return e ? std::atof(e) : 2.0; }();
+  // CWDM_V5_MIN_TPC, A/B knob; 1 since r04: config 5's 56^3 64-channel convs,
+  // 392 tiles, 57 -> 53 us on v5)
+  static const double min_tpc = [] { const char* e = std::getenv("CWDM_V5_MIN_TPC"); return e ? std::atof(e) : 1.0; }();
   return path == 2 || (double)v4_items(d) >= min_tpc * ncu;
 }
 

@@ -275,9 +275,12 @@ __global__ void __launch_bounds__(256) sampler2_kernel(cwdm_sampler_args a, S3w 
 // per 56^3 step); here each 16-lane group moves one whole 256-byte row.  Rows
 // are padded to 272 B so the per-thread row reads are conflict-free.  Bit-
 // identical to sampler2_kernel (same expressions in the same order).
+// CL = false: x_t and x_prev are channel-planar (voxel stride 1, the native
+// loop's NCDHW state): each thread moves its own voxel's 64 channels between
+// its row and HBM, one coalesced 256-byte wave access per channel.
 constexpr int S2V = 256;               // voxels per workgroup (one per thread)
 constexpr int S2P = 68;                // row pitch in floats (272 B)
-template <typename MirT>
+template <typename MirT, bool CL>
 __global__ void __launch_bounds__(256) sampler2_lds_kernel(cwdm_sampler_args a, S3w mo, S3w xt, S3w xp, S3w mi) {
   extern __shared__ __attribute__((aligned(16))) float tile[];   // [S2V][S2P]
   const int64_t nvox = a.d * a.h * a.w, total = a.B * nvox;
@@ -306,6 +309,13 @@ __global__ void __launch_bounds__(256) sampler2_lds_kernel(cwdm_sampler_args a, 
   const float* cf = a.coef + t * (a.per_band ? 64 * 8 : 8);
   float* row = tile + tid * S2P;
   float m[64];
+  // (planar x_t: the voxel's own channels, loads in flight during the model_out staging)
+  float xr[CL ? 1 : 64];
+  if constexpr (!CL) {
+    const float* src = a.x_t + b * xt.b + v;
+#pragma unroll
+    for (int q = 0; q < 64; ++q) xr[q] = live ? src[q * xt.c] : 0.f;
+  }
   stage_in(a.model_out, mo);
   __syncthreads();
 #pragma unroll
@@ -314,7 +324,13 @@ __global__ void __launch_bounds__(256) sampler2_lds_kernel(cwdm_sampler_args a, 
     m[4 * g] = u.x; m[4 * g + 1] = u.y; m[4 * g + 2] = u.z; m[4 * g + 3] = u.w;
   }
   __syncthreads();
-  stage_in(a.x_t, xt);
+  if constexpr (CL) {
+    stage_in(a.x_t, xt);
+  } else {
+#pragma unroll
+    for (int g = 0; g < 16; ++g)
+      *reinterpret_cast<float4*>(row + 4 * g) = make_float4(xr[4 * g], xr[4 * g + 1], xr[4 * g + 2], xr[4 * g + 3]);
+  }
   __syncthreads();
   if (a.mean_type == 1) {
 #pragma unroll
@@ -361,7 +377,14 @@ __global__ void __launch_bounds__(256) sampler2_lds_kernel(cwdm_sampler_args a, 
       }
     }
     *reinterpret_cast<float4*>(row + 4 * g) = make_float4(r[0], r[1], r[2], r[3]);
+    if constexpr (!CL) {
+      if (live) {
+        float* dst = a.x_prev + b * xp.b + v + (4 * g) * xp.c;
+        dst[0] = r[0]; dst[xp.c] = r[1]; dst[2 * xp.c] = r[2]; dst[3 * xp.c] = r[3];
+      }
+    }
   }
+  if (!CL && !a.mirror) return;
   __syncthreads();
   // rows out: x_prev (fp32) and the mirror (the next step's U-Net input channels)
 #pragma unroll 4
@@ -371,7 +394,7 @@ __global__ void __launch_bounds__(256) sampler2_lds_kernel(cwdm_sampler_args a, 
     if (j >= total) continue;
     const int64_t bb = j / nvox, vv = j - bb * nvox;
     const float4 u = *reinterpret_cast<const float4*>(tile + lv * S2P + 4 * g);
-    *reinterpret_cast<float4*>(a.x_prev + bb * xp.b + vv * xp.v + 4 * g) = u;
+    if constexpr (CL) *reinterpret_cast<float4*>(a.x_prev + bb * xp.b + vv * xp.v + 4 * g) = u;
     if (a.mirror) {
       MirT* o = reinterpret_cast<MirT*>(a.mirror) + bb * mi.b + vv * mi.v + 4 * g;
       if constexpr (sizeof(MirT) == 2) {
@@ -408,7 +431,10 @@ int sampler2_launch(const cwdm_sampler_args* a, hipStream_t s) {
   // aligned rows, Philox noise (or none), no pred_xstart output
   static const bool lds_on = [] { const char* e = std::getenv("CWDM_SAMPLER2_LDS"); return !(e && e[0] == '0'); }();
   const bool mir_ok = !a->mirror || ((vec & 32) && (a->mirror_dtype == CWDM_F32 ? ok(a->mirror, mi, 4) : true));
-  if (lds_on && (vec & 7) == 7 && !a->pred_xstart && !a->noise && mir_ok) {
+  // (or x_t / x_prev channel-planar: voxel stride 1, 4-byte aligned)
+  const bool planar = xt.v == 1 && xp.v == 1 && a->x_t && a->x_prev;
+  const bool cl = (vec & 6) == 6;
+  if (lds_on && (vec & 1) && (cl || planar) && !a->pred_xstart && !a->noise && mir_ok) {
     const dim3 g2((unsigned)ceil_div(a->B * a->d * a->h * a->w, S2V));
     const size_t sm = (size_t)S2V * S2P * 4;
     auto go = [&](auto k) -> int {
@@ -417,9 +443,9 @@ int sampler2_launch(const cwdm_sampler_args* a, hipStream_t s) {
       return (int)CWDM_OK;
     };
     int rc;
-    if (a->mirror && a->mirror_dtype == CWDM_BF16) rc = go(sampler2_lds_kernel<bf16_t>);
-    else if (a->mirror && a->mirror_dtype == CWDM_F16) rc = go(sampler2_lds_kernel<f16_t>);
-    else if (!a->mirror || a->mirror_dtype == CWDM_F32) rc = go(sampler2_lds_kernel<float>);
+    if (a->mirror && a->mirror_dtype == CWDM_BF16) rc = cl ? go(sampler2_lds_kernel<bf16_t, true>) : go(sampler2_lds_kernel<bf16_t, false>);
+    else if (a->mirror && a->mirror_dtype == CWDM_F16) rc = cl ? go(sampler2_lds_kernel<f16_t, true>) : go(sampler2_lds_kernel<f16_t, false>);
+    else if (!a->mirror || a->mirror_dtype == CWDM_F32) rc = cl ? go(sampler2_lds_kernel<float, true>) : go(sampler2_lds_kernel<float, false>);
     else return fail(CWDM_E_INVALID, "cwdm_sampler_step: bad mirror dtype");
     if (rc) return rc;
     CWDM_LAUNCHED();

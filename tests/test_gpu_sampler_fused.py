@@ -234,3 +234,16 @@ def test_sampler2_staged_kernel_equals_strided(clip, mean_type, per_band, update
     if mirror:
         assert torch.equal(mir[..., :64], out.to(mir.dtype))
         assert mir[..., 64:].abs().max() == 0
+    # the native loop's layout: channels-last model_out, channel-planar (NCDHW)
+    # x_t / x_prev -> the staged kernel's planar variant; also in place
+    for inplace in (False, True):
+        xs = x.clone()
+        outp = xs if inplace else torch.full_like(x, float("nan"))
+        if mirror:
+            mir.zero_()
+        ops.sampler_step(cl(mo), cs, xs, s, outp, s, None, (0, 0, 0), coef, t, diff.num_timesteps, B, d, h, w,
+                         mirror=mir, mr_s=ms, **kw)
+        assert torch.equal(outp, ref), inplace
+        if mirror:
+            assert torch.equal(mir[..., :64], cl(ref).to(mir.dtype))
+            assert mir[..., 64:].abs().max() == 0

@@ -44,6 +44,11 @@ CASES = {
     "C5_L1_256_128_cat": (28, 128, 128, 128, 0, True, 0, -1),
     "C5_L2_128_128_gn": (14, 128, 0, 128, 0, True, 0, -1),
     "C5_L0_64_64_gn": (56, 64, 0, 64, 0, True, 0, -1),
+    "C5_L0_64_64_nogn": (56, 64, 0, 64, 0, False, 0, -1),
+    "C5_L0_128_64_cat_nogn": (56, 64, 64, 64, 0, False, 0, -1),
+    # the down block's convs at 28^3 (64 -> 64 on the pooled input; conv2 adds the pooled x)
+    "C5_D1_64_64_nogn": (28, 64, 0, 64, 0, False, 0, -1),
+    "C5_D1_64_64_res": (28, 64, 0, 64, 0, False, 0, 0),
 }
 
 
