@@ -53,20 +53,24 @@ __device__ __forceinline__ float pw_dsilu(float z, float du) {
   return du * (s * (1.0f + z * (1.0f - s)));
 }
 
-template <typename T, bool GA>
-__global__ void __launch_bounds__(256, 2) pw_kernel(PwParams p) {
+// NM: 32-channel output blocks per workgroup (4: 128 channels, 2 waves / SIMD;
+// 2: 64 channels, the fused-apply instance -- 3 waves / SIMD to keep more of
+// its three input streams in flight)
+template <typename T, bool GA, int NM>
+__global__ void __launch_bounds__(256, NM == 2 ? 3 : 2) pw_kernel(PwParams p) {
+  constexpr int NC = 32 * NM;                      // output channels per workgroup
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const long long vt = blockIdx.x / p.nnb;
   const int nb = blockIdx.x % p.nnb;
   const long long row0 = vt * 256 + wv * 64;       // this wave's first voxel row (over B * V)
-  const int n0 = nb * 128;
-  // fused GroupNorm-backward apply (GA): the block's 128 channels' (sc, sh, k0,
+  const int n0 = nb * NC;
+  // fused GroupNorm-backward apply (GA): the block's NC channels' (sc, sh, k0,
   // k1, k2) for the (at most two) batch entries its 256 rows touch, in LDS
-  __shared__ float gk[2][5][128];
+  __shared__ float gk[2][5][NC];
   const long long b_lo = (vt * 256) / p.V;
   if (GA) {
-    for (int i = tid; i < 2 * 128; i += 256) {
-      const int bl = i >> 7, cl = i & 127, c = n0 + cl;
+    for (int i = tid; i < 2 * NC; i += 256) {
+      const int bl = i / NC, cl = i % NC, c = n0 + cl;
       const long long b = b_lo + bl;
       if (c < p.N && b * p.V < p.rows) {
         const float2 ss = *reinterpret_cast<const float2*>(p.gss + (b * p.N + c) * 2);
@@ -79,11 +83,11 @@ __global__ void __launch_bounds__(256, 2) pw_kernel(PwParams p) {
   }
   const int col = lane & 31, kg = lane >> 5;       // MFMA operand lane: column / row 0..31, K half
   const T* w = reinterpret_cast<const T*>(p.w);
-  f32x16 acc[2][4];
+  f32x16 acc[2][NM];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < NM; ++m)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[j][m][i] = 0.f;
 
@@ -103,25 +107,25 @@ __global__ void __launch_bounds__(256, 2) pw_kernel(PwParams p) {
     return *reinterpret_cast<const u32x4*>(w + pw_widx<T>(co, 16 * s + 8 * kg, p.K, p.NT));
   };
   const int ns = p.K / 16;
-  u32x4 a[4], b[2], an[4], bn[2];
+  u32x4 a[NM], b[2], an[NM], bn[2];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) a[m] = ldA(0, m);
+  for (int m = 0; m < NM; ++m) a[m] = ldA(0, m);
 #pragma unroll
   for (int j = 0; j < 2; ++j) b[j] = ldB(0, j);
   for (int s = 0; s < ns; ++s) {
     if (s + 1 < ns) {
 #pragma unroll
-      for (int m = 0; m < 4; ++m) an[m] = ldA(s + 1, m);
+      for (int m = 0; m < NM; ++m) an[m] = ldA(s + 1, m);
 #pragma unroll
       for (int j = 0; j < 2; ++j) bn[j] = ldB(s + 1, j);
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int m = 0; m < 4; ++m) mfma_acc(acc[j][m], a[m], b[j], (T*)nullptr);
+      for (int m = 0; m < NM; ++m) mfma_acc(acc[j][m], a[m], b[j], (T*)nullptr);
     if (s + 1 < ns) {
 #pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = an[m];
+      for (int m = 0; m < NM; ++m) a[m] = an[m];
 #pragma unroll
       for (int j = 0; j < 2; ++j) b[j] = bn[j];
     }
@@ -151,10 +155,10 @@ __global__ void __launch_bounds__(256, 2) pw_kernel(PwParams p) {
         return reinterpret_cast<T*>(p.out) + r * (p.out1 ? p.out_c0 : p.N) + c;
       };
       // (GA: half a row's loads at a time -- the fused apply's registers fit 2 waves / SIMD)
-      constexpr int MB = GA ? 2 : 4;
+      constexpr int MB = GA ? (NM == 2 ? 1 : 2) : NM;
 #pragma unroll
-      for (int m0 = 0; m0 < 4; m0 += MB) {
-      u32x4 qo[4][2], qx[4][2], qd[4][2];
+      for (int m0 = 0; m0 < NM; m0 += MB) {
+      u32x4 qo[NM][2], qx[NM][2], qd[NM][2];
 #pragma unroll
       for (int m = m0; m < m0 + MB; ++m)
 #pragma unroll
@@ -246,7 +250,7 @@ __global__ void __launch_bounds__(256, 2) pw_kernel(PwParams p) {
     if (r >= p.rows) continue;
     const int bb = (int)(r / p.V);
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < NM; ++m) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c = n0 + 32 * m + 8 * g + 4 * kg;   // 4 consecutive channels c .. c+3
@@ -302,23 +306,30 @@ int pw_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   p.NT = 32 * pick_nf(d->cout);   // the packed layout's rows per channel tile (cwdm_conv3d_pack)
   p.bias = d->bias; p.bias_bs = d->bias_bstride;
   p.out = d->out; p.out1 = d->out1; p.out_c0 = d->out_c0; p.accumulate = d->accumulate;
-  p.nnb = (int)ceil_div(d->cout, 128);
   if (g_gapply && !g_gapply->used && p.N % 8 == 0 && (!d->out1 || d->out_c0 % 8 == 0) && p.V >= 256 &&
       !d->bias) {
     p.gx0 = g_gapply->x0; p.gx1 = g_gapply->x1; p.gdu = g_gapply->du;
     p.gss = g_gapply->ss; p.gcoef = g_gapply->coef;
     g_gapply->used = true;
   }
+  const bool ga = p.gdu != nullptr;
+  // the fused apply on 64-channel blocks where 128-channel ones would leave a
+  // half-empty block (N = 192: 916 -> 770 us at 128^3; N = 128 stays on 128:
+  // 491 vs 526 us); env CWDM_PW_GA_NM = 2 / 4 forces one (A/B knob)
+  static const int ga_nm = [] { const char* e = std::getenv("CWDM_PW_GA_NM"); return e ? std::atoi(e) : 0; }();
+  const int nm = !ga ? 4 : (ga_nm == 2 || ga_nm == 4) ? ga_nm : (d->cout % 128 ? 2 : 4);
+  p.nnb = (int)ceil_div(d->cout, 32 * nm);
   const long long nblk = ceil_div(p.rows, 256) * p.nnb;
   CWDM_REQUIRE(nblk < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d (pointwise): grid too large");
   prof_begin(s);
-  const bool ga = p.gdu != nullptr;
   if (d->dtype == CWDM_F16) {
-    if (ga) hipLaunchKernelGGL((pw_kernel<f16_t, true>), dim3((unsigned)nblk), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((pw_kernel<f16_t, false>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    if (ga && nm == 2) hipLaunchKernelGGL((pw_kernel<f16_t, true, 2>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    else if (ga) hipLaunchKernelGGL((pw_kernel<f16_t, true, 4>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((pw_kernel<f16_t, false, 4>), dim3((unsigned)nblk), dim3(256), 0, s, p);
   } else {
-    if (ga) hipLaunchKernelGGL((pw_kernel<bf16_t, true>), dim3((unsigned)nblk), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((pw_kernel<bf16_t, false>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    if (ga && nm == 2) hipLaunchKernelGGL((pw_kernel<bf16_t, true, 2>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    else if (ga) hipLaunchKernelGGL((pw_kernel<bf16_t, true, 4>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((pw_kernel<bf16_t, false, 4>), dim3((unsigned)nblk), dim3(256), 0, s, p);
   }
   prof_end(s, 2.0 * p.rows * (double)p.N * p.K);
   CWDM_LAUNCHED();

@@ -358,6 +358,15 @@ __device__ __forceinline__ void wg_dma16(__amdgpu_buffer_rsrc_t r, unsigned char
                : "s"(la), "v"(voff), "s"(r)
                : "memory", "m0");
 }
+// (the same with the LDS destination as a wave-uniform LDS byte address: no
+// generic-pointer cast and null check per DMA)
+__device__ __forceinline__ void wg_dma16(__amdgpu_buffer_rsrc_t r, unsigned lds, unsigned voff) {
+  const unsigned la = __builtin_amdgcn_readfirstlane(lds);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(la), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
 #pragma clang diagnostic pop
 
 template <typename T, int MC, int MODE>
@@ -370,7 +379,8 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
   constexpr int DI = 256 * QPV / 64;     // dY wave instructions per brick
   constexpr int ESZ = (int)sizeof(T);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  // (wv wave-uniform in an SGPR: the DMAs' LDS destinations are scalar adds)
+  const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   // XCD-aware map of the 1-D grid: workgroups are dealt to the 8 XCDs round
   // robin, so the k-th workgroup of XCD j takes unit j * upx + k of the
   // range-major (brick range, channel tile) list -- the channel tiles of a
@@ -402,18 +412,67 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
       for (int i = 0; i < 16; ++i) acc[k][m][i] = 0.f;
   const int nb_vol = p.tx * p.ty * p.tz;
   const long long sv_n = (long long)p.SD * p.SH * p.SW;
+  // per-lane DMA offsets relative to the brick origin, for the bricks whose
+  // halo lies inside the volume and whose dY rows are all in range (interior
+  // bricks: two thirds at 128^3): their issue is one add per DMA instead of the
+  // coordinate arithmetic below, which the MFMA waves ran serially before every
+  // brick (~280 VALU + ~390 SALU ahead of the first MFMA).  MODE 1: x0, y0, z0
+  // are even, so (x0 + d) >> 1 = x0 / 2 + (d >> 1) (arithmetic shift: -1 -> -1).
+  constexpr int HJ = (HI + 3) / 4, DJ = DI / 4;
+  int hrel[HJ], drel[DJ];
+#pragma unroll
+  for (int j = 0; j < HJ; ++j) {
+    const int pc = (wv + 4 * j) * 64 + lane, hv = pc >> 1, q = pc & 1;
+    int hx = hv % WHX - 1, hy = (hv / WHX) % WHY - 1, hz = hv / (WHX * WHY) - 1;
+    if (MODE == 1) { hx >>= 1; hy >>= 1; hz >>= 1; }
+    hrel[j] = ((hz * p.SH + hy) * p.SW + hx) * 32 + q * 16;
+  }
+#pragma unroll
+  for (int j = 0; j < DJ; ++j) {
+    const int pc = (wv + 4 * j) * 64 + lane, v = pc / QPV, pos = pc % QPV;
+    const int qd = dy_quad<T, MC>(pos, v);
+    drel[j] = ((((v >> 6) * p.H + ((v >> 4) & 3)) * p.W + (v & 15)) * p.dy_cs + qd * EPQ) * ESZ;
+  }
 
-  auto issue = [&](long long bi, unsigned char* buf) {
-    const int b = (int)(bi / nb_vol);
-    int r = (int)(bi % nb_vol);
-    const int x0 = (r % p.tx) * WBX;
-    r /= p.tx;
-    const int y0 = (r % p.ty) * WBY;
-    const int z0 = (r / p.ty) * WBZ;
+  // brick coordinates of the next brick to issue, advanced in brick order (a
+  // 64-bit division per brick was ~130 SALU ahead of the MFMAs)
+  int nb_b = (int)(bb / nb_vol), nb_x, nb_y, nb_z;
+  {
+    const int r0 = (int)(bb % nb_vol);
+    nb_x = r0 % p.tx; nb_y = (r0 / p.tx) % p.ty; nb_z = r0 / (p.tx * p.ty);
+  }
+  auto issue = [&](unsigned lb) {
+    const int b = nb_b, x0 = nb_x * WBX, y0 = nb_y * WBY, z0 = nb_z * WBZ;
+    if (++nb_x == p.tx) {
+      nb_x = 0;
+      if (++nb_y == p.ty) {
+        nb_y = 0;
+        if (++nb_z == p.tz) { nb_z = 0; ++nb_b; }
+      }
+    }
     const __amdgpu_buffer_rsrc_t ra =
         __builtin_amdgcn_make_buffer_rsrc((void*)(p.act + (long long)b * p.act_bs), (short)0, (int)p.act_bs, 0x00020000);
     const __amdgpu_buffer_rsrc_t rd =
         __builtin_amdgcn_make_buffer_rsrc((void*)(p.dy + (long long)b * p.dy_bs), (short)0, (int)p.dy_bs, 0x00020000);
+    if (x0 >= 1 && y0 >= 1 && z0 >= 1 && x0 + WBX < p.W && y0 + WBY < p.H && z0 + WBZ < p.D &&
+        co0 + C::CO <= p.dy_cs) {
+      const int hbase = MODE == 1 ? (((z0 >> 1) * p.SH + (y0 >> 1)) * p.SW + (x0 >> 1)) * 32
+                                  : ((z0 * p.SH + y0) * p.SW + x0) * 32;
+      const int dbase = (((z0 * p.H + y0) * p.W + x0) * p.dy_cs + co0) * ESZ;
+#pragma unroll
+      for (int j = 0; j < HJ; ++j) {
+        const int k = wv + 4 * j;
+        if (k < HI && (k * 64 + lane) / 2 < WHV) {
+#pragma unroll
+          for (int c = 0; c < NCH; ++c)
+            wg_dma16(ra, lb + c * WIMG + k * 1024,
+                     (unsigned)(hbase + hrel[j]) + (unsigned)((long long)(ci0 / 16 + c) * sv_n * 32));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < DJ; ++j) wg_dma16(rd, lb + C::DY_OFF + (wv + 4 * j) * 1024, (unsigned)(dbase + drel[j]));
+      return;
+    }
     // halo: instruction k of a chunk image covers pieces 64 k .. +63 = voxel slots 32 k .. +31, both quads
 #pragma unroll
     for (int j = 0; j < (HI + 3) / 4; ++j) {
@@ -432,7 +491,7 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
           for (int c = 0; c < NCH; ++c) {
             const unsigned cofs = (unsigned)((long long)(ci0 / 16 + c) * sv_n * 32);  // chunk ci0 / 16 + c
             const unsigned voff = vb == 0xFFFFFFF0u ? vb : vb + cofs;
-            wg_dma16(ra, buf + c * WIMG + k * 1024, voff);
+            wg_dma16(ra, lb + c * WIMG + k * 1024, voff);
           }
         }
       }
@@ -448,16 +507,17 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
       const bool in = x < p.W && y < p.H && z < p.D && cc < p.dy_cs;
       const unsigned voff =
           in ? ((unsigned)((z * p.H + y) * p.W + x) * (unsigned)p.dy_cs + (unsigned)cc) * (unsigned)ESZ : 0xFFFFFFF0u;
-      wg_dma16(rd, buf + C::DY_OFF + k * 1024, voff);
+      wg_dma16(rd, lb + C::DY_OFF + k * 1024, voff);
     }
   };
 
-  if (bb < be) issue(bb, smem);
+  const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)smem;
+  if (bb < be) issue(lds0);
   for (long long bi = bb; bi < be; ++bi) {
     unsigned char* cur = smem + ((bi - bb) & 1) * BUF;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this brick's DMA (issued one brick ago) landed
     __syncthreads();                                  // ... for every wave; the other stage is free
-    if (bi + 1 < be) issue(bi + 1, smem + ((bi - bb + 1) & 1) * BUF);
+    if (bi + 1 < be) issue(lds0 + (unsigned)(((bi - bb + 1) & 1) * BUF));   // brick bi + 1
     wg_brick_mfma<T, MC, 27>(cur, cur + C::DY_OFF, acc, toff, ntap, wv, lane);
   }
   // the partial tile -> the brick range's slab in dw's OIDHW order: per 32-channel

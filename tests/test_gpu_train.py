@@ -84,7 +84,15 @@ def test_conv3d_wgrad_random_shapes_vs_torch(case, dtype_name):
     _run_wgrad_case(case, dtype_name)
 
 
-CM_CASES = [c for c in WG_CASES + RANDOM_WG_CASES if c[8] == 3]
+CM_CASES = [c for c in WG_CASES + RANDOM_WG_CASES if c[8] == 3] + [
+    # grids with interior bricks (halo inside the volume: the DMA kernel's
+    # precomputed-offset issue), two batches (brick counters cross a batch),
+    # the upsampling source, a ragged x edge and dY rows with spare channels
+    ("cm_interior", 2, (12, 12, 48), 64, 0, 64, 0, False, 3, 64),
+    ("cm_interior_up", 1, (16, 16, 48), 32, 0, 64, 1, False, 3, 64),
+    ("cm_interior_ragged", 1, (12, 16, 40), 32, 0, 32, 0, True, 3, 48),
+    ("cm_interior_cs_short", 2, (12, 12, 48), 32, 0, 40, 0, False, 3, 48),
+]
 
 
 @pytest.mark.parametrize("dtype_name", ["bf16", "fp16"])
