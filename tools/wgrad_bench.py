@@ -49,8 +49,11 @@ def run(n, cin, cout, gn, iters=5, cm=False, umode=0):
 
 if __name__ == "__main__":
     if "--dma" in sys.argv:   # the kept-activation (LDS-DMA) kernel on the R0 / R1 training shapes
-        for n, cin, cout, um in ((128, 64, 64, 0), (128, 192, 64, 0), (128, 128, 64, 0), (128, 128, 128, 1),
-                                 (64, 128, 128, 0), (64, 256, 128, 0), (64, 384, 128, 0)):
+        cases = ((128, 64, 64, 0), (128, 192, 64, 0), (128, 128, 64, 0), (128, 128, 128, 1),
+                 (64, 128, 128, 0), (64, 256, 128, 0), (64, 384, 128, 0))
+        if "--case" in sys.argv:   # one of them (index), e.g. for a PMC pass
+            cases = (cases[int(sys.argv[sys.argv.index("--case") + 1])],)
+        for n, cin, cout, um in cases:
             run(n, cin, cout, False, cm=True, umode=um)
         sys.exit(0)
     for n, cin, cout in ((128, 64, 64), (128, 128, 64), (64, 128, 128), (32, 256, 256)):
