@@ -83,7 +83,7 @@ __device__ __forceinline__ int dy_quad(int qd, int v) {
 }
 
 // halo offset (in rows) of tap t = (kz, ky, kx)
-__device__ __forceinline__ int tap_rows(int t) {
+__host__ __device__ constexpr int tap_rows(int t) {
   const int kz = t / 9, ky = (t / 3) % 3, kx = t % 3;
   return (kz * WHY + ky) * WHX + kx;
 }
@@ -100,24 +100,33 @@ __device__ __forceinline__ void wg_brick_mfma(const unsigned char* halo, const u
   const unsigned char* bimg = halo + (g & 1) * WIMG + 8 * pp;
   constexpr int NS = TAPS == 27 ? 16 : 4;   // K-steps of this wave
   const int s0 = TAPS == 27 ? 0 : 4 * wv;
+  // per-lane LDS addresses without the K-step part, which is wave-uniform (one
+  // address add per fragment and K-step; the hi halves are immediate offsets).
+  // dY row v = 16 s + 8 h + q (+ 4): the quad swizzle reads bit 1 of v, = bit 1 of q
+  const unsigned char* abase[MC];
+  const unsigned char* bbase[NT];
+#pragma unroll
+  for (int m = 0; m < MC; ++m) {
+    const int qd = 4 * m + 2 * (g & 1) + (pp >> 1);
+    abase[m] = dyl + (8 * h + q) * C::DYP + dy_quad<T, MC>(qd, q) * 16 + 8 * (pp & 1);
+  }
+#pragma unroll
+  for (int k = 0; k < NT; ++k) bbase[k] = bimg + (8 * h + q + toff[k]) * 32;
   // fragments of K-step s: dY (A) for every co sub-tile, U (B) for every tap
   auto load_frags = [&](int s, u32x4* a, u32x4* bfr) {
     const int y = s & 3, z = s >> 2;
+    const int aoff = 16 * s * C::DYP, boff = (z * WHY + y) * WHX * 32;
 #pragma unroll
     for (int m = 0; m < MC; ++m) {
-      const int v0 = 16 * s + 8 * h + q, v1 = v0 + 4;
-      const int qd = 4 * m + 2 * (g & 1) + (pp >> 1);
-      const v4s lo = tr_read(dyl + v0 * C::DYP + dy_quad<T, MC>(qd, v0) * 16 + 8 * (pp & 1));
-      const v4s hi = tr_read(dyl + v1 * C::DYP + dy_quad<T, MC>(qd, v1) * 16 + 8 * (pp & 1));
-      a[m] = join(lo, hi);
+      const unsigned char* ap = abase[m] + aoff;
+      a[m] = join(tr_read(ap), tr_read(ap + 4 * C::DYP));
     }
-    const int hrow = (z * WHY + y) * WHX + 8 * h + q;
     // every wave reads NT fragments (a wave with 6 taps reads a valid
     // dummy 7th, toff = tap 0, and skips its MFMAs): no divergent phi on
     // the operand registers
 #pragma unroll
     for (int k = 0; k < NT; ++k) {
-      const unsigned char* bp = bimg + (hrow + toff[k]) * 32;
+      const unsigned char* bp = bbase[k] + boff;
       bfr[k] = join(tr_read(bp), tr_read(bp + 4 * 32));
     }
   };
