@@ -770,3 +770,26 @@ extern "C" int cwdm_debug_conv_stamps(void* buf) {
   g_stamps.store(reinterpret_cast<unsigned long long*>(buf));
   return CWDM_OK;
 }
+
+// diagnostics / tests: the fused GroupNorm finalize + pre-pass (gn_fin_apply_kernel)
+// on its own, so it can be compared with cwdm_gn_finalize + cwdm_gn_apply in one
+// process (the plan picks it per conv; CWDM_GNFIN is read once)
+extern "C" int cwdm_debug_gn_fin_apply(const float* stats0, int64_t parts0, int c0, const float* stats1,
+                                       int64_t parts1, int c1, const float* gamma, const float* beta, int groups,
+                                       int64_t B, int64_t voxels, float eps, const void* x0, const void* x1,
+                                       int dtype, float* scale_shift, float* mean_rstd, void* out_cm,
+                                       cwdm_stream_t stream) {
+  CWDM_REQUIRE(stats0 && x0 && gamma && beta && scale_shift && mean_rstd && out_cm && (c1 == 0 || (stats1 && x1)),
+               CWDM_E_INVALID, "cwdm_debug_gn_fin_apply: null pointer");
+  CWDM_REQUIRE(B > 0 && voxels > 0 && parts0 > 0 && (c1 == 0 || parts1 > 0), CWDM_E_SHAPE,
+               "cwdm_debug_gn_fin_apply: empty shape");
+  GnFinFuse f{};
+  f.s0 = stats0; f.p0 = parts0; f.c0 = c0;
+  f.s1 = stats1; f.p1 = parts1; f.c1 = c1;
+  f.gamma = gamma; f.beta = beta; f.groups = groups; f.voxels = voxels; f.eps = eps;
+  f.ss = scale_shift; f.mr = mean_rstd; f.B = B;
+  CWDM_REQUIRE(gn_fin_fusable(f, dtype, c0, c1), CWDM_E_UNSUPPORTED,
+               "cwdm_debug_gn_fin_apply: not a fusable shape (16-bit, 16-channel chunks, <= 16 channels per "
+               "group dividing 16, <= 256 partials)");
+  return gn_fin_apply(f, x0, c0, x1, c1, B, voxels, dtype, out_cm, (hipStream_t)stream);
+}

@@ -759,8 +759,16 @@ bool v5_eligible(const cwdm_conv3d_desc* d, bool gn) {
     if (d->out_dtype != CWDM_F32 || d->accumulate || d->out1) return false;
     if (d->a_mode != 0 && d->a_mode != 1) return false;
     if (d->res_mode < -1 || d->res_mode > 1) return false;
+    // the 1x1 skip product is added through the residual slot (conv3d_v4_forward): not both
+    if (d->b_w && d->res_mode >= 0) return false;
     if (d->W < kWideMinW || d->H % 4 || d->D % 4 || d->cout % 64) return false;
-    if (d->D * d->H * d->W * d->cout * 4 >= 0xFFFFE000LL) return false;
+    // 32-bit buffer offsets per batch: the output, and the sources (raw, or the
+    // activated (c0 + c1)-channel copy of the training forward's pre-pass)
+    const int64_t lim = 0xFFFFE000LL;
+    if (d->D * d->H * d->W * d->cout * 4 >= lim) return false;
+    const int64_t sv = d->a_mode == 1 ? d->D * d->H * d->W / 8 : d->D * d->H * d->W;
+    if (d->a_gn ? sv * (d->a_c0 + d->a_c1) * 4 >= lim : (sv * d->a_c0 * 4 >= lim || sv * d->a_c1 * 4 >= lim))
+      return false;
     return !(gn && d->a_mode == 1);
   }
   if (mode <= 0 || (mode == 1 && !gn) || path == 1 || path == 3) return false;

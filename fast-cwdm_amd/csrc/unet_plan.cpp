@@ -1449,6 +1449,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
     d.u0 = u0; d.u_c0 = uc0; d.u1 = u1; d.u_c1 = uc1; d.u_mode = umode; d.u_gn = ugn;
     d.dy = dy; d.dy_cs = dy_cs; d.cout = cout; d.dw = dw;
     d.workspace = gb + G.wgws;
+    d.ws_bytes = G.wgws_bytes;
     return cwdm_conv3d_wgrad(&d, stream);
   };
   // conv ci's wgrad from the activated input its forward kept (training
@@ -1462,6 +1463,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
     d.u0 = wb + L.keep_off[ci]; d.u_c0 = uc0 + uc1; d.u_mode = umode; d.u_cm = 1;
     d.dy = dy; d.dy_cs = dy_cs; d.cout = cout; d.dw = dw;
     d.workspace = gb + G.wgws;
+    d.ws_bytes = G.wgws_bytes;
     return cwdm_conv3d_wgrad(&d, stream);
   };
   auto dgrad = [&](int ci, const void* dy) -> int {

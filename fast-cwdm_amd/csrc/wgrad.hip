@@ -846,6 +846,8 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
     CWDM_REQUIRE(d->D % 2 == 0 && d->H % 2 == 0 && d->W % 2 == 0, CWDM_E_SHAPE,
                  "cwdm_conv3d_wgrad: upsampled grid must be even");
   CWDM_REQUIRE(d->workspace, CWDM_E_WORKSPACE, "cwdm_conv3d_wgrad: workspace (cwdm_conv3d_wgrad_workspace_bytes) missing");
+  CWDM_REQUIRE(d->ws_bytes >= cwdm_conv3d_wgrad_workspace_bytes(d->cout, cin, d->ksize), CWDM_E_WORKSPACE,
+               "cwdm_conv3d_wgrad: ws_bytes below cwdm_conv3d_wgrad_workspace_bytes(cout, cin, ksize)");
   WgradParams p{};
   ConvParams& c = p.cp;
   c.B = (int)d->B; c.D = (int)d->D; c.H = (int)d->H; c.W = (int)d->W;

@@ -81,6 +81,7 @@ class WgradDesc(ctypes.Structure):
         ("dw", vp),
         ("workspace", vp),
         ("u_cm", ctypes.c_int),
+        ("ws_bytes", i64),
     ]
 
 
@@ -150,6 +151,8 @@ _PROTOS = {
     "cwdm_gn_apply": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, vp, i64, i64, ctypes.c_int, vp, vp]),
     "cwdm_conv3d_set_path": (ctypes.c_int, [ctypes.c_int]),
     "cwdm_debug_v5_grid": (ctypes.c_int, [ctypes.c_int]),
+    "cwdm_debug_gn_fin_apply": (ctypes.c_int, [vp, i64, ctypes.c_int, vp, i64, ctypes.c_int, vp, vp, ctypes.c_int,
+                                               i64, i64, ctypes.c_float, vp, vp, ctypes.c_int, vp, vp, vp, vp]),
     "cwdm_debug_head2": (ctypes.c_int, [ctypes.c_int]),
     "cwdm_debug_conv_stamps": (ctypes.c_int, [vp]),
     "cwdm_conv3d_wgrad": (ctypes.c_int, [ctypes.POINTER(WgradDesc), vp]),

@@ -16,7 +16,7 @@ from .ops import _need_cuda, _stream
 
 
 class FlatAdamW(torch.optim.Optimizer):
-    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, direct_grads=False):
         params = list(model.parameters())
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         flat = model.flat_params
@@ -29,9 +29,13 @@ class FlatAdamW(torch.optim.Optimizer):
         if o != flat.numel():
             raise ValueError("FlatAdamW: flat buffer / parameter size mismatch")
         self._model = model
-        # the model's backward then hands its flat gradient buffer over as the
-        # parameters' .grad views (no per-parameter copies; flat_grad() is that buffer)
-        model.direct_grads = True
+        # direct_grads=True: the model's backward hands its flat gradient buffer
+        # over as the parameters' .grad views (no per-parameter copies; flat_grad()
+        # is that buffer).  Opt-in, since it changes what torch.autograd.grad and
+        # backward(inputs=...) see on that model; TrainLoop sets model.direct_grads
+        # itself.  Either way step() reads model.flat_grad().
+        if direct_grads:
+            model.direct_grads = True
         self._flat = flat
         self._m = torch.zeros_like(flat)
         self._v = torch.zeros_like(flat)

@@ -363,6 +363,18 @@ int cwdm_conv3d_set_path(int path);
  * CU.  Returns the previous cap. */
 int cwdm_debug_v5_grid(int n);
 
+/* Diagnostics / tests only: the fused GroupNorm finalize + pre-pass the plan
+ * offers a small-level consumer conv (GnFinFuse): the finalize of
+ * cwdm_gn_finalize (same arguments, scale_shift and mean_rstd both written)
+ * fused with cwdm_gn_apply into the conv's chunk-major activated input
+ * out_cm [B][(c0+c1)/16][voxels][16].  16-bit dtype, c0 and c1 multiples of 16,
+ * C/groups <= 16 dividing 16, <= 256 partials per source (CWDM_E_UNSUPPORTED
+ * otherwise). */
+int cwdm_debug_gn_fin_apply(const float* stats0, int64_t parts0, int c0, const float* stats1, int64_t parts1,
+                            int c1, const float* gamma, const float* beta, int groups, int64_t B, int64_t voxels,
+                            float eps, const void* x0, const void* x1, int dtype, float* scale_shift,
+                            float* mean_rstd, void* out_cm, cwdm_stream_t stream);
+
 /* Diagnostics / tests only: which output-head kernel runs -- 0 = the
  * second-generation head wherever its shape holds (64 input channels,
  * W % 16, H % 4, D % 4; default), -1 = the first head only, n > 0 = the
@@ -396,7 +408,7 @@ int cwdm_gn_apply(const void* x0, int c0, const void* x1, int c1, const float* s
  * and is accumulated into (dw += dW).  workspace: fp32 scratch of
  * cwdm_conv3d_wgrad_workspace_bytes: every (K range, channel tile) unit stores
  * its partial tile into its range's slab, and one pass adds the slabs into dw
- * in range order -- no atomics, two calls on the same inputs are bitwise
+ * in range order (ws_bytes is checked against the size) -- no atomics, two calls on the same inputs are bitwise
  * identical.  Nothing in it needs zeroing or survives the call.
  * ksize 1: the 1x1 skip conv. */
 typedef struct {
@@ -414,6 +426,8 @@ typedef struct {
                                activated, chunk-major [B][cin/16][SV][16] (SV = the source grid, half of
                                D, H, W for u_mode 1), 16-bit dtype, ksize 3, u_gn NULL, no u1: staged by
                                LDS-DMA with no recompute */
+  int64_t ws_bytes;         /* size of workspace: >= cwdm_conv3d_wgrad_workspace_bytes(cout, cin, ksize)
+                               (CWDM_E_WORKSPACE otherwise; the slabs are up to S_max x cout x cin x k^3) */
 } cwdm_wgrad_desc;
 int64_t cwdm_conv3d_wgrad_workspace_bytes(int cout, int cin, int ksize);
 int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* desc, cwdm_stream_t stream);

@@ -277,3 +277,99 @@ def test_fullsize_wavunet_forward_fp32_vs_oracle():
     with torch.no_grad():
         ref = ow.wunet_forward(P, x, t, num_groups=32, **cfg)
     assert rel_err(out, ref) < 1e-3
+
+
+# --------------------------------------------------------------------------- config 3 at its size
+def _train_case():
+    vols = data.brats_batch(2 * N, seed=41, batch=1)                      # 4 x (1, 1, 256^3)
+    noise = torch.randn(1, 1, 2 * N, 2 * N, 2 * N, generator=torch.Generator().manual_seed(42))
+    return vols, torch.tensor([640]), noise
+
+
+def test_fullsize_training_step_fp32_vs_oracle():
+    """Config 3's step at its own size (reference train_util.py:396-470,
+    gaussian_diffusion.py:1131-1166): 4 x 256^3 volumes -> training_losses
+    (4 DWTs + noise DWT + q_sample into the 32-channel 128^3 input, native
+    forward of the 81.5 M U-Net, MSE) -> native backward, fp32, against the
+    CPU oracle's loss and autograd: the model output within 1e-3, the loss
+    within 1e-4 and EVERY parameter gradient within 1e-3 rel-L2 (this is the
+    128^3-only backward: the unfused GroupNorm backward at W > 64, v5 dgrad at
+    W = 128, the S-adaptive weight-gradient slab reduce); then the fused AdamW
+    step == torch.optim.AdamW on that gradient."""
+    from cwdm_hip.optim import FlatAdamW
+    P = ou.random_params(seed=7)
+    model, diffusion = _production("fp32", P)
+    vols, t, noise = _train_case()
+    terms, out, _ = diffusion.training_losses(model, {k: v.to(DEV) for k, v in vols.items()}, t.to(DEV),
+                                              mode="i2i", contr="t1n", noise=noise.to(DEV))
+    loss = terms["mse_wav"].mean()
+    loss.backward()
+    grads = {n: p.grad.detach().cpu() for n, p in model.named_parameters()}
+    out, loss_v = out.detach().cpu(), float(loss)
+    p0, gflat = model.flat_params.detach().cpu(), model.flat_grad().detach().cpu()
+    opt = FlatAdamW(model, lr=1e-4, weight_decay=0.01)
+    opt.step()
+    p1 = model.flat_params.detach().cpu()
+    del model, opt, terms, loss
+    torch.cuda.empty_cache()
+    ref = p0.clone().requires_grad_(True)
+    topt = torch.optim.AdamW([ref], lr=1e-4, weight_decay=0.01, foreach=False)
+    ref.grad = gflat
+    topt.step()
+    assert rel_err(p1, ref.detach()) < 1e-6
+    torch.set_num_threads(16)
+    tab = od.Tables(od.beta_schedule("linear", 1000, "direct"))
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    rterms, rout, _ = od.training_losses(tab, lambda x, tt, **kw: ou.unet_forward(Pr, x, tt), vols, t, noise,
+                                         contr="t1n")
+    rloss = rterms["mse_wav"].mean()
+    rloss.backward()
+    assert rel_err(out, rout.detach()) < 1e-3
+    assert abs(loss_v - float(rloss)) / float(rloss) < 1e-4, (loss_v, float(rloss))
+    assert set(grads) == set(Pr) and len(grads) == len(P)
+    worst = {k: float((grads[k].double() - Pr[k].grad.double()).norm() / Pr[k].grad.double().norm().clamp_min(1e-30))
+             for k in Pr}
+    top = sorted(worst.items(), key=lambda kv: -kv[1])[:5]
+    print("config-3 fp32 128^3 step, worst gradients vs oracle autograd:", top)
+    assert top[0][1] < 1e-3, top
+
+
+@pytest.mark.parametrize("dtype", ["bf16"])
+def test_fullsize_training_two_steps_bitwise_reproducible(dtype):
+    """The config-3 benchmark step itself (bf16, 128^3, kept activations,
+    TrainLoop's direct .grad hand-over, fused AdamW): two runs of two steps
+    from the same weights and batches give bitwise-identical gradients and
+    parameters -- the 128^3 shapes of the fixed-order reductions (slab reduce at
+    large S, GroupNorm-backward partials, channel sums)."""
+    from cwdm_hip.optim import FlatAdamW
+    P = ou.random_params(seed=7)
+    vols, t, noise = _train_case()
+    vols = {k: v.to(DEV) for k, v in vols.items()}
+    noise2 = torch.randn(noise.shape, generator=torch.Generator().manual_seed(43)).to(DEV)
+    t2 = torch.tensor([77], device=DEV)
+
+    def run():
+        model, diffusion = _production(dtype, P)
+        opt = FlatAdamW(model, lr=1e-4, weight_decay=0.01, direct_grads=True)
+        grads, losses = [], []
+        for tt, nz in ((t.to(DEV), noise.to(DEV)), (t2, noise2)):
+            opt.zero_grad()
+            terms, _, _ = diffusion.training_losses(model, vols, tt, mode="i2i", contr="t1n", noise=nz)
+            loss = terms["mse_wav"].mean()
+            loss.backward()
+            losses.append(loss.detach().clone())
+            grads.append(model.flat_grad().detach().clone())
+            opt.step()
+        torch.cuda.synchronize()
+        p = model.flat_params.detach().clone()
+        del model, opt
+        return grads, losses, p
+
+    g_a, l_a, p_a = run()
+    g_b, l_b, p_b = run()
+    for i in range(2):
+        assert torch.isfinite(g_a[i]).all() and torch.isfinite(l_a[i])
+        assert torch.equal(l_a[i], l_b[i]), ("loss", i)
+        assert torch.equal(g_a[i], g_b[i]), ("step", i, float((g_a[i] - g_b[i]).abs().max()))
+    assert not torch.equal(g_a[0], g_a[1])
+    assert torch.equal(p_a, p_b)

@@ -417,6 +417,9 @@ SPLIT_CASES = [
     ("x_partial_x_nogn", 2, (4, 8, 56), 48, 16, 64, 0, False, False, 0),
     ("x_skip", 1, (4, 4, 64), 128, 64, 64, 0, True, True, -1),
     ("x_w24_up_nogn", 2, (4, 8, 24), 32, 0, 64, 1, False, False, 1),
+    # a residual AND a 1x1 skip: the split path refuses it (the skip pre-pass would
+    # take the residual slot); the exact-fp32 kernels add both
+    ("x_skip_res", 1, (4, 4, 64), 64, 0, 64, 0, True, True, 0),
 ]
 
 
@@ -637,6 +640,51 @@ def test_gn_finalize_matches_group_norm():
     y = x * o[..., 0][:, :, None, None, None] + o[..., 1][:, :, None, None, None]
     ref = F.group_norm(x, G, gamma.cpu(), beta.cpu(), eps=1e-5)
     assert rel_err(y, ref) < 1e-5
+
+
+@pytest.mark.parametrize("dtype_name", ["bf16", "fp16"])
+@pytest.mark.parametrize("concat", [False, True], ids=["single", "concat"])
+@pytest.mark.parametrize("cpg", [1, 2, 4, 8, 16])
+def test_gn_fin_apply_matches_finalize_plus_apply(cpg, concat, dtype_name):
+    """The fused finalize + pre-pass of the small levels (gn_fin_apply_kernel,
+    GnFinFuse) == cwdm_gn_finalize + cwdm_gn_apply: the (scale, shift) and
+    (mean, rstd) it writes for the backward within 1e-6, and its chunk-major
+    activated output within one 16-bit ulp of the unfused pair's."""
+    from cwdm_hip import _lib
+    from cwdm_hip._lib import check, lib
+    dt, tdt = _DTN[dtype_name]
+    g = torch.Generator().manual_seed(40 + cpg)
+    B, C, parts, V = 2, 64, 8, 512
+    c0, c1 = (32, 32) if concat else (64, 0)
+    G = C // cpg
+    x = (torch.randn(B, V, C, generator=g) * 1.5 + 0.3).to(tdt).float()
+    xv = x.view(B, parts, V // parts, C)
+    st = torch.stack([xv.sum(2), (xv ** 2).sum(2)], -1).contiguous()     # [B][P][C][2]
+    s0, s1 = st[:, :, :c0].contiguous().to(DEV), st[:, :, c0:].contiguous().to(DEV)
+    gamma = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    x0 = x[..., :c0].contiguous().to(DEV, tdt)
+    x1 = x[..., c0:].contiguous().to(DEV, tdt) if c1 else None
+    L = lib()
+    ss_a, mr_a = torch.empty(B, C, 2, device=DEV), torch.empty(B, G, 2, device=DEV)
+    act_a = torch.empty(B, V, C, device=DEV, dtype=tdt)
+    check(L.cwdm_gn_finalize(s0.data_ptr(), parts, c0, s1.data_ptr() if c1 else None, parts, c1, gamma.data_ptr(),
+                             beta.data_ptr(), G, B, V, 1e-5, ss_a.data_ptr(), mr_a.data_ptr(), None))
+    check(L.cwdm_gn_apply(x0.data_ptr(), c0, x1.data_ptr() if c1 else None, c1, ss_a.data_ptr(), B, V, dt,
+                          act_a.data_ptr(), None))
+    ss_b, mr_b = torch.empty_like(ss_a), torch.empty_like(mr_a)
+    act_b = torch.empty(B, C // 16, V, 16, device=DEV, dtype=tdt)
+    check(L.cwdm_debug_gn_fin_apply(s0.data_ptr(), parts, c0, s1.data_ptr() if c1 else None, parts, c1,
+                                    gamma.data_ptr(), beta.data_ptr(), G, B, V, 1e-5, x0.data_ptr(),
+                                    x1.data_ptr() if c1 else None, dt, ss_b.data_ptr(), mr_b.data_ptr(),
+                                    act_b.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert rel_err(ss_b, ss_a) < 1e-6
+    assert rel_err(mr_b, mr_a) < 1e-6
+    a = act_a.float().view(B, V, C // 16, 16).permute(0, 2, 1, 3).cpu()
+    b = act_b.float().cpu()
+    ulp = {"bf16": 2.0 ** -7, "fp16": 2.0 ** -10}[dtype_name]
+    assert torch.all((a - b).abs() <= ulp * a.abs() + 1e-6), float((a - b).abs().max())
 
 
 def test_copy3_layouts():

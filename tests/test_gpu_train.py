@@ -152,7 +152,7 @@ def _run_wgrad_case(case, dtype_name, cm=False):
         act = _nd(h_src).reshape(B, sv, cin // 16, 16).permute(0, 2, 1, 3).contiguous().to(DEV, tdt)
         d.u0, d.u_c0, d.u1, d.u_c1, d.u_gn, d.u_cm = act.data_ptr(), cin, None, 0, None, 1
     wsw = torch.empty(lib().cwdm_conv3d_wgrad_workspace_bytes(cout, cin, k), dtype=torch.uint8, device=DEV)
-    d.workspace = wsw.data_ptr()
+    d.workspace, d.ws_bytes = wsw.data_ptr(), wsw.numel()
     check(lib().cwdm_conv3d_wgrad(ctypes.byref(d), None))
     tol = 1e-4 if (dtype_name == "fp32" or cm) else 1e-2
     assert rel_err(dw - dw0, ref) < tol, name
@@ -734,7 +734,7 @@ def test_production_training_two_steps_bitwise_reproducible(dtype):
     def run():
         model = _product_model(PROD_CFG, 32, P, dtype)
         model.keep_activations = True
-        opt = FlatAdamW(model, lr=1e-3, weight_decay=0.01)
+        opt = FlatAdamW(model, lr=1e-3, weight_decay=0.01, direct_grads=True)
         grads = []
         for xi in (x, x2):
             opt.zero_grad()

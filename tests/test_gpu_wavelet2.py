@@ -142,7 +142,11 @@ def test_config5_graph_loop_runs_at_224(dtype):
     model = script_util.create_model(image_size=224, num_channels=64, num_res_blocks=2, channel_mult="1,2,2",
                                      attention_resolutions="", dims=3, num_groups=32, in_channels=256,
                                      out_channels=64, bottleneck_attention=False, resample_2d=False,
-                                     resblock_updown=True, compute_dtype=dtype).to(DEV)
+                                     resblock_updown=True, compute_dtype=dtype)
+    # seeded non-degenerate weights: the reference initialisation zeroes out_layers.3
+    # and out.2, which would make the U-Net output exactly 0
+    model.load_state_dict(ou.random_params(seed=5, **C5_FULL_CFG))
+    model.to(DEV)
     diffusion = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
                                                       timestep_respacing="3", wavelet_levels=2)
     g = torch.Generator(device=DEV).manual_seed(1)
@@ -154,7 +158,75 @@ def test_config5_graph_loop_runs_at_224(dtype):
         torch.manual_seed(0)
         outs.append(diffusion.p_sample_loop(model, x_T.shape, noise=x_T, cond=cond, progress=False))
     assert torch.isfinite(outs[0]).all()
+    assert float(outs[0].abs().max()) > 0
     assert torch.equal(outs[0], outs[1])
+
+
+C5_FULL_CFG = dict(in_channels=256, model_channels=64, out_channels=64, num_res_blocks=2, channel_mult=(1, 2, 2))
+C5_SHIFT = [-1.5, 0.2, 0.3, 0.5, 0.2, 0.4, 0.6, 1.0] + [0.8, 1.0, 1.2, 1.0, 1.2, 1.4, 1.8]
+_C5_REF = {}
+
+
+def _c5_full_case():
+    """224^3 phantoms -> 2-level analysis (cond: 3 x 64 channels on the 56^3 grid),
+    x_t and the step noise, seeded; the oracle step (cached: four dtypes use it)."""
+    if not _C5_REF:
+        from oracle import data
+        g = torch.Generator().manual_seed(31)
+        cond = torch.cat([w2.analysis2(data.phantom(224, seed=60 + k)) for k in range(3)], dim=1)
+        x_t = torch.randn(1, 64, 56, 56, 56, generator=g)
+        noise = torch.randn(1, 64, 56, 56, 56, generator=g)
+        P = ou.random_params(seed=5, **C5_FULL_CFG)
+        tab = od.Tables(od.beta_schedule("linear", 1000, "direct"), band_shift=w2.channel_shift(C5_SHIFT))
+        torch.set_num_threads(16)
+        with torch.no_grad():
+            ref = od.p_sample(tab, ou.OracleUNet(P, num_groups=32, **C5_FULL_CFG), x_t, torch.tensor([_C5_T]), cond,
+                              noise, process=w2.process_xstart2)
+        _C5_REF.update(P=P, cond=cond, x_t=x_t, noise=noise, ref=ref)
+    return _C5_REF
+
+
+_C5_T = 480
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp32x", "fp16", "bf16"])
+def test_config5_step_at_224_vs_oracle(dtype):
+    """Config 5 at its own size with non-degenerate weights: one denoising step
+    of the native loop (3-level U-Net 256 -> 64 channels, mc 64, mult 1,2,2,
+    2 res blocks, on the 56^3 level-2 grid of 224^3 images; the 2-level fused
+    sampler with FATS per-subband rows) against the CPU oracle's p_sample with
+    process_xstart2.  fp32 and the accurate fast mode fp32x within 1e-3 (fp32x
+    runs the split-bf16 warp-specialised conv at 56^3); fp16 (the config's dtype)
+    and bf16 run the 16-bit 56^3 v5 / 28^3 v4 / 14^3 small-grid convs, bounded
+    at their measured rounding error."""
+    from guided_diffusion import script_util
+    c = _c5_full_case()
+    model = script_util.create_model(image_size=224, num_channels=64, num_res_blocks=2, channel_mult="1,2,2",
+                                     attention_resolutions="", dims=3, num_groups=32, in_channels=256,
+                                     out_channels=64, bottleneck_attention=False, resample_2d=False,
+                                     resblock_updown=True, compute_dtype=dtype)
+    model.load_state_dict(c["P"])
+    model.to(DEV)
+    diffusion = script_util.create_gaussian_diffusion(steps=1000, predict_xstart=True, mode="i2i",
+                                                      band_log_snr_shift=C5_SHIFT, wavelet_levels=2)
+    it = iter([c["noise"].to(DEV)])
+    loop = diffusion._native_loop(model, c["x_t"].to(DEV), [_C5_T], c["cond"].to(DEV).contiguous(), True,
+                                  noise_fn=lambda x: next(it), graph=False)
+    out = next(loop)
+    sample, pred = out["sample"].cpu(), out["pred_xstart"].cpu()
+    ref = c["ref"]
+    l2 = lambda a, b: float((a.double() - b.double()).norm() / b.double().norm())  # noqa: E731
+    e = {"pred_max": rel_err(pred, ref["pred_xstart"]), "sample_max": rel_err(sample, ref["sample"]),
+         "pred_l2": l2(pred, ref["pred_xstart"]), "sample_l2": l2(sample, ref["sample"])}
+    print(f"config 5 at 224^3, {dtype} step vs oracle:", {k: f"{v:.3e}" for k, v in e.items()})
+    assert torch.isfinite(sample).all() and float(ref["pred_xstart"].abs().max()) > 0
+    if dtype in ("fp32", "fp32x"):
+        assert e["pred_max"] < 1e-3 and e["sample_max"] < 1e-3, e
+    else:
+        # 16-bit activations: bounded like the config-2 full-size half step
+        # (test_gpu_fullsize.test_fullsize_half_step_close_to_fp32)
+        bound = {"fp16": 1e-2, "bf16": 6e-2}[dtype]
+        assert e["pred_l2"] < bound and e["sample_l2"] < bound, e
 
 
 @pytest.mark.parametrize("per_band", [False, True])

@@ -31,6 +31,7 @@ def run(n, cin, cout, gn, iters=5, cm=False, umode=0):
     d.u_gn = g.data_ptr() if (gn and not cm) else None
     d.u_cm = 1 if cm else 0
     d.dy, d.dy_cs, d.cout, d.dw, d.workspace = dy.data_ptr(), cout, cout, dw.data_ptr(), ws.data_ptr()
+    d.ws_bytes = ws.numel()
     for _ in range(2):
         check(lib().cwdm_conv3d_wgrad(ctypes.byref(d), None))
     torch.cuda.synchronize()
