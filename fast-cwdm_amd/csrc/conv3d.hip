@@ -189,30 +189,36 @@ __global__ void __launch_bounds__(256) pack_tile_kernel(const PackJob* __restric
 }
 
 // Split-bf16 packing of an fp32 conv for the accurate fast mode (conv3d_v5.hip,
-// cwdm_conv3d_desc.a_w_split): the bf16 layout of a virtual conv with 4 cin
-// inputs -- per fp32 K chunk c (8 channels) two bf16 chunks: pass 0 = [hi(w) | hi(w)],
-// pass 1 = [lo(w) | lo(w)] over the (hi(x) | lo(x)) halo planes, hi = bf16(w),
-// lo = bf16(w - hi): hi.hi + hi.lo + lo.hi + lo.lo of every product, fp32-accumulated
+// cwdm_conv3d_desc.a_w_split): the bf16 layout of a virtual conv with 3 cin
+// inputs -- per pair of fp32 K chunks (a: channels 16 p .. + 7, b: + 8 .. + 15)
+// three bf16 chunks: A = [hi(w_a) | hi(w_a)] and B = [hi(w_b) | hi(w_b)] over a
+// chunk's (hi(x) | lo(x)) halo planes, C = [lo(w_a) | lo(w_b)] over (hi(x_a) |
+// hi(x_b)); hi = bf16(w), lo = bf16(w - hi): hi.hi + lo.hi + hi.lo of every
+// product, fp32-accumulated.  Quad slots swizzled by bit 3 of the output row as
+// in pack_impl (only C's two quads differ).
 __global__ void __launch_bounds__(256) pack_split_kernel(const float* __restrict__ w, int cout, int cin, int NT,
                                                          bf16_t* __restrict__ out, long long total) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int nch = cin / 4;  // virtual 16-channel chunks
+  const int nvc = 3 * (cin / 16);  // virtual 16-channel chunks
   const int e = (int)(i % 8);
   long long r = i / 8;
-  r /= 2;  // quad (either plane carries the same 8 channels)
+  const int qp = (int)(r % 2);
+  r /= 2;
   const int n = (int)(r % NT);
   r /= NT;
   const int tap = (int)(r % 27);
   r /= 27;
-  const int chunk = (int)(r % nch);
-  const int ct = (int)(r / nch);
-  const int co = ct * NT + n, ci = (chunk >> 1) * 8 + e;
+  const int vc = (int)(r % nvc);
+  const int ct = (int)(r / nvc);
+  const int pair = vc / 3, kind = vc % 3;
+  const int q = qp ^ ((n >> 3) & 1);   // the logical K half this slot carries
+  const int co = ct * NT + n, ci = pair * 16 + (kind == 2 ? 8 * q : 8 * kind) + e;
   float v = 0.f;
   if (co < cout) {
     const float x = w[((long long)co * cin + ci) * 27 + tap];
     const float hi = bf2f(f2bf(x));
-    v = (chunk & 1) ? x - hi : hi;
+    v = kind == 2 ? x - hi : hi;
   }
   out[i] = f2bf(v);
 }
@@ -266,16 +272,16 @@ extern "C" int cwdm_conv3d_pack(const float* w, int cout, int cin, int ksize, in
 }
 
 extern "C" int64_t cwdm_conv3d_packed_split_bytes(int cout, int cin) {
-  if (cout <= 0 || cout % 64 || cin <= 0 || cin % 8) return -1;
-  return cwdm_conv3d_packed_bytes(cout, 4 * cin, 3, CWDM_BF16);
+  if (cout <= 0 || cout % 64 || cin <= 0 || cin % 16) return -1;
+  return cwdm_conv3d_packed_bytes(cout, 3 * cin, 3, CWDM_BF16);
 }
 
 extern "C" int cwdm_conv3d_pack_split(const float* w, int cout, int cin, void* packed, cwdm_stream_t stream) {
   CWDM_REQUIRE(w && packed, CWDM_E_INVALID, "cwdm_conv3d_pack_split: null pointer");
-  CWDM_REQUIRE(cout > 0 && cout % 64 == 0 && cin > 0 && cin % 8 == 0, CWDM_E_UNSUPPORTED,
-               "cwdm_conv3d_pack_split: cout % 64 == 0, cin % 8 == 0");
+  CWDM_REQUIRE(cout > 0 && cout % 64 == 0 && cin > 0 && cin % 16 == 0, CWDM_E_UNSUPPORTED,
+               "cwdm_conv3d_pack_split: cout % 64 == 0, cin % 16 == 0");
   const int NT = 64;
-  const long long total = (long long)(cout / NT) * (cin / 4) * 27 * NT * 16;
+  const long long total = (long long)(cout / NT) * (3 * cin / 16) * 27 * NT * 16;
   hipLaunchKernelGGL(pack_split_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, w,
                      cout, cin, NT, reinterpret_cast<bf16_t*>(packed), total);
   CWDM_LAUNCHED();

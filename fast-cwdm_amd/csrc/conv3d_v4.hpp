@@ -482,7 +482,9 @@ __device__ __forceinline__ V4Tile v4_tile_of(const V4Params& p, int it) {
 // voxel slots of the two quad planes, so 5 voxel indices serve all 10; -2 marks
 // the padding slots (never written: bias / statistics scratch).  Recomputed per
 // chunk (a few VALU per piece) rather than held in registers.
-template <typename T, int MODE>
+// PB: byte stride of the two quad planes (v4 / v5: the padded 1280 slots; the
+// split-bf16 kernel packs them at 1224 slots -- the padding lanes never write)
+template <typename T, int MODE, int PB = V4Cfg::HVP * 16>
 __device__ __forceinline__ void v4_issue_halo(const V4Params& p, const V4Tile& tt, int c, unsigned char* hb, int wv,
                                               int lane) {
   using C = V4Cfg;
@@ -522,8 +524,9 @@ __device__ __forceinline__ void v4_issue_halo(const V4Params& p, const V4Tile& t
     const int sv = svox[j % 5];
     const unsigned voff = sv >= 0 ? (unsigned)sv * rowb + cofs + (unsigned)((j / 5) * 16) : 0xFFFFFFF0u;
     if (sv != -2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(hb + pc * 1024), 16,
-                                               voff, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(hb + (PB == 20 * 1024 ? pc * 1024 : (pc / 20) * PB + (pc % 20) * 1024)),
+          16, voff, 0, 0, 0);
   }
 }
 

@@ -435,26 +435,43 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
 
 
 // ---------------------------------------------------------------------------
-// The accurate fast mode: fp32 activations, conv MFMAs on bf16 hi/lo splits.
-// Same pipeline as conv3d_v5_kernel with three changes:
-//   * helpers convert every DMA'd fp32 chunk (8 channels, 32 B per voxel; the
-//     GroupNorm+SiLU applied first when agn is set) in place into two bf16
-//     planes: quad plane 0 = hi(x) of the 8 channels, plane 1 = lo(x) =
-//     bf16(x - hi(x)) -- the same 32 bytes per voxel slot;
-//   * the MFMA waves run two bf16 weight passes over each chunk
-//     (cwdm_conv3d_pack_split: [hi(w) | hi(w)] then [lo(w) | lo(w)]), i.e.
-//     hi.hi + hi.lo + lo.hi + lo.lo of every product, fp32-accumulated: a
-//     relative error ~2^-16 per product instead of 2^-8 (bf16) at 2x the bf16
-//     MFMA work per 8 fp32 channels (the exact-fp32 MFMA runs at 1/16 rate);
+// The accurate fast mode: fp32 activations, conv MFMAs on bf16 hi/lo splits,
+// three bf16 products per fp32 product: hi(x) hi(w) + lo(x) hi(w) + hi(x) lo(w)
+// (lo(x) lo(w) is below fp32 rounding: dropped).  Same warp-specialised
+// pipeline as conv3d_v5_kernel, but per PAIR of fp32 chunks (16 channels):
+//   * helpers DMA both chunks (8 fp32 channels = 32 B per voxel slot each) and
+//     convert each in place (the GroupNorm+SiLU applied first when agn is set)
+//     into two bf16 planes: plane 0 = hi(x), plane 1 = lo(x) = bf16(x - hi(x));
+//     the planes are packed at 1224 slots (no padding), so four chunk buffers --
+//     two pairs, double-buffered -- fit the CU's LDS;
+//   * the MFMA waves run three bf16 passes per pair (cwdm_conv3d_pack_split):
+//     A = [hi(x_a) | lo(x_a)] . [hi(w_a) | hi(w_a)], B = the same for chunk b,
+//     C = [hi(x_a) | hi(x_b)] . [lo(w_a) | lo(w_b)] -- pass C's second K half is
+//     read from the other chunk's buffer (only the lane base differs), so
+//     3 MFMA passes per 16 fp32 channels instead of 4 (2^-16 relative per
+//     product instead of bf16's 2^-8; the exact-fp32 MFMA runs at 1/16 rate);
 //   * fp32 outputs leave from the accumulators (no 16-bit staging), with the
 //     (sum, sum^2) partials reduced across the two plane waves of a channel
 //     half through LDS (the second to arrive writes them: deterministic).
+// Channels: c0 and c1 multiples of 16 (a pair never straddles the sources).
 // ---------------------------------------------------------------------------
+struct V5sCfg {
+  static constexpr int PLANE = V4Cfg::HV * 16;   // 19584: one quad plane of a chunk (1224 slots)
+  static constexpr int BUF = 2 * PLANE;          // one fp32 chunk as its (hi, lo) planes
+  static constexpr int PAIR = 2 * BUF;           // two chunks: one pipeline stage
+  static constexpr int BIAS = 2 * PAIR;          // 156672: bias of tile parity s at + 256 s
+  static constexpr int SCR = BIAS + 512;         // statistics partials
+  static constexpr int GSS = SCR + 2048;         // GroupNorm (sc, sh) [4 buffers][4 helpers][8 ch][2] fp32 (128 B rows)
+  static constexpr int CNT = GSS + 2048;         // statistics arrival counters
+  static constexpr int SMEM = CNT + 256;         // 161536 of the CU's 163840
+};
+static_assert(V5sCfg::SMEM <= 163840, "v5s LDS");
+
 template <int MODE, bool GN>
 __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
   using C = V4Cfg;
-  constexpr int NI = 10 + (GN ? 1 : 0);
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[V5Cfg::SMEM];
+  using S = V5sCfg;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[S::SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, hh = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -463,8 +480,8 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
   if (ntile <= 0) return;
   auto tile_of = [&](int it) { return v4_tile_of(p, it); };
   const int tiles = p.tx * p.ty * p.tz;
-  const int nchv = 2 * p.nch;   // bf16 weight chunks: two passes per fp32 chunk
-  unsigned* cnt = reinterpret_cast<unsigned*>(smem + V5Cfg::CNT);
+  const int nvc = 3 * (p.nch / 2);   // bf16 weight chunks: three passes per pair of fp32 chunks
+  unsigned* cnt = reinterpret_cast<unsigned*>(smem + S::CNT);
 
   if (wv < 4) {
     // ------------------------------------------------------------ MFMA waves
@@ -472,26 +489,28 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
     const int f = wv & 1, vg = wv >> 1, zb = 2 * vg;
     const unsigned char* wlane = p.aw + f * 1024 + lr * 32 + ((hh ^ ((lr >> 3) & 1)) << 4);
     auto load_w = [&](u32x4 (&w)[3], int ct, int cv, int g) {
-      const unsigned char* src = wlane + ((long long)ct * nchv + cv) * 27 * 2048 + ((g / 3) * 9 + (g % 3)) * 2048;
+      const unsigned char* src = wlane + ((long long)ct * nvc + cv) * 27 * 2048 + ((g / 3) * 9 + (g % 3)) * 2048;
       v4_gload(w[0], src);
       v4_gload(w[1], src + 3 * 2048);
       v4_gload(w[2], src + 6 * 2048);
     };
-    const int hlane = hh * (C::HVP * 16) + (zb * (C::HX * C::HY) + lr) * 16;
+    const int rows = (zb * (C::HX * C::HY) + lr) * 16;
+    const int hl_ab = hh * S::PLANE + rows;   // passes A / B: (hi, lo) planes of one chunk
+    const int hl_c = hh * S::BUF + rows;      // pass C: the hi planes of chunk a (K 0-7) and chunk b (K 8-15)
     f32x16 acc[2][4];
     u32x4 wr[3][3];
     V4Tile cur = tile_of(0);
-    load_w(wr[0], cur.ct, 2 * cur.c0, 0);
-    load_w(wr[1], cur.ct, 2 * cur.c0, 1);
+    load_w(wr[0], cur.ct, 3 * (cur.c0 / 2), 0);
+    load_w(wr[1], cur.ct, 3 * (cur.c0 / 2), 1);
     __builtin_amdgcn_s_barrier();   // B0
-    int gch = 0;
+    int gp = 0;
     const long long HW = (long long)p.H * p.W, V = (long long)p.D * HW;
     for (int it = 0; it < ntile; ++it) {
       const bool more = it + 1 < ntile;
       const V4Tile nxt = more ? tile_of(it + 1) : cur;
       {
         float bia[16];
-        const float* bl = reinterpret_cast<const float*>(smem + V5Cfg::BIAS + (it & 1) * 256) + f * 32 + 4 * hh;
+        const float* bl = reinterpret_cast<const float*>(smem + S::BIAS + (it & 1) * 256) + f * 32 + 4 * hh;
 #pragma unroll
         for (int i = 0; i < 16; ++i) bia[i] = bl[8 * (i >> 2) + (i & 3)];
         const float bm = p.bias ? 1.f : 0.f;
@@ -502,7 +521,7 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[a][m][i] = bia[i] * bm;
       }
-      // one bf16 weight pass (virtual chunk cv) over the halo at hb; LASTV: the tile's last pass
+      // one bf16 weight pass (virtual chunk cv) over the planes at hb; LASTV: the tile's last pass
       auto vpass = [&](auto lastc, int cv, const unsigned char* hb) {
         constexpr bool LASTV = decltype(lastc)::value;
         u32x4 av[2][6];
@@ -513,7 +532,7 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
           if (PL == 0) {                                                                                     \
             if (GI + 2 < 9) load_w(wr[(GI + 2) % 3], cur.ct, cv, GI + 2);                                    \
             else if (!LASTV) load_w(wr[(GI + 2) % 3], cur.ct, cv + 1, GI - 7);                               \
-            else load_w(wr[(GI + 2) % 3], nxt.ct, 2 * nxt.c0, GI - 7);                                       \
+            else load_w(wr[(GI + 2) % 3], nxt.ct, 3 * (nxt.c0 / 2), GI - 7);                                 \
           }                                                                                                  \
           if (KN < 18) v4_read_step<KN % 18>(av[BC ^ 1], hb);                                                \
           if (PL == 0) V4_WAIT_W(6, wr[GI % 3]);                                                             \
@@ -528,20 +547,23 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
         V5S_STEP(12) V5S_STEP(13) V5S_STEP(14) V5S_STEP(15) V5S_STEP(16) V5S_STEP(17)
 #undef V5S_STEP
       };
-      for (int c = cur.c0; c + 1 < cur.c1; ++c) {
-        const unsigned char* hb = smem + (gch % 3) * C::HALO_B + hlane;
-        vpass(std::false_type{}, 2 * c, hb);
-        vpass(std::false_type{}, 2 * c + 1, hb);
-        __builtin_amdgcn_s_barrier();   // chunk k read; chunk k + 1 split
-        ++gch;
+      const int p1 = cur.c1 / 2;
+      for (int pp = cur.c0 / 2; pp + 1 < p1; ++pp) {
+        const unsigned char* base = smem + (gp & 1) * S::PAIR;
+        vpass(std::false_type{}, 3 * pp, base + hl_ab);
+        vpass(std::false_type{}, 3 * pp + 1, base + S::BUF + hl_ab);
+        vpass(std::false_type{}, 3 * pp + 2, base + hl_c);
+        __builtin_amdgcn_s_barrier();   // pair k read; pair k + 1 split
+        ++gp;
       }
       {
-        const int c = cur.c1 - 1;
-        const unsigned char* hb = smem + (gch % 3) * C::HALO_B + hlane;
-        vpass(std::false_type{}, 2 * c, hb);
-        vpass(std::true_type{}, 2 * c + 1, hb);
+        const int pp = p1 - 1;
+        const unsigned char* base = smem + (gp & 1) * S::PAIR;
+        vpass(std::false_type{}, 3 * pp, base + hl_ab);
+        vpass(std::false_type{}, 3 * pp + 1, base + S::BUF + hl_ab);
+        vpass(std::true_type{}, 3 * pp + 2, base + hl_c);
         __builtin_amdgcn_s_barrier();
-        ++gch;
+        ++gp;
       }
       // fp32 epilogue from the accumulators: + residual, store, (sum, sum^2) partials
       {
@@ -602,7 +624,7 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
             ssq[i] += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, ssq[i]), 0x401F));
           }
           // this wave's partial: scratch [f][vg][2 halves][16] sums, then squares at + 256
-          float* sc = reinterpret_cast<float*>(smem + V5Cfg::SCR) + (f * 2 + vg) * 32 + hh * 16;
+          float* sc = reinterpret_cast<float*>(smem + S::SCR) + (f * 2 + vg) * 32 + hh * 16;
           if (lr == 0) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) { sc[i] = ssum[i]; sc[256 + i] = ssq[i]; }
@@ -614,7 +636,7 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
           if (old & 1u) {   // the second of the channel half's two plane waves
             if (lane < 32) {
               const int h2 = (lane >> 2) & 1, i = 4 * (lane >> 3) + (lane & 3);
-              const float* s0 = reinterpret_cast<const float*>(smem + V5Cfg::SCR) + f * 64 + h2 * 16 + i;
+              const float* s0 = reinterpret_cast<const float*>(smem + S::SCR) + f * 64 + h2 * 16 + i;
               const float su = s0[0] + s0[32], sq = s0[256] + s0[256 + 32];
               const long long pidx = ((long long)cur.b * tiles + cur.sl) * p.cout + c0w + lane;
               *reinterpret_cast<float2*>(p.stats + pidx * 2) = make_float2(su, sq);
@@ -633,33 +655,41 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
   const int h = wv - 4;
   int pit = 0;
   V4Tile pt = tile_of(0);
-  int pc = pt.c0;
-  auto issue_next = [&](int buf) -> bool {
+  int pc = pt.c0;   // the next pair's first fp32 chunk
+  // the next pair (two chunks) into pipeline stage st: buffers 2 st, 2 st + 1
+  auto issue_pair = [&](int st) -> bool {
     if (pit >= ntile) return false;
-    v4_issue_halo<float, MODE>(p, pt, pc, smem + buf * C::HALO_B, h, lane);
-    if constexpr (GN) {
-      if (lane < 16)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(p.agn + ((long long)pt.b * (p.ac0 + p.ac1) + pc * 8) * 2 + lane),
-            (__attribute__((address_space(3))) void*)(smem + V5Cfg::GSS + (buf * 4 + h) * 128), 4, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      v4_issue_halo<float, MODE, S::PLANE>(p, pt, pc + k, smem + st * S::PAIR + k * S::BUF, h, lane);
+      if constexpr (GN) {
+        if (lane < 16)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(p.agn + ((long long)pt.b * (p.ac0 + p.ac1) + (pc + k) * 8) * 2 +
+                                                              lane),
+              (__attribute__((address_space(3))) void*)(smem + S::GSS + ((2 * st + k) * 4 + h) * 128), 4, 0, 0);
+      }
     }
-    if (pc + 1 < pt.c1) ++pc;
+    if (pc + 2 < pt.c1) pc += 2;
     else if (++pit < ntile) { pt = tile_of(pit); pc = pt.c0; }
     return true;
   };
-  // fp32 chunk at buffer buf, this wave's voxel slots (h + 4 j) * 64 + lane: (GroupNorm + SiLU,)
-  // then plane 0 <- hi, plane 1 <- lo of the 8 channels
-  auto split = [&](int x0, int y0, int z0, int buf) {
-    unsigned char* hb = smem + buf * C::HALO_B;
+  // fp32 chunk in buffer bi, this wave's voxel slots (h + 4 j) * 64 + lane (< HV: the planes
+  // are packed, a padding slot would be the next plane's): (GroupNorm + SiLU,) then
+  // plane 0 <- hi, plane 1 <- lo of the 8 channels
+  auto split = [&](int x0, int y0, int z0, int bi) {
+    unsigned char* hb = smem + bi * S::BUF;
     u32x4 x[2][5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j)
+    for (int j = 0; j < 5; ++j) {
+      const int hv = (h + 4 * j) * 64 + lane;
 #pragma unroll
       for (int qd = 0; qd < 2; ++qd)
-        x[qd][j] = *reinterpret_cast<const u32x4*>(hb + qd * (C::HVP * 16) + ((h + 4 * j) * 64 + lane) * 16);
+        if (j < 4 || hv < C::HV) x[qd][j] = *reinterpret_cast<const u32x4*>(hb + qd * S::PLANE + hv * 16);
+    }
     float sc[8], sh[8], mk[5];
     if constexpr (GN) {
-      const float* gs = reinterpret_cast<const float*>(smem + V5Cfg::GSS + (buf * 4 + h) * 128);
+      const float* gs = reinterpret_cast<const float*>(smem + S::GSS + (bi * 4 + h) * 128);
 #pragma unroll
       for (int e = 0; e < 8; ++e) silu_aff_coef(gs[2 * e], gs[2 * e + 1], sc[e], sh[e]);
 #pragma unroll
@@ -674,6 +704,8 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
     }
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
+      const int hv = (h + 4 * j) * 64 + lane;
+      if (j == 4 && hv >= C::HV) continue;
       float v[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) { v[e] = __uint_as_float(x[0][j][e]); v[4 + e] = __uint_as_float(x[1][j][e]); }
@@ -687,42 +719,44 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
         hi[e] = pack2<bf16_t>(v[2 * e], v[2 * e + 1]);
         lo[e] = pack2<bf16_t>(v[2 * e] - lo2f<bf16_t>(hi[e]), v[2 * e + 1] - hi2f<bf16_t>(hi[e]));
       }
-      *reinterpret_cast<u32x4*>(hb + ((h + 4 * j) * 64 + lane) * 16) = hi;
-      *reinterpret_cast<u32x4*>(hb + C::HVP * 16 + ((h + 4 * j) * 64 + lane) * 16) = lo;
+      *reinterpret_cast<u32x4*>(hb + hv * 16) = hi;
+      *reinterpret_cast<u32x4*>(hb + S::PLANE + hv * 16) = lo;
     }
   };
   auto issue_bias = [&](const V4Tile& tt, int slot) {
     if (p.bias && h == 0)
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(p.bias + (long long)tt.b * p.bias_bs + tt.ct * 64 + lane),
-          (__attribute__((address_space(3))) void*)(smem + V5Cfg::BIAS + slot * 256), 4, 0, 0);
+          (__attribute__((address_space(3))) void*)(smem + S::BIAS + slot * 256), 4, 0, 0);
   };
   V4Tile cur = tile_of(0);
   if (h == 0 && lane < 2) cnt[lane] = 0u;
-  issue_next(0);
+  issue_pair(0);
   issue_bias(cur, 0);
-  issue_next(1);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   split(cur.x0, cur.y0, cur.z0, 0);
+  split(cur.x0, cur.y0, cur.z0, 1);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();   // B0
-  int gch = 0;
+  int gp = 0;
   for (int it = 0; it < ntile; ++it) {
     const bool more = it + 1 < ntile;
     const V4Tile nxt = more ? tile_of(it + 1) : cur;
-    for (int c = cur.c0; c < cur.c1; ++c) {
-      const bool first = c == cur.c0, lastc = c + 1 == cur.c1;
-      const bool iss = issue_next((gch + 2) % 3);
-      if (!(lastc && !more)) {
-        if (iss) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const V4Tile& t1 = lastc ? nxt : cur;
-        split(t1.x0, t1.y0, t1.z0, (gch + 1) % 3);
-      }
+    for (int pp = cur.c0 / 2; pp < cur.c1 / 2; ++pp) {
+      const bool first = pp == cur.c0 / 2, lastp = pp + 1 == cur.c1 / 2;
+      // stage gp + 1 (the tile's next pair, or the next tile's first) under this stage's MFMAs
+      const int st = (gp + 1) & 1;
+      const bool iss = issue_pair(st);
       if (first && more) issue_bias(nxt, (it + 1) & 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (iss) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const V4Tile& t1 = lastp ? nxt : cur;
+        split(t1.x0, t1.y0, t1.z0, 2 * st);
+        split(t1.x0, t1.y0, t1.z0, 2 * st + 1);
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      ++gch;
+      ++gp;
     }
     cur = nxt;
   }
@@ -758,6 +792,7 @@ bool v5_eligible(const cwdm_conv3d_desc* d, bool gn) {
     if (!d->a_w_split || path == 1 || path == 3) return false;
     if (d->out_dtype != CWDM_F32 || d->accumulate || d->out1) return false;
     if (d->a_mode != 0 && d->a_mode != 1) return false;
+    if (d->a_c0 % 16 || d->a_c1 % 16) return false;   // pairs of 8-channel fp32 chunks, never straddling the sources
     if (d->res_mode < -1 || d->res_mode > 1) return false;
     // the 1x1 skip product is added through the residual slot (conv3d_v4_forward): not both
     if (d->b_w && d->res_mode >= 0) return false;

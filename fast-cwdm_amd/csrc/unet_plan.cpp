@@ -556,7 +556,7 @@ void build(cwdm_unet* u) {
   u->off_emb_b = take((int64_t)u->R * 4);
   for (auto& cs : u->convs) {
     cs.w_off = take(cwdm_conv3d_packed_bytes(cs.cout, cs.cin_a, 3, c.dtype));
-    if (c.mfma_split && c.dtype == CWDM_F32 && !cs.s2 && cs.cout % 64 == 0 && cs.cin_a % 8 == 0)
+    if (c.mfma_split && c.dtype == CWDM_F32 && !cs.s2 && cs.cout % 64 == 0 && cs.cin_a % 16 == 0)
       cs.wsplit_off = take(cwdm_conv3d_packed_split_bytes(cs.cout, cs.cin_a));
     if (cs.ws_p >= 0) cs.wsk_off = take(cwdm_conv3d_packed_bytes(cs.cout, cs.cin_b, 1, c.dtype));
     if (cs.bias_kind == 0) cs.bias_off = take((int64_t)cs.cout * 4);

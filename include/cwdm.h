@@ -292,11 +292,14 @@ typedef struct {
   int accumulate;           /* out += result instead of out = result */
   const void* a_w_split;    /* fp32 convs (optional): cwdm_conv3d_pack_split weights -- the accurate fast
                                mode: the conv MFMAs run on bf16 hi/lo splits of the fp32 operands (every
-                               product hi.hi + hi.lo + lo.hi + lo.lo, fp32 accumulation) where the shape
-                               takes the warp-specialised kernel; fp32 in, fp32 out */
+                               product hi.hi + lo.hi + hi.lo, fp32 accumulation; lo.lo is below fp32
+                               rounding) where the shape takes the warp-specialised kernel (a_c0, a_c1
+                               multiples of 16); fp32 in, fp32 out */
 } cwdm_conv3d_desc;
 int64_t cwdm_conv3d_packed_bytes(int cout, int cin, int ksize, int dtype);
-/* Split-bf16 weights of a 3x3x3 fp32 conv (cout % 64 == 0) for cwdm_conv3d_desc.a_w_split. */
+/* Split-bf16 weights of a 3x3x3 fp32 conv (cout % 64 == 0, cin % 16 == 0) for
+ * cwdm_conv3d_desc.a_w_split: per 16 input channels three bf16 chunks
+ * ([hi|hi] of each 8-channel half, then [lo|lo] of the two halves). */
 int64_t cwdm_conv3d_packed_split_bytes(int cout, int cin);
 int cwdm_conv3d_pack_split(const float* w_oidhw, int cout, int cin, void* packed, cwdm_stream_t stream);
 int cwdm_conv3d_pack(const float* w_oidhw, int cout, int cin, int ksize, int dtype,
