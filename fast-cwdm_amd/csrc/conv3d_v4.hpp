@@ -79,6 +79,7 @@ struct V4Params {
   FastDiv gdiv;
   // conv3d_v5: GroupNorm scale / shift [B][ac0 + ac1][2] of the raw sources, applied in LDS (null: none)
   const float* agn;
+  int diag;   // timing-only diagnostics build (-DCWDM_V5_DIAG, env CWDM_V5_DIAGMASK): parts of v5 switched off
 };
 
 

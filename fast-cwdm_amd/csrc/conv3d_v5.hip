@@ -58,6 +58,16 @@ static_assert(V5Cfg::SMEM <= 163840, "v5 LDS");
 // [0] start, [1] MFMA waves past B0, [2 + k] MFMA wave 0 at chunk k's barrier, [18 + k] released from it,
 // [34 + k] helper 0 at chunk k's barrier (k < 16), [50] / [51] s_memrealtime at start / end of MFMA wave 0,
 // [52] end of helper 0, [53] HW_ID, [54] XCC_ID
+// timing-only diagnostics build (make V5DIAG=1; the results are garbage): env CWDM_V5_DIAGMASK bits
+// 1 helpers issue no halo DMA, 2 MFMA waves read no LDS operands, 4 MFMA waves load no weights,
+// 8 the in-LDS GroupNorm transform without its SiLU math (load + store only), 16 no transform at all,
+// 32 helpers drain nothing (no stores / statistics)
+#ifdef CWDM_V5_DIAG
+#define V5_DIAG(bit) ((p.diag & (bit)) != 0)
+#else
+#define V5_DIAG(bit) false
+#endif
+
 #ifdef CWDM_CONV_STAMPS
 #define V5_STAMP(k, cond)                                                                        \
   do {                                                                                           \
@@ -96,6 +106,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
     const int f = wv & 1, vg = wv >> 1, zb = 2 * vg;
     const unsigned char* wlane = p.aw + f * 1024 + lr * 32 + ((hh ^ ((lr >> 3) & 1)) << 4);
     auto load_w = [&](u32x4 (&w)[3], int ct, int c, int g) {
+      if (V5_DIAG(4)) return;
       const unsigned char* src = wlane + ((long long)ct * p.nch + c) * 27 * 2048 + ((g / 3) * 9 + (g % 3)) * 2048;
       v4_gload(w[0], src);
       v4_gload(w[1], src + 3 * 2048);
@@ -129,7 +140,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
         constexpr bool LAST = decltype(lastc)::value;
         const unsigned char* hb = smem + (gch % 3) * C::HALO_B + hlane;
         u32x4 av[2][6];
-        v4_read_step<0>(av[0], hb);
+        if (!V5_DIAG(2)) v4_read_step<0>(av[0], hb);
 #define V5_STEP(K)                                                                                           \
         {                                                                                                    \
           constexpr int GI = (K) / 2, PL = (K) % 2, KN = (K) + 1, BC = (K) & 1;                              \
@@ -142,7 +153,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
             else if (!LAST) load_w(wr[(GI + 2) % 3], cur.ct, c + 1, GI - 7);                                 \
             else load_w(wr[(GI + 2) % 3], nxt.ct, nxt.c0, GI - 7);                                           \
           }                                                                                                  \
-          if (KN < 18) v4_read_step<KN % 18>(av[BC ^ 1], hb);                                                \
+          if (KN < 18 && !V5_DIAG(2)) v4_read_step<KN % 18>(av[BC ^ 1], hb);                                 \
           if (PL == 0) V4_WAIT_W(6, wr[GI % 3]);                                                             \
           __builtin_amdgcn_sched_barrier(0);                                                                 \
           _Pragma("unroll") for (int dy = 0; dy < 3; ++dy)                                                   \
@@ -204,7 +215,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   int pc = pt.c0;
   auto issue_next = [&](int buf) -> bool {
     if (pit >= ntile) return false;
-    v4_issue_halo<T, MODE>(p, pt, pc, smem + buf * C::HALO_B, h, lane);
+    if (!V5_DIAG(1)) v4_issue_halo<T, MODE>(p, pt, pc, smem + buf * C::HALO_B, h, lane);
     if constexpr (GN) {
       if (lane < 32)
         __builtin_amdgcn_global_load_lds(
@@ -219,6 +230,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   // quad planes) of the chunk in buffer buf; slots outside the volume stay zero
   auto transform = [&](int x0, int y0, int z0, int buf) {
     if constexpr (GN) {
+      if (V5_DIAG(16)) return;
       unsigned char* hb = smem + buf * C::HALO_B;
       const float* gs = reinterpret_cast<const float*>(smem + V5Cfg::GSS + (buf * 4 + h) * 128);
       u32x4 x[2][5];
@@ -248,7 +260,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
           float xv[8], y[8];
           unpack<T>(x[qd][j], xv);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) y[e] = silu_aff(xv[e], sa[e], sb[e]);
+          for (int e = 0; e < 8; ++e) y[e] = V5_DIAG(8) ? xv[e] : silu_aff(xv[e], sa[e], sb[e]);
           if (!inner) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) y[e] *= mk[j];
@@ -289,6 +301,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   // y0 + (i & 3), z0 + (i >> 2)), channels tile + 8 q .. + 7; part 0 from halo buffer sb, part 1 from the
   // spare; the residual rows are in rq (drain_load)
   auto drain = [&](const V4Tile& tt, int part, int sb) {
+    if (V5_DIAG(32)) return;
     const int ox = tt.x0 + 8 * h + r8;
     const bool xin = ox < p.W;
     const float xm = xin ? 1.f : 0.f;
@@ -859,6 +872,10 @@ int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   p.stats = d->stats;
   p.ksplit = 1; p.kper = p.nch;
   p.agn = agn;
+#ifdef CWDM_V5_DIAG
+  static const int diag = [] { const char* e = std::getenv("CWDM_V5_DIAGMASK"); return e ? std::atoi(e) : 0; }();
+  p.diag = diag;
+#endif
   p.stamps = g_stamps.load(std::memory_order_relaxed);
   const long long nblk = (long long)p.B * p.tx * p.ty * p.tz * p.nct;
   p.nblk = (int)nblk;
