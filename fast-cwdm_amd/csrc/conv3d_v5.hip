@@ -67,6 +67,9 @@ static_assert(V5Cfg::SMEM <= 163840, "v5 LDS");
 #else
 #define V5_DIAG(bit) false
 #endif
+// bit 64: each tile runs its K chunks rotated by its spatial index (the same sum in another order), so
+// neighbouring CUs ask for different weight chunks at the same time
+#define V5_PHYS(t, c) (V5_DIAG(64) ? (t).c0 + ((c) - (t).c0 + (t).sl) % ((t).c1 - (t).c0) : (c))
 
 #ifdef CWDM_CONV_STAMPS
 #define V5_STAMP(k, cond)                                                                        \
@@ -116,8 +119,8 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
     f32x16 acc[2][4];
     u32x4 wr[3][3];
     V4Tile cur = tile_of(0);
-    load_w(wr[0], cur.ct, cur.c0, 0);
-    load_w(wr[1], cur.ct, cur.c0, 1);
+    load_w(wr[0], cur.ct, V5_PHYS(cur, cur.c0), 0);
+    load_w(wr[1], cur.ct, V5_PHYS(cur, cur.c0), 1);
     __builtin_amdgcn_s_barrier();   // B0: chunk 0 transformed, bias 0 landed
     V5_STAMP(1, tid == 0);
     int gch = 0;
@@ -149,9 +152,9 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
           /* reloads its own first group instead of skipping the load: nxt == cur there)               */ \
           /* weights two groups ahead (one MFMA wave per SIMD: nothing else hides an L2 round trip) */   \
           if (PL == 0) {                                                                                     \
-            if (GI + 2 < 9) load_w(wr[(GI + 2) % 3], cur.ct, c, GI + 2);                                     \
-            else if (!LAST) load_w(wr[(GI + 2) % 3], cur.ct, c + 1, GI - 7);                                 \
-            else load_w(wr[(GI + 2) % 3], nxt.ct, nxt.c0, GI - 7);                                           \
+            if (GI + 2 < 9) load_w(wr[(GI + 2) % 3], cur.ct, V5_PHYS(cur, c), GI + 2);                       \
+            else if (!LAST) load_w(wr[(GI + 2) % 3], cur.ct, V5_PHYS(cur, c + 1), GI - 7);                   \
+            else load_w(wr[(GI + 2) % 3], nxt.ct, V5_PHYS(nxt, nxt.c0), GI - 7);                             \
           }                                                                                                  \
           if (KN < 18 && !V5_DIAG(2)) v4_read_step<KN % 18>(av[BC ^ 1], hb);                                 \
           if (PL == 0) V4_WAIT_W(6, wr[GI % 3]);                                                             \
@@ -215,11 +218,12 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   int pc = pt.c0;
   auto issue_next = [&](int buf) -> bool {
     if (pit >= ntile) return false;
-    if (!V5_DIAG(1)) v4_issue_halo<T, MODE>(p, pt, pc, smem + buf * C::HALO_B, h, lane);
+    if (!V5_DIAG(1)) v4_issue_halo<T, MODE>(p, pt, V5_PHYS(pt, pc), smem + buf * C::HALO_B, h, lane);
     if constexpr (GN) {
       if (lane < 32)
         __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(p.agn + ((long long)pt.b * (p.ac0 + p.ac1) + pc * 16) * 2 + lane),
+            (const __attribute__((address_space(1))) void*)(p.agn + ((long long)pt.b * (p.ac0 + p.ac1) +
+                                                                      V5_PHYS(pt, pc) * 16) * 2 + lane),
             (__attribute__((address_space(3))) void*)(smem + V5Cfg::GSS + (buf * 4 + h) * 128), 4, 0, 0);
     }
     if (pc + 1 < pt.c1) ++pc;
