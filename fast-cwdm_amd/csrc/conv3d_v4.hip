@@ -217,7 +217,8 @@ int sg_skip_ksplit(const cwdm_conv3d_desc* d);
 int64_t sg_sync_bytes(int ksplit);
 bool v5_eligible(const cwdm_conv3d_desc* d, bool gn);
 int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
-              const float* agn, const void* res, int rmode, hipStream_t s);
+              const float* agn, const void* res, int rmode, hipStream_t s, const V5Aa* aa = nullptr);
+int v5_aa_units(const cwdm_conv3d_desc* d, int* lead);
 
 int64_t v4_items(const cwdm_conv3d_desc* d) {
   return d->B * ((d->W + 31) / 32) * (d->H / 4) * (d->D / 4) * (d->cout / 64);
@@ -532,9 +533,13 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   // inference only -- the training forward keeps the activated input for wgrad
   const float* agn = nullptr;
   if (d->a_gn && !g_act_keep && v5_eligible(d, true)) agn = d->a_gn;
+  // or the warp-specialised conv writes the activated copy itself, ahead of its sweep (apply-ahead:
+  // no pre-pass over HBM; the training forward keeps the copy it writes)
+  V5Aa aa{};
+  aa.units = (d->a_gn && !agn) ? v5_aa_units(d, &aa.lead) : 0;
   // an offered GroupNorm finalize (GnFinFuse): fused into the pre-pass below where it fits, else run now
   GnFinFuse* fin = (g_gnfin && !g_gnfin->used && d->a_gn && g_gnfin->ss == d->a_gn) ? g_gnfin : nullptr;
-  if (fin && (agn || !gn_fin_fusable(*fin, d->dtype, c0, c1))) {
+  if (fin && (agn || aa.units || !gn_fin_fusable(*fin, d->dtype, c0, c1))) {
     if ((rc = gnfin_flush(d, s))) return rc;
     fin = nullptr;
   }
@@ -548,7 +553,9 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     } else {
       ws += align256(d->B * SV * (c0 + c1) * esz);
     }
-    if (fin) {
+    if (aa.units) {
+      aa.x0 = a0; aa.c0 = c0; aa.x1 = a1; aa.c1 = c1; aa.gn = d->a_gn;
+    } else if (fin) {
       fin->used = true;
       if ((rc = gn_fin_apply(*fin, a0, c0, a1, c1, d->B, SV, d->dtype, act, s))) return rc;
     } else if ((rc = gn_apply(a0, c0, a1, c1, d->a_gn, d->B, SV, d->dtype, act, s, 1))) {
@@ -577,6 +584,7 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     res = skip; rmode = 0;
   }
   if (agn) return v5_launch(d, a0, c0, a1, c1, 0, agn, res, rmode, s);
+  if (aa.units) return v5_launch(d, a0, c0, nullptr, 0, 1, nullptr, res, rmode, s, &aa);
   return v4_launch(d, a0, c0, a1, c1, a0_cm, res, rmode, v4_ksplit(d) > 1 ? ws : nullptr, s);
 }
 

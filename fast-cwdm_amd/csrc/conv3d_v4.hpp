@@ -80,10 +80,21 @@ struct V4Params {
   // conv3d_v5: GroupNorm scale / shift [B][ac0 + ac1][2] of the raw sources, applied in LDS (null: none)
   const float* agn;
   int diag;   // timing-only diagnostics build (-DCWDM_V5_DIAG, env CWDM_V5_DIAGMASK): parts of v5 switched off
+  // conv3d_v5 apply-ahead (conv3d_v5_kernel<..., AA > 0>): the kernel writes SiLU(x sc + sh) of the raw
+  // channels-last sources ax0 (axc0 channels) / ax1 (axc1), sc / sh = agn, chunk-major into a0 itself,
+  // aa_lead sweep iterations ahead of the tiles that read it (batch 1)
+  const void* ax0; const void* ax1; int axc0, axc1; int aa_lead;
+  int aa_units;   // steps of the share per chunk (<= the instance's AA loads)
+  int aa_prio;    // helpers at s_setprio 1 for the share's transform (env CWDM_V5_AA_PRIO, A/B knob)
 };
 
 
 __device__ unsigned g_v4_cu_arrivals[8 * 256];
+
+// conv3d_v5 apply-ahead arguments (conv3d_v5.hip): the raw sources of a GroupNorm'd input, their
+// scale / shift, the sweep lead and the per-chunk share of the kernel instance (v5_aa_units)
+struct V5Aa { const void* x0; int c0; const void* x1; int c1; const float* gn; int lead, units; };
+
 struct V4Cfg {
   static constexpr int HX = 34, HY = 6, HZ = 6, HV = HX * HY * HZ;  // 1224 halo voxels
   static constexpr int HVP = 1280;                                   // slots per quad plane (20 pieces)
@@ -485,7 +496,9 @@ __device__ __forceinline__ V4Tile v4_tile_of(const V4Params& p, int it) {
 // chunk (a few VALU per piece) rather than held in registers.
 // PB: byte stride of the two quad planes (v4 / v5: the padded 1280 slots; the
 // split-bf16 kernel packs them at 1224 slots -- the padding lanes never write)
-template <typename T, int MODE, int PB = V4Cfg::HVP * 16>
+// ALL: every lane issues its pieces, the slots past the halo (helper 3's last piece) from an
+// out-of-range offset (zeros into the padding): a fixed count of vector-memory ops per chunk
+template <typename T, int MODE, int PB = V4Cfg::HVP * 16, bool ALL = false>
 __device__ __forceinline__ void v4_issue_halo(const V4Params& p, const V4Tile& tt, int c, unsigned char* hb, int wv,
                                               int lane) {
   using C = V4Cfg;
@@ -524,7 +537,7 @@ __device__ __forceinline__ void v4_issue_halo(const V4Params& p, const V4Tile& t
     const int pc = wv + 4 * j;
     const int sv = svox[j % 5];
     const unsigned voff = sv >= 0 ? (unsigned)sv * rowb + cofs + (unsigned)((j / 5) * 16) : 0xFFFFFFF0u;
-    if (sv != -2)
+    if (ALL || sv != -2)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rs, (__attribute__((address_space(3))) void*)(hb + (PB == 20 * 1024 ? pc * 1024 : (pc / 20) * PB + (pc % 20) * 1024)),
           16, voff, 0, 0, 0);

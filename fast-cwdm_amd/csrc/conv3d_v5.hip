@@ -80,7 +80,54 @@ static_assert(V5Cfg::SMEM <= 163840, "v5 LDS");
 #define V5_STAMP(k, cond) do { } while (0)
 #endif
 
-template <typename T, int MODE, bool GN>
+// ---------------------------------------------------------------------------
+// Apply-ahead (AA > 0): the GroupNorm + SiLU of the input without a pre-pass
+// over HBM and without transforming every halo voxel 2.4x in LDS.  The
+// persistent grid sweeps the work items in order -- iteration it runs items
+// [it G, (it + 1) G), G = gridDim.x (XCD x the contiguous eighth x of each
+// block) -- so the voxels iteration it reads are a prefix [0, need(it)) of the
+// source: through the top halo plane of its last tile.  Each workgroup's
+// helper waves transform 1/G of range R(r) = [need(r - 1), need(r)) during
+// iteration r - L (L = aa_lead), once per voxel, from the raw channels-last
+// source into the chunk-major copy the halo DMA reads (written through to
+// memory: sc1); a counter per range collects the G workgroups' completions,
+// and a helper waits on R(it)'s counter before it issues tile it's first
+// DMA.  R(0 .. L - 1) is transformed by all eight waves before the first tile
+// (the one grid-wide wait).  The workgroup that exits last re-zeroes the
+// counters for the next launch.  Batch 1, same-grid sources.
+// ---------------------------------------------------------------------------
+constexpr int kV5AaCnt = 4096;                 // [0] the prologue ranges, [r] range r, [kV5AaCnt - 1] exits
+__device__ unsigned g_v5aa_cnt[kV5AaCnt];
+
+__device__ __forceinline__ int v5aa_pos() {
+  const int G = gridDim.x;
+  const int b = blockIdx.x;
+  return (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3);
+}
+__device__ __forceinline__ V4Tile v5aa_tile_of(const V4Params& p, int it) {
+  const int wg = it * (int)gridDim.x + v5aa_pos();
+  V4Tile r;
+  r.ks = 0; r.c0 = 0; r.c1 = p.nch; r.b = 0;
+  r.ct = wg % p.nct;
+  r.sl = wg / p.nct;
+  r.x0 = (r.sl % p.tx) * 32; r.y0 = ((r.sl / p.tx) % p.ty) * 4; r.z0 = (r.sl / (p.tx * p.ty)) * 4;
+  r.ct = __builtin_amdgcn_readfirstlane(r.ct); r.sl = __builtin_amdgcn_readfirstlane(r.sl);
+  r.x0 = __builtin_amdgcn_readfirstlane(r.x0); r.y0 = __builtin_amdgcn_readfirstlane(r.y0);
+  r.z0 = __builtin_amdgcn_readfirstlane(r.z0);
+  return r;
+}
+// need(j): source voxels the tiles of sweep iterations <= j read (0 for j < 0)
+__host__ __device__ __forceinline__ unsigned v5aa_need(int j, int G, int nblk, int nct, int tx, int ty, int D, int H,
+                                                       int W) {
+  if (j < 0) return 0u;
+  long long w = (long long)(j + 1) * G;
+  if (w > nblk) w = nblk;
+  const int st = (int)(w - 1) / nct;
+  const int z1 = (st / (tx * ty)) * 4 + 5;
+  return (unsigned)(z1 < D ? z1 : D) * (unsigned)H * (unsigned)W;
+}
+
+template <typename T, int MODE, bool GN, int AA = 0>
 __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   using C = V4Cfg;
   using T16 = T;
@@ -90,10 +137,88 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, hh = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nblk = p.nblk;
-  const int ntile = (nblk - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int ntile = (nblk - (AA ? v5aa_pos() : (int)blockIdx.x) + (int)gridDim.x - 1) / (int)gridDim.x;
   if (ntile <= 0) return;
-  auto tile_of = [&](int it) { return v4_tile_of(p, it); };
+  auto tile_of = [&](int it) { return AA ? v5aa_tile_of(p, it) : v4_tile_of(p, it); };
   const int tiles = p.tx * p.ty * p.tz;
+
+  // apply-ahead: this thread's lane slot among nslot cooperating lanes -- quad q (8 channels) of
+  // voxel offset vo within each step of vps voxels; the 8 channels' SiLU coefficients
+  const int G = (int)gridDim.x;
+  const unsigned V = (unsigned)p.D * (unsigned)p.H * (unsigned)p.W;
+  struct AaLane { const unsigned char* src; unsigned rowb, oq; int vo, vps; bool on; float a[8], b[8]; };
+  auto aa_lane = [&](int slot, int nslot) {
+    AaLane l{};
+    if constexpr (AA > 0) {
+      const int Q = (p.axc0 + p.axc1) >> 3, q0 = p.axc0 >> 3;
+      l.vps = nslot / Q;
+      l.on = slot < l.vps * Q;
+      const int q = l.on ? slot % Q : 0;
+      l.vo = l.on ? slot / Q : 0;
+      l.src = q < q0 ? reinterpret_cast<const unsigned char*>(p.ax0) + q * 16
+                     : reinterpret_cast<const unsigned char*>(p.ax1) + (q - q0) * 16;
+      l.rowb = (unsigned)(q < q0 ? p.axc0 : p.axc1) * 2u;
+      l.oq = (unsigned)(q >> 1) * V * 32u + (unsigned)(q & 1) * 16u;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) silu_aff_coef(p.agn[(q * 8 + e) * 2], p.agn[(q * 8 + e) * 2 + 1], l.a[e], l.b[e]);
+    } else {
+      (void)slot; (void)nslot;
+    }
+    return l;
+  };
+  const __amdgpu_buffer_rsrc_t ract = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.a0), (short)0, (int)(AA ? V * (unsigned)(p.axc0 + p.axc1) * 2u : 0u), 0x00020000);
+  auto aa_load = [&](const AaLane& l, unsigned v, bool ok) -> u32x4 {
+    // a global (not flat) load: flat ops count in lgkmcnt too, which the barrier waits drain
+    return *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(
+        (const __attribute__((address_space(1))) unsigned char*)(l.src) + (size_t)(ok ? v : 0u) * l.rowb);
+  };
+  auto aa_store = [&](const AaLane& l, const u32x4& x, unsigned v, bool ok) {
+    float xv[8], y[8];
+    unpack<T>(x, xv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) y[e] = silu_aff(xv[e], l.a[e], l.b[e]);
+    // written through to memory (sc1): read by other XCDs' halo DMA after the range counter
+    __builtin_amdgcn_raw_buffer_store_b128(pack<T>(y), ract, ok ? l.oq + v * 32u : 0xFFFFFFF0u, 0, 16);
+  };
+  // piece [lo, hi) of this workgroup in range [r0, r1)
+  auto aa_piece = [&](unsigned r0, unsigned r1, unsigned& lo, unsigned& hi) {
+    const int pos = v5aa_pos();
+    lo = r0 + (unsigned)((unsigned long long)(r1 - r0) * (unsigned)pos / (unsigned)G);
+    hi = r0 + (unsigned)((unsigned long long)(r1 - r0) * (unsigned)(pos + 1) / (unsigned)G);
+  };
+  auto aa_need = [&](int j) { return v5aa_need(j, G, nblk, p.nct, p.tx, p.ty, p.D, p.H, p.W); };
+  const int aa_nit = (nblk + G - 1) / G;
+  if constexpr (AA > 0) {
+    V5_STAMP(55, tid == 0);
+    // ranges 0 .. L - 1 by all eight waves, then the grid-wide wait for them
+    const AaLane l = aa_lane(tid, 512);
+    unsigned lo, hi;
+    aa_piece(0u, aa_need(p.aa_lead - 1), lo, hi);
+    const int nst = l.vps > 0 ? (int)((hi - lo + (unsigned)l.vps - 1) / (unsigned)l.vps) : 0;
+    for (int s0 = 0; s0 < nst; s0 += 4) {
+      u32x4 x[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned v = lo + (unsigned)((s0 + k) * l.vps + l.vo);
+        x[k] = aa_load(l, v, l.on && v < hi);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned v = lo + (unsigned)((s0 + k) * l.vps + l.vo);
+        aa_store(l, x[k], v, l.on && v < hi);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(&g_v5aa_cnt[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int n = 0; __hip_atomic_load(&g_v5aa_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)G &&
+                      n < (1 << 24); ++n)
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __syncthreads();
+  }
 
   V5_STAMP(0, tid == 0);
 #ifdef CWDM_CONV_STAMPS
@@ -276,9 +401,11 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
       (void)x0; (void)y0; (void)z0; (void)buf;
     }
   };
-  const long long HW = (long long)p.H * p.W, V = (long long)p.D * HW;
+  const long long HW = (long long)p.H * p.W, VV = (long long)p.D * HW;
   const unsigned rowb = (unsigned)p.W * (unsigned)p.cout * 2u, planeb = (unsigned)HW * (unsigned)p.cout * 2u;
   float s1[8], s2[8];   // this lane's statistics over both drain parts of a tile
+  u32x4 dq[8];          // a drain slice's output rows and their byte offsets (drain -> drain_put)
+  unsigned doff[8];
   // the residual rows of drain part `part` of tile tt (this lane's rows i = 8 part .. + 7): loaded
   // one chunk ahead of their drain (part 0 under the tile's last chunk, part 1 under part 0's
   // chunk), so their latency is not on the helper's path at the tile seam
@@ -287,7 +414,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
     if (p.rmode < 0) return;
     const int ox = tt.x0 + 8 * h + r8;
     const bool xin = ox < p.W;
-    const long long rV = p.rmode == 1 ? V / 8 : V;
+    const long long rV = p.rmode == 1 ? VV / 8 : VV;
     const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(reinterpret_cast<const T16*>(p.res) + (long long)tt.b * rV * p.cout), (short)0,
         (int)(rV * p.cout * 2), 0x00020000);
@@ -301,10 +428,11 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
           rr, xin ? rv * (unsigned)p.cout * 2u + (unsigned)(tt.ct * 64 + 8 * q) * 2u : 0xFFFFFFF0u, 0, 0);
     }
   };
-  // drain part `part` of staged tile tt: rows i = 8 part .. + 7 of this lane = voxels (x0 + 8 h + r8,
-  // y0 + (i & 3), z0 + (i >> 2)), channels tile + 8 q .. + 7; part 0 from halo buffer sb, part 1 from the
-  // spare; the residual rows are in rq (drain_load)
-  auto drain = [&](const V4Tile& tt, int part, int sb) {
+  // drain rows k0 .. k1 - 1 of part `part` of staged tile tt: row k = voxel (x0 + 8 h + r8, y0 + (i & 3),
+  // z0 + (i >> 2)), i = 8 part + k, channels tile + 8 q .. + 7; part 0 from halo buffer sb (all its rows
+  // at once: the next DMA overwrites it), part 1 from the spare (spread over the next tile's chunks); the
+  // residual rows are in rq (drain_load); the statistics leave with the last row of part 1
+  auto drain = [&](const V4Tile& tt, int part, int sb, int k0, int k1) {
     if (V5_DIAG(32)) return;
     const int ox = tt.x0 + 8 * h + r8;
     const bool xin = ox < p.W;
@@ -313,6 +441,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
     const unsigned char* base = smem + (part ? V5Cfg::STG1 : sb * C::HALO_B);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
+      if (k < k0 || k >= k1) continue;
       const int row = 8 * (h + 4 * k) + r8;
       sv[k] = *reinterpret_cast<const u32x4*>(base + row * 128 + ((q ^ r8) << 4));
     }
@@ -320,12 +449,11 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
     }
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<T16*>(p.out) + (long long)tt.b * V * p.cout, (short)0, (int)(V * p.cout * 2), 0x00020000);
     const unsigned obase =
         ((unsigned)((tt.z0 * p.H + tt.y0) * p.W) + (unsigned)ox) * (unsigned)p.cout * 2u + (unsigned)(tt.ct * 64 + 8 * q) * 2u;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
+      if (k < k0 || k >= k1) continue;
       const int i = 8 * part + k;
       float v[8];
       unpack<T>(sv[k], v);
@@ -342,9 +470,10 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
         s2[e] += vv * vv;
       }
       const unsigned oo = obase + (unsigned)(i >> 2) * planeb + (unsigned)(i & 3) * rowb;
-      __builtin_amdgcn_raw_buffer_store_b128(pack<T>(v), ro, xin ? oo : 0xFFFFFFF0u, 0, 0);
+      dq[k] = pack<T>(v);
+      doff[k] = xin ? oo : 0xFFFFFFF0u;
     }
-    if (part == 1 && p.stats) {
+    if (part == 1 && k1 == 8 && p.stats) {
       // sum over the 8 lanes of each channel block q (lanes q + 8 r8): xor 8 (DPP), 16 (swizzle), 32 (permlane)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
@@ -378,12 +507,171 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
       }
     }
   };
+  // the stores of drain slice k0 .. k1 - 1 (tile tt)
+  auto drain_put = [&](const V4Tile& tt, int k0, int k1) {
+    if (V5_DIAG(32)) return;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<T16*>(p.out) + (long long)tt.b * VV * p.cout, (short)0, (int)(VV * p.cout * 2), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < k0 || k >= k1) continue;
+      __builtin_amdgcn_raw_buffer_store_b128(dq[k], ro, doff[k], 0, 0);
+    }
+  };
   auto issue_bias = [&](const V4Tile& tt, int slot) {
     if (p.bias && h == 0)
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(p.bias + (long long)tt.b * p.bias_bs + tt.ct * 64 + lane),
           (__attribute__((address_space(3))) void*)(smem + V5Cfg::BIAS + slot * 256), 4, 0, 0);
   };
+
+  if constexpr (AA > 0) {
+    // ------------------------------------------------- helper waves, apply-ahead sweep
+    // Per chunk, in this order (every chunk issues the same vector-memory ops, so the counted
+    // waits need no branches): the drain slice's LDS reads and math (outputs held in registers;
+    // the compiler's wait for its residual retires chunk k + 1's pieces), AA = A raw loads of this
+    // tile's share of range R(it + L), the halo DMA of chunk k + 2, a counted wait that retires
+    // everything older than the AA loads, the AA transform + write-through stores, part 1's
+    // residual loads, the drain stores.
+    constexpr int NA = 10;   // halo pieces per chunk and helper (every lane issues: v4_issue_halo<.., true>)
+    const AaLane al = aa_lane(h * 64 + lane, 256);
+    const int L = p.aa_lead;
+    int pit = 0;
+    V4Tile pt = tile_of(0);
+    int pc = pt.c0;
+    bool chk = false;   // the cursor's tile reads a range some other workgroup may still write
+    auto issue_aa = [&](int buf) {
+      v4_issue_halo<T, MODE, C::HVP * 16, true>(p, pt, pc, smem + buf * C::HALO_B, h, lane);
+      if (pc + 1 < pt.c1) {
+        ++pc;
+      } else if (pit + 1 < ntile) {
+        ++pit; pt = tile_of(pit); pc = pt.c0;
+        chk = pit >= L && pit < aa_nit;
+      }   // past the last tile: the last chunk again, into a buffer nobody reads
+    };
+    V4Tile cur = tile_of(0);
+    if (h == 0 && lane == 0) *cnt = 0u;
+    issue_aa(0);
+    issue_bias(cur, 0);
+    issue_aa(1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // B0
+    int gch = 0;
+    int pend = 0, pr = 0;
+    const int nch = cur.c1 - cur.c0;
+    const int nslice = (nch - 1) < 3 ? (nch - 1) : 3;
+    const int srows = (8 + nslice - 1) / nslice;
+    const int cs = nch >= 3 ? 1 : 0;   // the AA share skips the part-0 drain chunk where it can
+    V4Tile dt = cur;
+    for (int it = 0; it < ntile; ++it) {
+      const bool more = it + 1 < ntile;
+      const V4Tile nxt = more ? tile_of(it + 1) : cur;
+      unsigned plo = 0u, phi = 0u;   // this tile's share of R(it + L)
+      if (it + L < aa_nit) aa_piece(aa_need(it + L - 1), aa_need(it + L), plo, phi);
+      for (int c = cur.c0; c < cur.c1; ++c) {
+        const bool first = c == cur.c0, lastc = c + 1 == cur.c1;
+        const int cc = c - cur.c0;
+        // the range tile it + 1's halo reads: every workgroup's share written? (the DMA of its
+        // first chunk goes out in this chunk; the wait's vmcnt(0) retires only what is due anyway)
+        if (chk && pc == pt.c0) {
+#ifdef CWDM_CONV_STAMPS
+          const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+          for (int n = 0; __hip_atomic_load(&g_v5aa_cnt[pit], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)G &&
+                          n < (1 << 24); ++n)
+            __builtin_amdgcn_s_sleep(1);
+          chk = false;
+#ifdef CWDM_CONV_STAMPS
+          if (p.stamps && tid == 256) p.stamps[(long long)blockIdx.x * 64 + 56] += __builtin_amdgcn_s_memtime() - t0;
+#endif
+        }
+        // the previous tile's AA share is retired in every helper (chunk 0's wait + barrier): publish it
+        if (cc == 1 && it > 0 && it - 1 + L < aa_nit && tid == 256)
+          __hip_atomic_fetch_add(&g_v5aa_cnt[it - 1 + L], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int d0 = 0, k0 = 0, k1 = 0;
+        if (pend == 2) {
+          drain(dt, 0, (gch + 2) % 3, 0, 8);
+          d0 = 1; k0 = 0; k1 = 8;
+          pend = 1; pr = 0;
+        } else if (pend == 1) {
+          k0 = pr; k1 = pr + srows < 8 ? pr + srows : 8;
+          drain(dt, 1, 0, k0, k1);
+          pr = k1;
+          if (pr == 8) pend = 0;
+        }
+        if (k1 > k0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // this chunk's AA loads (steps n0 .. n0 + AA - 1 of the share; none in the skipped chunk)
+        const int n0 = cc >= cs ? (cc - cs) * p.aa_units : -1;
+        // (compiler-invisible loads, as the MFMA waves' weights: an ordinary load's own wait would
+        // retire the halo DMA issued behind it -- LDS-DMA and loads mixed in vmcnt make the compiler
+        // wait for zero)
+        u32x4 ax[AA];
+        unsigned av[AA];
+        bool aok[AA];
+#pragma unroll
+        for (int a = 0; a < AA; ++a) {
+          av[a] = plo + (unsigned)((n0 + a) * al.vps + al.vo);
+          aok[a] = n0 >= 0 && a < p.aa_units && al.on && av[a] < phi;
+          v4_gload(ax[a], al.src + (size_t)(aok[a] ? av[a] : 0u) * al.rowb);
+        }
+        issue_aa((gch + 2) % 3);
+        // chunk k + 1's pieces and the AA loads (everything older than this chunk's DMA) retired
+        if constexpr (AA == 1) {
+          asm volatile("s_waitcnt vmcnt(%1)" : "+v"(ax[0]) : "n"(NA) : "memory");
+        } else if constexpr (AA == 2) {
+          asm volatile("s_waitcnt vmcnt(%2)" : "+v"(ax[0]), "+v"(ax[1]) : "n"(NA) : "memory");
+        } else if constexpr (AA == 4) {
+          asm volatile("s_waitcnt vmcnt(%4)" : "+v"(ax[0]), "+v"(ax[1]), "+v"(ax[2]), "+v"(ax[3]) : "n"(NA) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(%8)"
+                       : "+v"(ax[0]), "+v"(ax[1]), "+v"(ax[2]), "+v"(ax[3]), "+v"(ax[4]), "+v"(ax[5]), "+v"(ax[6]),
+                         "+v"(ax[7])
+                       : "n"(NA)
+                       : "memory");
+        }
+        if (p.aa_prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int a = 0; a < AA; ++a)
+          if (a < p.aa_units) aa_store(al, ax[a], av[a], aok[a]);
+        if (p.aa_prio) __builtin_amdgcn_s_setprio(0);
+        if (d0) drain_load(dt, 1);
+        if (k1 > k0) drain_put(dt, k0, k1);
+        // the finishing tile's part-0 residual rows, under its last chunk
+        if (lastc) drain_load(cur, 0);
+        if (first && more) issue_bias(nxt, (it + 1) & 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        V5_STAMP(34 + gch, tid == 256 && gch < 16);
+        __builtin_amdgcn_s_barrier();
+        if (lastc) {
+          __builtin_amdgcn_s_barrier();   // B2: the MFMA waves staged tile it
+          dt = cur;
+          pend = 2;
+        }
+        ++gch;
+      }
+      cur = nxt;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    drain(dt, 0, (gch + 2) % 3, 0, 8);
+    drain_put(dt, 0, 8);
+    drain_load(dt, 1);
+    drain(dt, 1, 0, 0, 8);
+    drain_put(dt, 0, 8);
+    V5_STAMP(52, tid == 256);
+    // the last workgroup out re-zeroes the sweep counters for the next launch
+    if (h == 0) {
+      unsigned old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(&g_v5aa_cnt[kV5AaCnt - 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (old == (unsigned)G - 1u) {
+        for (int r = lane; r < aa_nit; r += 64)
+          __hip_atomic_store(&g_v5aa_cnt[r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(&g_v5aa_cnt[kV5AaCnt - 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
 
   // prologue: chunk 0 and tile 0's bias, chunk 1; transform chunk 0
   V4Tile cur = tile_of(0);
@@ -396,30 +684,53 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();   // B0
   int gch = 0;
-  int pend = 0;                   // drain parts of dt still to run (2: both, 1: part 1)
+  int pend = 0;                   // drain parts of dt still to run (2: both, 1: part 1 from row pr)
+  int pr = 0;
+  // part 1 (the spare staging half, free until this tile's own hand-off) drains in S slices over the
+  // next tile's chunks 1 .. S: one whole part per chunk left the helpers behind the MFMA waves at
+  // every tile seam of the 4-chunk (64-input-channel) convs (r05 stamps: ~2k cycles per tile)
+  const int nslice = (cur.c1 - cur.c0 - 1) < 3 ? (cur.c1 - cur.c0 - 1) : 3;
+  const int srows = (8 + nslice - 1) / nslice;
   V4Tile dt = cur;
   for (int it = 0; it < ntile; ++it) {
     const bool more = it + 1 < ntile;
     const V4Tile nxt = more ? tile_of(it + 1) : cur;
     for (int c = cur.c0; c < cur.c1; ++c) {
       const bool first = c == cur.c0, lastc = c + 1 == cur.c1;
-      // the drain part runs first: its residual wait (the compiler's) then also retires chunk
+      // the drain slice runs first: its residual wait (the compiler's) then also retires chunk
       // k + 1's pieces, and part 0 frees this wave's blocks of the buffer chunk k + 2 goes to
-      const bool drained = pend > 0;
       // (part 0 is followed by part 1's residual loads: 8 stores + 8 loads in flight before the DMA)
       const bool d0 = pend == 2 && p.rmode >= 0;
-      if (pend == 2) { drain(dt, 0, (gch + 2) % 3); drain_load(dt, 1); pend = 1; }
-      else if (pend == 1) { drain(dt, 1, 0); pend = 0; }
-      if (drained) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      int nst = 0;   // stores of this chunk's drain slice
+      if (pend == 2) {
+        drain(dt, 0, (gch + 2) % 3, 0, 8);
+        drain_put(dt, 0, 8);
+        drain_load(dt, 1);
+        pend = 1; pr = 0; nst = 8;
+      } else if (pend == 1) {
+        const int k1 = pr + srows < 8 ? pr + srows : 8;
+        drain(dt, 1, 0, pr, k1);
+        drain_put(dt, pr, k1);
+        nst = k1 - pr; pr = k1;
+        if (pr == 8) pend = 0;
+      }
+      if (nst) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const bool iss = issue_next((gch + 2) % 3);
       if (!(lastc && !more)) {
         // chunk k + 1 (the rest of this tile, or the next tile's first chunk): own pieces landed?
+        // (everything issued after them: this slice's stores, part 1's residual loads, this DMA)
         if (d0) {
           if (iss) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + 16) : "memory");
           else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        } else if (drained) {
+        } else if (nst >= 8) {
           if (iss) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + 8) : "memory");
           else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else if (nst >= 4) {
+          if (iss) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + 4) : "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else if (nst >= 2) {
+          if (iss) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + 2) : "memory");
+          else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         } else {
           if (iss) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
           else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -444,9 +755,11 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   }
   // the last tile (the MFMA waves have left; its part-0 residual rows were loaded under its last chunk)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  drain(dt, 0, (gch + 2) % 3);
+  drain(dt, 0, (gch + 2) % 3, 0, 8);
+  drain_put(dt, 0, 8);
   drain_load(dt, 1);
-  drain(dt, 1, 0);
+  drain(dt, 1, 0, 0, 8);
+  drain_put(dt, 0, 8);
   V5_STAMP(52, tid == 256);
 }
 
@@ -791,6 +1104,8 @@ int v4_ksplit(const cwdm_conv3d_desc* d);
 extern std::atomic<int> g_conv_path;
 extern std::atomic<unsigned long long*> g_stamps;
 std::atomic<int> g_v5_grid{0};
+std::atomic<int> g_v5_aa{[] { const char* e = std::getenv("CWDM_V5_AA"); return e ? std::atoi(e) : 1; }()};
+std::atomic<int> g_v5_aa_launches{0};
 int64_t v4_items(const cwdm_conv3d_desc* d);
 bool gbwd_grid_ok(const cwdm_conv3d_desc* d);
 
@@ -852,8 +1167,56 @@ bool v5_eligible(const cwdm_conv3d_desc* d, bool gn) {
 
 // sources a0 (c0 channels; chunk-major if a0_cm) and a1 (c1, channels-last);
 // agn: [B][c0 + c1][2] GroupNorm scale / shift applied in LDS (null: none)
+// apply-ahead (conv3d_v5_kernel<.., AA>) for a GroupNorm'd conv input: the per-chunk share AA (1, 2, 4,
+// 8 steps of 256 lanes) its sweep needs, or 0 where it does not apply (env CWDM_V5_AA=0: never)
+int v5_aa_units(const cwdm_conv3d_desc* d, int* lead) {
+  const int mode = g_v5_aa.load(std::memory_order_relaxed);
+  if (!mode || !d->a_gn || d->B != 1 || d->a_mode != 0 || !dtype_half(d->dtype)) return 0;
+  const int C = d->a_c0 + d->a_c1;
+  if (d->a_c0 % 8 || d->a_c1 % 8 || C % 16 || C > 2048) return 0;
+  if (!v5_eligible(d, false)) return 0;
+  // the helpers' share per chunk fits beside the drain from 8 input chunks (r05 stamps: the
+  // 4-chunk 64-channel convs left them ~4k cycles behind the MFMA waves per chunk); env
+  // CWDM_V5_AA_MINCH (A/B knob)
+  static const int minch = [] { const char* e = std::getenv("CWDM_V5_AA_MINCH"); return e ? std::atoi(e) : 8; }();
+  if (mode == 1 && (d->a_c0 + d->a_c1) / 16 < minch) return 0;
+  const int64_t V = d->D * d->H * d->W;
+  if (V * C * 2 >= 0x7FFFF000LL) return 0;
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  const int cap = g_v5_grid.load(std::memory_order_relaxed);
+  const int tx = (int)((d->W + 31) / 32), ty = (int)(d->H / 4), tz = (int)(d->D / 4), nct = d->cout / 64;
+  const int64_t nblk = (int64_t)tx * ty * tz * nct;
+  const int G = (int)std::min<int64_t>(nblk, cap > 0 ? cap : ncu);
+  const int nit = (int)((nblk + G - 1) / G);
+  if (nit > kV5AaCnt - 2) return 0;
+  const int nch = C / 16;
+  const int L = nch >= 8 ? 2 : 3;
+  // the ranges of the first L iterations are a prologue nothing overlaps: worth it only where the
+  // sweep is long (r05: the 128^3 128-channel conv, 32 iterations, 1650 -> 1593 us; the 64^3
+  // ones, 4 iterations, all prologue, +3 %)
+  if (mode == 1 && nit < 16) return 0;
+  const int Q = C / 8, vps = 256 / Q;
+  if (vps < 1) return 0;
+  const int cs = nch >= 3 ? 1 : 0;
+  int64_t steps = 0;
+  for (int r = L; r < nit; ++r) {
+    const int64_t len = (int64_t)v5aa_need(r, G, (int)nblk, nct, tx, ty, (int)d->D, (int)d->H, (int)d->W) -
+                        v5aa_need(r - 1, G, (int)nblk, nct, tx, ty, (int)d->D, (int)d->H, (int)d->W);
+    steps = std::max<int64_t>(steps, ((len + G - 1) / G + vps - 1) / vps);
+  }
+  const int64_t per = std::max<int64_t>(1, (steps + (nch - cs) - 1) / (nch - cs));
+  if (per > 8) return 0;
+  if (lead) *lead = L;
+  return (int)per;
+}
+
 int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
-              const float* agn, const void* res, int rmode, hipStream_t s) {
+              const float* agn, const void* res, int rmode, hipStream_t s, const V5Aa* aa) {
   const int esz = dtype_size(d->dtype);
   const int ck = 32 / esz;
   const int64_t SV = d->a_mode == 1 ? d->D * d->H * d->W / 8 : d->D * d->H * d->W;
@@ -876,6 +1239,15 @@ int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   p.stats = d->stats;
   p.ksplit = 1; p.kper = p.nch;
   p.agn = agn;
+  if (aa) {
+    CWDM_REQUIRE(a0_cm && !agn && d->B == 1 && d->a_mode == 0, CWDM_E_INVALID, "conv3d_v5: apply-ahead arguments");
+    p.ax0 = aa->x0; p.axc0 = aa->c0; p.ax1 = aa->x1; p.axc1 = aa->c1;
+    p.agn = aa->gn;
+    p.aa_lead = aa->lead;
+    p.aa_units = aa->units;
+    static const int prio = [] { const char* e = std::getenv("CWDM_V5_AA_PRIO"); return e ? std::atoi(e) : 0; }();
+    p.aa_prio = prio;
+  }
 #ifdef CWDM_V5_DIAG
   static const int diag = [] { const char* e = std::getenv("CWDM_V5_DIAGMASK"); return e ? std::atoi(e) : 0; }();
   p.diag = diag;
@@ -911,6 +1283,16 @@ int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
       if (p.amode == 1) hipLaunchKernelGGL((conv3d_v5s_kernel<1, false>), grid, dim3(512), 0, s, p);
       else hipLaunchKernelGGL((conv3d_v5s_kernel<0, false>), grid, dim3(512), 0, s, p);
     }
+  } else if (aa) {
+    g_v5_aa_launches.fetch_add(1, std::memory_order_relaxed);
+    auto go_aa = [&](auto tag) {
+      using T = decltype(tag);
+      // (the instance's loads per chunk >= the share: 4 or 8)
+      if (aa->units <= 4) hipLaunchKernelGGL((conv3d_v5_kernel<T, 0, false, 4>), grid, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((conv3d_v5_kernel<T, 0, false, 8>), grid, dim3(512), 0, s, p);
+    };
+    if (d->dtype == CWDM_BF16) go_aa(bf16_t{});
+    else go_aa(f16_t{});
   } else if (d->dtype == CWDM_BF16) {
     go(bf16_t{});
   } else {
@@ -929,12 +1311,21 @@ template __global__ void conv3d_v5_kernel<f16_t, 0, true>(V4Params);
 template __global__ void conv3d_v5_kernel<f16_t, 1, true>(V4Params);
 template __global__ void conv3d_v5_kernel<f16_t, 0, false>(V4Params);
 template __global__ void conv3d_v5_kernel<f16_t, 1, false>(V4Params);
+template __global__ void conv3d_v5_kernel<bf16_t, 0, false, 4>(V4Params);
+template __global__ void conv3d_v5_kernel<bf16_t, 0, false, 8>(V4Params);
+template __global__ void conv3d_v5_kernel<f16_t, 0, false, 4>(V4Params);
+template __global__ void conv3d_v5_kernel<f16_t, 0, false, 8>(V4Params);
 template __global__ void conv3d_v5s_kernel<0, true>(V4Params);
 template __global__ void conv3d_v5s_kernel<1, true>(V4Params);
 template __global__ void conv3d_v5s_kernel<0, false>(V4Params);
 template __global__ void conv3d_v5s_kernel<1, false>(V4Params);
 
 }  // namespace cwdm
+
+extern "C" int cwdm_debug_v5_aa(int on) {
+  if (on < 0) return cwdm::g_v5_aa_launches.load(std::memory_order_relaxed);
+  return cwdm::g_v5_aa.exchange(on > 2 ? 2 : on);
+}
 
 extern "C" int cwdm_debug_v5_grid(int n) {
   CWDM_REQUIRE(n >= 0, CWDM_E_INVALID, "cwdm_debug_v5_grid: n >= 0");

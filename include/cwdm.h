@@ -366,6 +366,14 @@ int cwdm_conv3d_set_path(int path);
  * CU.  Returns the previous cap. */
 int cwdm_debug_v5_grid(int n);
 
+/* Diagnostics / tests only: the warp-specialised conv's apply-ahead GroupNorm
+ * (the conv writes the SiLU(GroupNorm) copy of its input itself, ahead of its
+ * tile sweep, instead of the cwdm_gn_apply pre-pass): 1 on where the input has
+ * >= 8 chunks of 16 channels (default; env CWDM_V5_AA=0 starts it off), 2 on
+ * for any eligible conv, 0 off; returns the previous setting.  -1: changes
+ * nothing, returns the number of apply-ahead launches so far. */
+int cwdm_debug_v5_aa(int on);
+
 /* Diagnostics / tests only: the fused GroupNorm finalize + pre-pass the plan
  * offers a small-level consumer conv (GnFinFuse): the finalize of
  * cwdm_gn_finalize (same arguments, scale_shift and mean_rstd both written)

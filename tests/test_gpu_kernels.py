@@ -519,6 +519,58 @@ def test_conv3d_v5_bitexact_vs_v4(case, dtype_name):
     assert rel_err(s5.cpu(), s4.cpu()) < {"bf16": 2e-3, "fp16": 3e-4}[dtype_name], name
 
 
+AA_CASES = [
+    # name, grid (D, H, W), c0, c1, cout, rmode, grid cap -- batch 1, GroupNorm'd input.  Capped grids
+    # whose sweep iterations cover whole z-rows of tiles: several ranges past the lead (2 for >= 8
+    # chunks, else 3), each transformed by every workgroup and waited on through its counter
+    ("aa_64_res_8wg", (32, 16, 64), 64, 0, 64, 0, 8),
+    ("aa_concat_c128_16wg", (32, 16, 64), 64, 64, 128, -1, 16),
+    ("aa_partial_x_res_8wg", (24, 16, 56), 64, 0, 64, 0, 8),
+    ("aa_c192_cout64_4wg", (16, 8, 64), 128, 64, 64, -1, 4),
+    # uncapped: one iteration past the prologue's ranges (or none)
+    ("aa_concat_uncapped", (32, 32, 128), 64, 32, 128, -1, 0),
+]
+
+
+@pytest.mark.parametrize("dtype_name", ["bf16", "fp16"])
+@pytest.mark.parametrize("case", AA_CASES, ids=lambda c: c[0])
+def test_conv3d_v5_apply_ahead_bitexact_vs_prepass(case, dtype_name):
+    """Apply-ahead (the warp-specialised conv writes the SiLU(GroupNorm) copy of
+    its input itself, range by range ahead of its tile sweep, synchronised by
+    per-range counters across workgroups) stores exactly what the cwdm_gn_apply
+    pre-pass + the same conv store, statistics included; run twice (the last
+    workgroup out re-zeroes the counters for the next launch)."""
+    from cwdm_hip._lib import lib
+    L = lib()
+    name, grid, c0, c1, cout, rmode, cap = case
+    dtype, tdt = _DTN[dtype_name]
+    g = torch.Generator().manual_seed(23)
+    D, H, W = grid
+    cin = c0 + c1
+    a0 = torch.randn(1, D, H, W, c0, generator=g).to(DEV, tdt)
+    a1 = torch.randn(1, D, H, W, c1, generator=g).to(DEV, tdt) if c1 else None
+    w = (torch.randn(cout, cin, 3, 3, 3, generator=g) / math.sqrt(27 * cin)).to(DEV)
+    bias = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    gn = torch.stack([1 + 0.2 * torch.randn(1, cin, generator=g), 0.2 * torch.randn(1, cin, generator=g)],
+                     -1).contiguous().to(DEV)
+    res = torch.randn(1, D, H, W, cout, generator=g).to(DEV, tdt) if rmode >= 0 else None
+    outs = {}
+    n0 = L.cwdm_debug_v5_aa(-1)
+    for aa in (0, 1, 1):
+        prev, prevg, preva = L.cwdm_conv3d_set_path(2), L.cwdm_debug_v5_grid(cap), L.cwdm_debug_v5_aa(2 * aa)
+        try:
+            outs.setdefault(aa, []).append(_conv_call(dtype, (1, D, H, W), a0, a1, 0, gn, w, bias, res=res, rmode=rmode))
+        finally:
+            L.cwdm_conv3d_set_path(prev)
+            L.cwdm_debug_v5_grid(prevg)
+            L.cwdm_debug_v5_aa(preva)
+    assert L.cwdm_debug_v5_aa(-1) - n0 == 2, f"{name}: the apply-ahead path did not run"
+    (o0, s0), = outs[0]
+    for o1, s1 in outs[1]:
+        assert torch.equal(o0.view(torch.int16), o1.view(torch.int16)), name
+        assert torch.equal(s0, s1), name
+
+
 SG_CASES = [
     # name, B, grid(out), c0, c1, cout, amode, gn, skip1x1, rmode  (16-bit; W < 32, cout % 64 == 0,
     # 32-channel K chunks: the small-grid kernel, conv3d_sg.hip, incl. its 1x1 skip mode and K split)

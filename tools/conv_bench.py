@@ -23,6 +23,7 @@ CASES = {
     "L0_64_64_gn_res": (128, 64, 0, 64, 0, True, 0, 0),
     "L0_64_64_gn_skip192": (128, 64, 0, 64, 0, True, 192, -1),
     "L0_128_128_up": (128, 128, 0, 128, 1, True, 0, -1),
+    "L0_128_128_gn": (128, 128, 0, 128, 0, True, 0, -1),
     "L0_192_64_cat": (128, 128, 64, 64, 0, True, 0, -1),
     "L0_64_8_out": (128, 64, 0, 8, 0, True, 0, -1),
     "L0_64_8_out_nogn": (128, 64, 0, 8, 0, False, 0, -1),

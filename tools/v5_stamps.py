@@ -31,6 +31,10 @@ def main():
     st = [r for r in buf.view(nwg, 64).cpu().tolist() if r[0] != 0]
     mean = lambda v: sum(v) / max(len(v), 1)  # noqa: E731
     print(f"{case}: {len(st)} workgroups; cycles, mean over workgroups (min / max)")
+    if all(r[55] for r in st):
+        print(f"  apply-ahead prologue (entry -> start) {mean([r[0] - r[55] for r in st]):8.0f}"
+              f" ({min(r[0] - r[55] for r in st)}/{max(r[0] - r[55] for r in st)});"
+              f" helper 0 waiting on range counters {mean([r[56] for r in st]):8.0f} ({max(r[56] for r in st)} max)")
     print(f"  prologue (start -> past B0)   {mean([r[1] - r[0] for r in st]):8.0f}")
     for k in range(16):
         if not all(r[2 + k] for r in st):
