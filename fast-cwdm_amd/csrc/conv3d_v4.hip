@@ -211,6 +211,8 @@ int sg_launch(const V4Params& v, const cwdm_conv3d_desc* d, void* partial, hipSt
 int64_t ksplit_slice_voxels(const cwdm_conv3d_desc* d);
 bool pw_eligible(const cwdm_conv3d_desc* d);
 int pw_forward(const cwdm_conv3d_desc* d, hipStream_t s);
+bool pw_split_eligible(const cwdm_conv3d_desc* d);
+int pw_split_forward(const cwdm_conv3d_desc* d, hipStream_t s);
 int sg_ksplit(const cwdm_conv3d_desc* d);
 int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, void* partial, hipStream_t s);
 int sg_skip_ksplit(const cwdm_conv3d_desc* d);
@@ -578,6 +580,8 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
       if ((rc = sg_skip_launch(&e, skip, ws, s))) return rc;   // ws: the K-split region, free until the conv
     } else if (pw_eligible(&e)) {
       if ((rc = pw_forward(&e, s))) return rc;
+    } else if (pw_split_eligible(&e)) {
+      if ((rc = pw_split_forward(&e, s))) return rc;
     } else if ((rc = legacy_conv3d_forward(&e, (cwdm_stream_t)s))) {
       return rc;
     }

@@ -276,6 +276,106 @@ __global__ void __launch_bounds__(256, NM == 2 ? 3 : 2) pw_kernel(PwParams p) {
   }
 }
 
+// The accurate fast mode's 1x1 skip (fp32 in / out, the conv3d_v5s split):
+// three bf16 MFMA passes per 16 K -- hi(x) hi(w) + lo(x) hi(w) + hi(x) lo(w),
+// lo = bf16(v - hi) -- with both operands split in registers (the weights from
+// their fp32 packing), 2^-16 relative per product.  The exact-fp32 brick kernel
+// it replaces ran the 128^3 skips at ~40 TF/s (1.0-1.3 ms each, 5 ms per
+// accurate-mode step).  Same tiling as pw_kernel: workgroup = 256 voxels x 32 NM
+// output channels, wave = 2 x 32 voxels; fp32 epilogue straight from the
+// accumulators (4 consecutive channels = 16 bytes per lane and row).
+template <int NM>
+__global__ void __launch_bounds__(256, 2) pw_split_kernel(PwParams p) {
+  constexpr int NC = 32 * NM;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const long long vt = blockIdx.x / p.nnb;
+  const int nb = blockIdx.x % p.nnb;
+  const long long row0 = vt * 256 + wv * 64;
+  const int n0 = nb * NC;
+  const int col = lane & 31, kg = lane >> 5;
+  const float* w = reinterpret_cast<const float*>(p.w);
+  f32x16 acc[2][NM];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[j][m][i] = 0.f;
+  // 8 consecutive K values of K step s: B = voxel row (row0 + 32 j + col), A = output channel
+  // n0 + 32 m + col (its two 4-channel quads of the fp32 packing)
+  auto ldB = [&](int s, int j, float4 (&f)[2]) {
+    const long long r = row0 + 32 * j + col;
+    const int k = 16 * s + 8 * kg;
+    if (r >= p.rows) { f[0] = f[1] = make_float4(0.f, 0.f, 0.f, 0.f); return; }
+    const float* src = k < p.K0 ? reinterpret_cast<const float*>(p.b0) + r * p.K0 + k
+                                : reinterpret_cast<const float*>(p.b1) + r * (p.K - p.K0) + (k - p.K0);
+    f[0] = *reinterpret_cast<const float4*>(src);
+    f[1] = *reinterpret_cast<const float4*>(src + 4);
+  };
+  auto ldA = [&](int s, int m, float4 (&f)[2]) {
+    const int co = n0 + 32 * m + col;
+    if (co >= p.N) { f[0] = f[1] = make_float4(0.f, 0.f, 0.f, 0.f); return; }
+    const int k = 16 * s + 8 * kg;
+    f[0] = *reinterpret_cast<const float4*>(w + pw_widx<float>(co, k, p.K, p.NT));
+    f[1] = *reinterpret_cast<const float4*>(w + pw_widx<float>(co, k + 4, p.K, p.NT));
+  };
+  auto split = [](const float4 (&f)[2], u32x4& hi, u32x4& lo) {
+    const float v[8] = {f[0].x, f[0].y, f[0].z, f[0].w, f[1].x, f[1].y, f[1].z, f[1].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      hi[e] = pack2<bf16_t>(v[2 * e], v[2 * e + 1]);
+      lo[e] = pack2<bf16_t>(v[2 * e] - lo2f<bf16_t>(hi[e]), v[2 * e + 1] - hi2f<bf16_t>(hi[e]));
+    }
+  };
+  const int ns = p.K / 16;
+  float4 fa[NM][2], fb[2][2];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) ldA(0, m, fa[m]);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) ldB(0, j, fb[j]);
+  for (int s = 0; s < ns; ++s) {
+    u32x4 ah[NM], al[NM], bh[2], bl[2];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) split(fa[m], ah[m], al[m]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) split(fb[j], bh[j], bl[j]);
+    if (s + 1 < ns) {
+#pragma unroll
+      for (int m = 0; m < NM; ++m) ldA(s + 1, m, fa[m]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) ldB(s + 1, j, fb[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        mfma_acc(acc[j][m], ah[m], bh[j], (bf16_t*)nullptr);
+        mfma_acc(acc[j][m], ah[m], bl[j], (bf16_t*)nullptr);
+        mfma_acc(acc[j][m], al[m], bh[j], (bf16_t*)nullptr);
+      }
+  }
+  // acc[j][m][4 g + e] = channel n0 + 32 m + 8 g + 4 kg + e of voxel row row0 + 32 j + col
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const long long r = row0 + 32 * j + col;
+    if (r >= p.rows) continue;
+    const long long bb = r / p.V;
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = n0 + 32 * m + 8 * g + 4 * kg;
+        if (c >= p.N) continue;
+        float4 v = make_float4(acc[j][m][4 * g], acc[j][m][4 * g + 1], acc[j][m][4 * g + 2], acc[j][m][4 * g + 3]);
+        if (p.bias) {
+          const float* bs = p.bias + bb * p.bias_bs + c;
+          v.x += bs[0]; v.y += bs[1]; v.z += bs[2]; v.w += bs[3];
+        }
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + r * p.N + c) = v;
+      }
+  }
+}
+
 }  // namespace
 
 // shapes the pointwise kernel takes: a pure 1x1 (segment B only), 16-bit, no
@@ -331,6 +431,39 @@ int pw_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     else if (ga) hipLaunchKernelGGL((pw_kernel<bf16_t, true, 4>), dim3((unsigned)nblk), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((pw_kernel<bf16_t, false, 4>), dim3((unsigned)nblk), dim3(256), 0, s, p);
   }
+  prof_end(s, 2.0 * p.rows * (double)p.N * p.K);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+// the accurate fast mode's pure 1x1 (a_w_split marks it: the split weights of
+// the conv this skip belongs to): fp32, no residual / statistics / second output
+bool pw_split_eligible(const cwdm_conv3d_desc* d) {
+  if (d->dtype != CWDM_F32 || !d->a_w_split || d->a_w || !d->b_w || d->res_mode >= 0 || d->stats ||
+      d->out_dtype != CWDM_F32 || d->out1 || d->accumulate)
+    return false;
+  const int K = d->b_c0 + d->b_c1;
+  return K % 16 == 0 && d->b_c0 % 16 == 0 && d->cout % 32 == 0 && d->B * d->D * d->H * d->W < (1LL << 40);
+}
+
+int pw_split_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
+  PwParams p{};
+  p.V = d->D * d->H * d->W;
+  p.rows = d->B * p.V;
+  p.K = d->b_c0 + d->b_c1; p.K0 = d->b_c0;
+  p.b0 = d->b0; p.b1 = d->b1;
+  p.w = reinterpret_cast<const unsigned char*>(d->b_w);
+  p.N = d->cout;
+  p.NT = 32 * pick_nf(d->cout);   // the fp32 packing's rows per channel tile
+  p.bias = d->bias; p.bias_bs = d->bias_bstride;
+  p.out = d->out;
+  const int nm = d->cout % 128 ? 2 : 4;
+  p.nnb = (int)ceil_div(d->cout, 32 * nm);
+  const long long nblk = ceil_div(p.rows, 256) * p.nnb;
+  CWDM_REQUIRE(nblk < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d (pointwise split): grid too large");
+  prof_begin(s);
+  if (nm == 2) hipLaunchKernelGGL((pw_split_kernel<2>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((pw_split_kernel<4>), dim3((unsigned)nblk), dim3(256), 0, s, p);
   prof_end(s, 2.0 * p.rows * (double)p.N * p.K);
   CWDM_LAUNCHED();
   return CWDM_OK;
