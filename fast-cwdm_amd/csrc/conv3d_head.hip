@@ -774,6 +774,80 @@ int head_sampler_forward(const cwdm_conv3d_desc* d, const cwdm_sampler_args* a, 
   return CWDM_OK;
 }
 
+// ---------------------------------------------------------------------------
+// The accurate fast mode's output head (fp32 storage): the head conv as a bf16
+// conv over a K-expanded input, x3 = [hi(y) | lo(y) | hi(y)] with y =
+// SiLU(GN(x)), lo = bf16(y - hi), against weights [hi(w) | hi(w) | lo(w)]
+// (head_split3_pack) -- the three products hi.hi + lo.hi + hi.lo of the split
+// conv kernels, summed by ONE bf16 head launch in fp32 accumulators.  The exact-
+// fp32 brick kernel it replaces ran the 64 -> 8 head at 128^3 in 2.2 ms.
+// ---------------------------------------------------------------------------
+namespace {
+// one thread per (voxel, 8-channel group) of the C-channel fp32 input
+__global__ void __launch_bounds__(256) head_split3_prep_kernel(const float* __restrict__ x, const float* __restrict__ gn,
+                                                               long long rows, long long V, int C,
+                                                               unsigned short* __restrict__ x3) {
+  const int Q = C / 8;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * Q) return;
+  const long long r = i / Q;
+  const int q = (int)(i - r * Q);
+  const long long b = r / V;
+  const float4 a0 = *reinterpret_cast<const float4*>(x + r * C + q * 8);
+  const float4 a1 = *reinterpret_cast<const float4*>(x + r * C + q * 8 + 4);
+  float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  const float* g = gn + (b * C + q * 8) * 2;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float sa, sb;
+    silu_aff_coef(g[2 * e], g[2 * e + 1], sa, sb);
+    v[e] = silu_aff(v[e], sa, sb);
+  }
+  u32x4 hi, lo;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hi[e] = pack2<bf16_t>(v[2 * e], v[2 * e + 1]);
+    lo[e] = pack2<bf16_t>(v[2 * e] - lo2f<bf16_t>(hi[e]), v[2 * e + 1] - hi2f<bf16_t>(hi[e]));
+  }
+  unsigned short* o = x3 + r * 3 * C + q * 8;
+  *reinterpret_cast<u32x4*>(o) = hi;
+  *reinterpret_cast<u32x4*>(o + C) = lo;
+  *reinterpret_cast<u32x4*>(o + 2 * C) = hi;
+}
+
+// w [cout][cin][27] fp32 -> w3 [cout][3 cin][27] fp32 = [hi(w) | hi(w) | lo(w)] (bf16-exact values)
+__global__ void head_split3_w_kernel(const float* __restrict__ w, int cout, int cin, float* __restrict__ w3) {
+  const long long n = (long long)cout * cin * 27;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long co = i / ((long long)cin * 27), rest = i - co * cin * 27;
+    const float v = w[i];
+    const float hi = lo2f<bf16_t>(pack2<bf16_t>(v, 0.f));
+    const float lo = lo2f<bf16_t>(pack2<bf16_t>(v - hi, 0.f));
+    float* o = w3 + co * 3 * cin * 27 + rest;
+    o[0] = hi;
+    o[(long long)cin * 27] = hi;
+    o[2LL * cin * 27] = lo;
+  }
+}
+}  // namespace
+
+int head_split3_prep(const float* x, const float* gn, int64_t B, int64_t V, int C, void* x3, hipStream_t s) {
+  CWDM_REQUIRE(x && gn && x3 && C % 8 == 0 && B > 0 && V > 0, CWDM_E_INVALID, "head_split3_prep: bad arguments");
+  const long long items = B * V * (C / 8);
+  hipLaunchKernelGGL(head_split3_prep_kernel, dim3((unsigned)ceil_div(items, 256)), dim3(256), 0, s, x, gn, (long long)B * V,
+                     (long long)V, C, reinterpret_cast<unsigned short*>(x3));
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
+// the K-expanded split weights of a head conv, packed bf16 at out (cwdm_conv3d_packed_bytes(cout, 3 cin,
+// 3, BF16) bytes); tmp: 3 cout cin 27 fp32 scratch
+int head_split3_pack(const float* w, int cout, int cin, float* tmp, void* out, hipStream_t s) {
+  hipLaunchKernelGGL(head_split3_w_kernel, dim3(64), dim3(256), 0, s, w, cout, cin, tmp);
+  CWDM_LAUNCHED();
+  return cwdm_conv3d_pack(tmp, cout, 3 * cin, 3, CWDM_BF16, out, (cwdm_stream_t)s);
+}
+
 }  // namespace cwdm
 
 extern "C" int cwdm_debug_head2(int mode) {

@@ -81,6 +81,8 @@ struct ConvStep {
   bool stats;
   int skip_conv = -1;           // conv1 of a block with a 1x1 skip: index of the block's conv2
   int64_t wsplit_off = -1;      // accurate fast mode: split-bf16 packed weights (cwdm_conv3d_pack_split), -1 none
+  int64_t hsplit_off = -1;      // accurate fast mode, output head: K-expanded bf16 weights [hi | hi | lo] (head_split3_pack)
+  int64_t hsplit_tmp = -1;      //   and their fp32 staging
   int s2 = 0;                   // stride-2 conv (Downsample.op) over a space-to-depth input: cin_a = 8 x its channels
 };
 
@@ -558,6 +560,11 @@ void build(cwdm_unet* u) {
     cs.w_off = take(cwdm_conv3d_packed_bytes(cs.cout, cs.cin_a, 3, c.dtype));
     if (c.mfma_split && c.dtype == CWDM_F32 && !cs.s2 && cs.cout % 64 == 0 && cs.cin_a % 16 == 0)
       cs.wsplit_off = take(cwdm_conv3d_packed_split_bytes(cs.cout, cs.cin_a));
+    if (c.mfma_split && c.dtype == CWDM_F32 && &cs == &u->convs[u->head_c] && cs.a1 < 0 && cs.amode == 0 &&
+        cs.gn >= 0 && cs.cout <= 16 && cs.cin_a % 32 == 0 && 3 * cs.cin_a <= 256) {
+      cs.hsplit_off = take(cwdm_conv3d_packed_bytes(cs.cout, 3 * cs.cin_a, 3, CWDM_BF16));
+      cs.hsplit_tmp = take((int64_t)3 * cs.cout * cs.cin_a * 27 * 4);
+    }
     if (cs.ws_p >= 0) cs.wsk_off = take(cwdm_conv3d_packed_bytes(cs.cout, cs.cin_b, 1, c.dtype));
     if (cs.bias_kind == 0) cs.bias_off = take((int64_t)cs.cout * 4);
   }
@@ -588,6 +595,8 @@ void build(cwdm_unet* u) {
 namespace cwdm {
 bool v4_eligible(const cwdm_conv3d_desc* d);
 bool v5_eligible(const cwdm_conv3d_desc* d, bool gn);
+int head_split3_prep(const float* x, const float* gn, int64_t B, int64_t V, int C, void* x3, hipStream_t s);
+int head_split3_pack(const float* w, int cout, int cin, float* tmp, void* out, hipStream_t s);
 bool apply_skip_ok(int dtype, int C, int cout, int64_t B, int64_t vpb);
 int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
                   const void* wskip, int cout, void* act, void* skip, hipStream_t s);
@@ -922,6 +931,12 @@ extern "C" int cwdm_unet_pack(const cwdm_unet* uc, const float* const* P, void* 
                              cs.wsb_p >= 0 ? P[cs.wsb_p] : nullptr, cs.cout, 0});
     }
   }
+  // the accurate fast mode's head weights: bf16, so packed now, outside the batch (which packs in the model's dtype)
+  for (const auto& cs : u->convs)
+    if (cs.hsplit_off >= 0 &&
+        (rc = cwdm::head_split3_pack(P[cs.w_p], cs.cout, cs.cin_a, reinterpret_cast<float*>(base + cs.hsplit_tmp),
+                                     base + cs.hsplit_off, s)))
+      return rc;
   for (const auto& g : u->gns) {
     cp(g.gamma_p, g.gamma_off);
     cp(g.beta_p, g.beta_off);
@@ -1127,10 +1142,24 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
         d.b0 = d.b1 = nullptr; d.b_c0 = d.b_c1 = 0; d.b_w = nullptr;
         d.res = wb + L.skipbuf; d.res_mode = 0;
       }
+      const int64_t x3_bytes = B * d.D * d.H * d.W * 3 * d.a_c0 * 2;
       if (samp && cs.out < 0 && cwdm::head_sampler_eligible(&d, samp)) {
         if ((rc = flush_fin())) return rc;
         if ((rc = cwdm::head_sampler_forward(&d, samp, s))) return rc;
         if (fused) *fused = 1;
+      } else if (cs.hsplit_off >= 0 && !keep && d.a_gn && x3_bytes <= L.split_bytes) {
+        // the accurate fast mode's head: a bf16 head over the K-expanded split input (head_split3_prep)
+        if ((rc = flush_fin())) return rc;
+        void* x3 = wb + L.split;
+        if ((rc = cwdm::head_split3_prep(reinterpret_cast<const float*>(d.a0), d.a_gn, B, d.D * d.H * d.W, d.a_c0, x3,
+                                          s)))
+          return rc;
+        cwdm_conv3d_desc e = d;
+        e.dtype = CWDM_BF16;
+        e.a0 = x3; e.a_c0 = 3 * d.a_c0; e.a1 = nullptr; e.a_c1 = 0;
+        e.a_gn = nullptr; e.a_w = pk + cs.hsplit_off; e.a_w_split = nullptr;
+        e.workspace = nullptr; e.ws_bytes = 0;
+        if ((rc = cwdm_conv3d_forward(&e, stream))) return rc;
       } else {
         cwdm::ActKeepScope ks(keep && L.keep_off[st.idx] >= 0 ? wb + L.keep_off[st.idx] : nullptr);
         cwdm::GnFinFuse ff{};
