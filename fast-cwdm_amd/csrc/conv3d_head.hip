@@ -816,18 +816,58 @@ __global__ void __launch_bounds__(256) head_split3_prep_kernel(const float* __re
 }
 
 // w [cout][cin][27] fp32 -> w3 [cout][3 cin][27] fp32 = [hi(w) | hi(w) | lo(w)] (bf16-exact values)
-__global__ void head_split3_w_kernel(const float* __restrict__ w, int cout, int cin, float* __restrict__ w3) {
-  const long long n = (long long)cout * cin * 27;
+__global__ void head_split3_w_kernel(const float* __restrict__ w, int cout, int cin, int taps, float* __restrict__ w3) {
+  const long long n = (long long)cout * cin * taps;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const long long co = i / ((long long)cin * 27), rest = i - co * cin * 27;
+    const long long co = i / ((long long)cin * taps), rest = i - co * cin * taps;
     const float v = w[i];
     const float hi = lo2f<bf16_t>(pack2<bf16_t>(v, 0.f));
     const float lo = lo2f<bf16_t>(pack2<bf16_t>(v - hi, 0.f));
-    float* o = w3 + co * 3 * cin * 27 + rest;
+    float* o = w3 + co * 3 * cin * taps + rest;
     o[0] = hi;
-    o[(long long)cin * 27] = hi;
-    o[2LL * cin * 27] = lo;
+    o[(long long)cin * taps] = hi;
+    o[2LL * cin * taps] = lo;
   }
+}
+// the small grids' version (conv3d_sg over a K-expanded input): two channels-last fp32 sources
+// (a concat), SiLU(GN) applied if gn is given, output chunk-major [B][3C / 16][V][16] bf16 (cm: the
+// 3x3x3 conv's source -- channel j of [hi | lo | hi] in chunk j / 16) or channels-last [B][V][3C]
+// (the 1x1 skip's)
+__global__ void __launch_bounds__(256) split3_cm_kernel(const float* __restrict__ x0, int c0,
+                                                        const float* __restrict__ x1, int c1,
+                                                        const float* __restrict__ gn, long long rows, long long V,
+                                                        int cm, unsigned short* __restrict__ x3) {
+  const int C = c0 + c1, Q = C / 8;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * Q) return;
+  const long long r = i / Q;
+  const int q = (int)(i - r * Q);
+  const long long b = r / V, v = r - b * V;
+  const bool first = 8 * q < c0;
+  const float* src = first ? x0 + r * c0 + 8 * q : x1 + r * c1 + (8 * q - c0);
+  const float4 a0 = *reinterpret_cast<const float4*>(src);
+  const float4 a1 = *reinterpret_cast<const float4*>(src + 4);
+  float y[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  if (gn) {   // (null: an input activated upstream, e.g. cwdm_gn_silu_pool's)
+    const float* g = gn + (b * C + 8 * q) * 2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float sa, sb;
+      silu_aff_coef(g[2 * e], g[2 * e + 1], sa, sb);
+      y[e] = silu_aff(y[e], sa, sb);
+    }
+  }
+  u32x4 hi, lo;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hi[e] = pack2<bf16_t>(y[2 * e], y[2 * e + 1]);
+    lo[e] = pack2<bf16_t>(y[2 * e] - lo2f<bf16_t>(hi[e]), y[2 * e + 1] - hi2f<bf16_t>(hi[e]));
+  }
+  const long long nk = 3 * C / 16;
+  auto at = [&](int j) { return cm ? x3 + ((b * nk + j / 16) * V + v) * 16 + (j % 16) : x3 + r * 3 * C + j; };
+  *reinterpret_cast<u32x4*>(at(8 * q)) = hi;
+  *reinterpret_cast<u32x4*>(at(C + 8 * q)) = lo;
+  *reinterpret_cast<u32x4*>(at(2 * C + 8 * q)) = hi;
 }
 }  // namespace
 
@@ -840,12 +880,23 @@ int head_split3_prep(const float* x, const float* gn, int64_t B, int64_t V, int 
   return CWDM_OK;
 }
 
+int split3_prep(const float* x0, int c0, const float* x1, int c1, const float* gn, int64_t B, int64_t V, int cm,
+                void* x3, hipStream_t s) {
+  CWDM_REQUIRE(x0 && x3 && (c1 == 0 || x1) && c0 % 8 == 0 && c1 % 8 == 0 && (c0 + c1) % 16 == 0 && B > 0 && V > 0,
+               CWDM_E_INVALID, "split3_prep: bad arguments");
+  const long long items = B * V * ((c0 + c1) / 8);
+  hipLaunchKernelGGL(split3_cm_kernel, dim3((unsigned)ceil_div(items, 256)), dim3(256), 0, s, x0, c0, x1, c1, gn,
+                     (long long)(B * V), (long long)V, cm, reinterpret_cast<unsigned short*>(x3));
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
+
 // the K-expanded split weights of a head conv, packed bf16 at out (cwdm_conv3d_packed_bytes(cout, 3 cin,
 // 3, BF16) bytes); tmp: 3 cout cin 27 fp32 scratch
-int head_split3_pack(const float* w, int cout, int cin, float* tmp, void* out, hipStream_t s) {
-  hipLaunchKernelGGL(head_split3_w_kernel, dim3(64), dim3(256), 0, s, w, cout, cin, tmp);
+int head_split3_pack(const float* w, int cout, int cin, float* tmp, void* out, hipStream_t s, int k) {
+  hipLaunchKernelGGL(head_split3_w_kernel, dim3(256), dim3(256), 0, s, w, cout, cin, k * k * k, tmp);
   CWDM_LAUNCHED();
-  return cwdm_conv3d_pack(tmp, cout, 3 * cin, 3, CWDM_BF16, out, (cwdm_stream_t)s);
+  return cwdm_conv3d_pack(tmp, cout, 3 * cin, k, CWDM_BF16, out, (cwdm_stream_t)s);
 }
 
 }  // namespace cwdm

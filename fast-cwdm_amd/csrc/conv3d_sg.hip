@@ -328,7 +328,9 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   bool inb[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) inb[m] = ox < p.W && (y0 + m * C::LPO + yl) < p.H && oz < p.D;
+  // out_f32 (the accurate fast mode's K-expanded split convs, sg_fp32x): fp32 output AND residual
   uint2 rq[4];
+  float4 rf[4];
   if (p.rmode >= 0) {
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -337,7 +339,11 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
       if (p.rmode == 1)
         rvox = (((long long)b * (p.D >> 1) + (oz >> 1)) * (p.H >> 1) + (oy >> 1)) * (p.W >> 1) + (ox >> 1);
       rq[m] = uint2{0u, 0u};
-      if (inb[m]) rq[m] = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(p.res) + rvox * p.cout + co);
+      rf[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (inb[m]) {
+        if (p.out_f32) rf[m] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.res) + rvox * p.cout + co);
+        else rq[m] = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(p.res) + rvox * p.cout + co);
+      }
     }
   }
 #pragma unroll
@@ -348,8 +354,12 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = acc[m][i];
     if (p.rmode >= 0) {
-      v[0] += lo2f<T>(rq[m].x); v[1] += hi2f<T>(rq[m].x);
-      v[2] += lo2f<T>(rq[m].y); v[3] += hi2f<T>(rq[m].y);
+      if (p.out_f32) {
+        v[0] += rf[m].x; v[1] += rf[m].y; v[2] += rf[m].z; v[3] += rf[m].w;
+      } else {
+        v[0] += lo2f<T>(rq[m].x); v[1] += hi2f<T>(rq[m].x);
+        v[2] += lo2f<T>(rq[m].y); v[3] += hi2f<T>(rq[m].y);
+      }
     }
     if (inb[m]) {
 #pragma unroll
@@ -357,10 +367,14 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
         ssum[i] += v[i];
         ssq[i] += v[i] * v[i];
       }
-      uint2 sq;
-      sq.x = pack2<T>(v[0], v[1]);
-      sq.y = pack2<T>(v[2], v[3]);
-      *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.out) + vox * p.cout + co) = sq;
+      if (p.out_f32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + vox * p.cout + co) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 sq;
+        sq.x = pack2<T>(v[0], v[1]);
+        sq.y = pack2<T>(v[2], v[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<T*>(p.out) + vox * p.cout + co) = sq;
+      }
     }
   }
   if (p.stats) {
@@ -413,11 +427,15 @@ template __global__ void conv3d_sg_kernel<f16_t, 8, 8, 1, 27>(SGParams);
 template __global__ void conv3d_sg_kernel<f16_t, 8, 8, 0, 1>(SGParams);
 
 extern std::atomic<int> g_conv_path;
+// set by the U-Net plan around the accurate fast mode's K-expanded small-grid convs: a 16-bit conv
+// with fp32 output takes this kernel, its residual fp32 too (SgFp32xScope)
+thread_local bool g_sg_fp32x = false;
 
 namespace {
 bool sg_shape_ok(const cwdm_conv3d_desc* d) {
   if (g_conv_path.load(std::memory_order_relaxed) == 1) return false;
-  if (!dtype_half(d->dtype) || d->out_dtype != d->dtype || d->accumulate || d->out1 || d->cout % 64) return false;
+  if (!dtype_half(d->dtype) || d->accumulate || d->out1 || d->cout % 64) return false;
+  if (d->out_dtype != d->dtype && !(d->out_dtype == CWDM_F32 && g_sg_fp32x)) return false;
   // W < kWideMinW (the wide kernels take the rest): 16 x 4 x 4 bricks for W >= 16,
   // 8 x 8 x 4 below (pick_brick's statistics bricks), the last brick of an axis partial
   return d->W >= 1 && d->W < kWideMinW && d->H >= 1 && d->D >= 1;
@@ -570,6 +588,7 @@ int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, void* partial, hipStrea
   p.aw = reinterpret_cast<const unsigned char*>(d->b_w);
   p.bias = nullptr; p.res = nullptr; p.rmode = -1;
   p.out = out; p.stats = nullptr;
+  p.out_f32 = (d->out_dtype == CWDM_F32) ? 1 : 0;   // (the accurate fast mode's K-expanded skip, sg_shape_ok)
   q.ntile16 = d->cout / 16;
   const SgGeom gm = sg_geom(d);
   q.parts = (int)gm.parts();

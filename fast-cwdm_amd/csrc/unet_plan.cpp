@@ -82,7 +82,8 @@ struct ConvStep {
   int skip_conv = -1;           // conv1 of a block with a 1x1 skip: index of the block's conv2
   int64_t wsplit_off = -1;      // accurate fast mode: split-bf16 packed weights (cwdm_conv3d_pack_split), -1 none
   int64_t hsplit_off = -1;      // accurate fast mode, output head: K-expanded bf16 weights [hi | hi | lo] (head_split3_pack)
-  int64_t hsplit_tmp = -1;      //   and their fp32 staging
+  int64_t xsplit_off = -1;      // accurate fast mode, small grids (level >= 2): the same for the bf16 small-grid kernel
+  int64_t xsplit_sk_off = -1;   //   and for its 1x1 skip (k = 1)
   int s2 = 0;                   // stride-2 conv (Downsample.op) over a space-to-depth input: cin_a = 8 x its channels
 };
 
@@ -165,6 +166,7 @@ struct cwdm_unet {
   std::vector<char> ginit;        // backward: gradient buffer of tensor written yet
   int64_t off_te_w1, off_te_b1, off_te_w2, off_te_b2, off_emb_w, off_emb_b;
   int64_t packed_bytes = 0;
+  int64_t split3_tmp = -1;      // fp32 staging of head_split3_pack (one region, the packs run in stream order)
   // profiling
   bool profiling = false;
   std::vector<hipEvent_t> ev;
@@ -556,6 +558,7 @@ void build(cwdm_unet* u) {
   u->off_te_b2 = take(u->params[u->te_b2].numel() * 4);
   u->off_emb_w = take((int64_t)u->R * E * 4);
   u->off_emb_b = take((int64_t)u->R * 4);
+  int64_t split3_max = 0;
   for (auto& cs : u->convs) {
     cs.w_off = take(cwdm_conv3d_packed_bytes(cs.cout, cs.cin_a, 3, c.dtype));
     if (c.mfma_split && c.dtype == CWDM_F32 && !cs.s2 && cs.cout % 64 == 0 && cs.cin_a % 16 == 0)
@@ -563,7 +566,18 @@ void build(cwdm_unet* u) {
     if (c.mfma_split && c.dtype == CWDM_F32 && &cs == &u->convs[u->head_c] && cs.a1 < 0 && cs.amode == 0 &&
         cs.gn >= 0 && cs.cout <= 16 && cs.cin_a % 32 == 0 && 3 * cs.cin_a <= 256) {
       cs.hsplit_off = take(cwdm_conv3d_packed_bytes(cs.cout, 3 * cs.cin_a, 3, CWDM_BF16));
-      cs.hsplit_tmp = take((int64_t)3 * cs.cout * cs.cin_a * 27 * 4);
+      split3_max = std::max(split3_max, (int64_t)3 * cs.cout * cs.cin_a * 27 * 4);
+    }
+    // the small grids' K-expanded split convs (unet_forward_impl, xsg_plan): every 3x3x3 conv
+    // that can land on a grid below the wide kernels' minimum width
+    if (c.mfma_split && c.dtype == CWDM_F32 && !cs.s2 && cs.level >= 2 && cs.amode <= 1 &&
+        cs.cout % 64 == 0 && cs.cin_a % 32 == 0) {
+      cs.xsplit_off = take(cwdm_conv3d_packed_bytes(cs.cout, 3 * cs.cin_a, 3, CWDM_BF16));
+      split3_max = std::max(split3_max, (int64_t)3 * cs.cout * cs.cin_a * 27 * 4);
+      if (cs.ws_p >= 0 && cs.cin_b % 32 == 0) {
+        cs.xsplit_sk_off = take(cwdm_conv3d_packed_bytes(cs.cout, 3 * cs.cin_b, 1, CWDM_BF16));
+        split3_max = std::max(split3_max, (int64_t)3 * cs.cout * cs.cin_b * 4);
+      }
     }
     if (cs.ws_p >= 0) cs.wsk_off = take(cwdm_conv3d_packed_bytes(cs.cout, cs.cin_b, 1, c.dtype));
     if (cs.bias_kind == 0) cs.bias_off = take((int64_t)cs.cout * 4);
@@ -572,6 +586,7 @@ void build(cwdm_unet* u) {
     gs.gamma_off = take((int64_t)gs.channels * 4);
     gs.beta_off = take((int64_t)gs.channels * 4);
   }
+  if (split3_max > 0) u->split3_tmp = take(split3_max);
   u->packed_bytes = off;
 
   // flat gradient layout (state_dict order, contiguous)
@@ -596,7 +611,18 @@ namespace cwdm {
 bool v4_eligible(const cwdm_conv3d_desc* d);
 bool v5_eligible(const cwdm_conv3d_desc* d, bool gn);
 int head_split3_prep(const float* x, const float* gn, int64_t B, int64_t V, int C, void* x3, hipStream_t s);
-int head_split3_pack(const float* w, int cout, int cin, float* tmp, void* out, hipStream_t s);
+int head_split3_pack(const float* w, int cout, int cin, float* tmp, void* out, hipStream_t s, int k);
+int split3_prep(const float* x0, int c0, const float* x1, int c1, const float* gn, int64_t B, int64_t V, int cm,
+                void* x3, hipStream_t s);
+bool sg_skip_eligible(const cwdm_conv3d_desc* d);
+int sg_skip_ksplit(const cwdm_conv3d_desc* d);
+int sg_skip_launch(const cwdm_conv3d_desc* d, void* out, void* partial, hipStream_t s);
+bool sg_eligible(const cwdm_conv3d_desc* d);
+int sg_ksplit(const cwdm_conv3d_desc* d);
+int64_t ksplit_slice_voxels(const cwdm_conv3d_desc* d);
+extern thread_local bool g_sg_fp32x;
+bool pw_split_eligible(const cwdm_conv3d_desc* d);
+int pw_split_forward(const cwdm_conv3d_desc* d, hipStream_t s);
 bool apply_skip_ok(int dtype, int C, int cout, int64_t B, int64_t vpb);
 int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
                   const void* wskip, int cout, void* act, void* skip, hipStream_t s);
@@ -626,6 +652,11 @@ namespace {
 struct SgSyncScope {
   SgSyncScope(void* block) { cwdm::g_sg_sync = reinterpret_cast<unsigned*>(block); }
   ~SgSyncScope() { cwdm::g_sg_sync = nullptr; }
+};
+// the small-grid kernel's fp32 output / residual, for the K-expanded split convs only
+struct SgFp32xScope {
+  SgFp32xScope() { cwdm::g_sg_fp32x = true; }
+  ~SgFp32xScope() { cwdm::g_sg_fp32x = false; }
 };
 }  // namespace
 namespace {
@@ -668,6 +699,59 @@ cwdm_conv3d_desc conv_shape(const cwdm_unet* u, const ConvStep& cs, int64_t B, i
   return d;
 }
 
+// the accurate fast mode on a small grid: the fp32 conv d (GroupNorm+SiLU'd or plain input, optional 1x1
+// skip) as ONE bf16 small-grid conv over the K-expanded split input [hi | lo | hi] of SiLU(GN(x))
+// (cwdm::split3_prep, chunk-major) against the weights [hi | hi | lo] (cs.xsplit_off): the three
+// products hi.hi + lo.hi + hi.lo of the split kernels, fp32 output and residual.  The 1x1 skip,
+// if any, runs first into an fp32 residual buffer: the same K expansion on the small-grid kernel's
+// 1x1 form (channels-last split of the raw input, cs.xsplit_sk_off), else pw_split.
+// Workspace: x3 (the conv's or the skip's split input) | skip | K-split slices.
+struct XsgPlan {
+  bool ok = false;
+  bool sk_sg = false;     // the skip on the small-grid kernel
+  cwdm_conv3d_desc e{};   // the bf16 desc (pointers filled in by the forward)
+  cwdm_conv3d_desc ek{};  //   and the skip's
+  int64_t x3_bytes = 0, skip_bytes = 0, total = 0;
+};
+XsgPlan xsg_plan(const cwdm_unet* u, const ConvStep& cs, const cwdm_conv3d_desc& d) {
+  XsgPlan x;
+  if (cs.xsplit_off < 0 || d.res_mode > 1 || (d.b_w && d.res_mode >= 0)) return x;
+  const int64_t sv = cs.amode == 1 ? (d.D / 2) * (d.H / 2) * (d.W / 2) : d.D * d.H * d.W;
+  const int C = d.a_c0 + d.a_c1;
+  cwdm_conv3d_desc e = d;
+  e.dtype = CWDM_BF16;
+  e.a_c0 = 3 * C; e.a_c1 = 0; e.a_gn = nullptr; e.a_w_split = nullptr;
+  e.b_c0 = e.b_c1 = 0; e.b_w = nullptr;
+  if (d.b_w) e.res_mode = 0;
+  e.out_dtype = CWDM_F32;
+  SgFp32xScope fx;
+  if (!cwdm::sg_eligible(&e)) return x;
+  x.e = e;
+  x.x3_bytes = align_up(d.B * sv * 3 * C * 2);
+  x.skip_bytes = d.b_w ? align_up(d.B * d.D * d.H * d.W * d.cout * 4) : 0;
+  const int S = cwdm::sg_ksplit(&e);
+  int64_t part = S > 1 ? (int64_t)S * d.B * cwdm::ksplit_slice_voxels(&e) * d.cout * 4 : 0;
+  if (d.b_w && cs.xsplit_sk_off >= 0) {
+    cwdm_conv3d_desc k = d;
+    k.dtype = CWDM_BF16;
+    k.a0 = k.a1 = nullptr; k.a_c0 = k.a_c1 = 0; k.a_gn = nullptr; k.a_w = nullptr; k.a_w_split = nullptr; k.a_mode = 0;
+    k.b_c0 = 3 * (d.b_c0 + d.b_c1); k.b_c1 = 0; k.b1 = nullptr;
+    k.bias = nullptr; k.bias_bstride = 0; k.stats = nullptr; k.res = nullptr; k.res_mode = -1;
+    k.out_dtype = CWDM_F32;
+    if (cwdm::sg_skip_eligible(&k)) {
+      x.sk_sg = true;
+      x.ek = k;
+      x.x3_bytes = std::max(x.x3_bytes, align_up(d.B * d.D * d.H * d.W * k.b_c0 * 2));
+      const int Sk = cwdm::sg_skip_ksplit(&k);
+      if (Sk > 1) part = std::max(part, (int64_t)Sk * d.B * cwdm::ksplit_slice_voxels(&k) * d.cout * 4);
+    }
+  }
+  x.total = x.x3_bytes + x.skip_bytes + part;
+  (void)u;
+  x.ok = true;
+  return x;
+}
+
 Layout layout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
   Layout L;
   int64_t off = 0;
@@ -698,6 +782,8 @@ Layout layout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
     cwdm_conv3d_desc d = conv_shape(u, cs, B, D, H, W);
     const int64_t n = cwdm_conv3d_workspace_bytes(&d);
     if (n > split) split = n;
+    const XsgPlan xp = xsg_plan(u, cs, d);
+    if (xp.ok && xp.total > split) split = xp.total;
   }
   L.split_bytes = split;
   L.split = take(split);
@@ -931,12 +1017,16 @@ extern "C" int cwdm_unet_pack(const cwdm_unet* uc, const float* const* P, void* 
                              cs.wsb_p >= 0 ? P[cs.wsb_p] : nullptr, cs.cout, 0});
     }
   }
-  // the accurate fast mode's head weights: bf16, so packed now, outside the batch (which packs in the model's dtype)
-  for (const auto& cs : u->convs)
-    if (cs.hsplit_off >= 0 &&
-        (rc = cwdm::head_split3_pack(P[cs.w_p], cs.cout, cs.cin_a, reinterpret_cast<float*>(base + cs.hsplit_tmp),
-                                     base + cs.hsplit_off, s)))
+  // the accurate fast mode's K-expanded weights (head, small grids): bf16, so packed now, outside the
+  // batch (which packs in the model's dtype)
+  for (const auto& cs : u->convs) {
+    float* tmp = reinterpret_cast<float*>(base + u->split3_tmp);
+    for (const int64_t o : {cs.hsplit_off, cs.xsplit_off})
+      if (o >= 0 && (rc = cwdm::head_split3_pack(P[cs.w_p], cs.cout, cs.cin_a, tmp, base + o, s, 3))) return rc;
+    if (cs.xsplit_sk_off >= 0 &&
+        (rc = cwdm::head_split3_pack(P[cs.ws_p], cs.cout, cs.cin_b, tmp, base + cs.xsplit_sk_off, s, 1)))
       return rc;
+  }
   for (const auto& g : u->gns) {
     cp(g.gamma_p, g.gamma_off);
     cp(g.beta_p, g.beta_off);
@@ -1160,6 +1250,47 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
         e.a_gn = nullptr; e.a_w = pk + cs.hsplit_off; e.a_w_split = nullptr;
         e.workspace = nullptr; e.ws_bytes = 0;
         if ((rc = cwdm_conv3d_forward(&e, stream))) return rc;
+      } else if (XsgPlan xp = keep ? XsgPlan{} : xsg_plan(u, cs, d); xp.ok && xp.total <= L.split_bytes) {
+        // the accurate fast mode on a small grid: one bf16 small-grid conv over the K-expanded split input
+        if ((rc = flush_fin())) return rc;
+        unsigned char* x3 = wb + L.split;
+        const void* res = d.res;
+        int rmode = d.res_mode;
+        SgFp32xScope fx;
+        void* part = x3 + xp.x3_bytes + xp.skip_bytes;
+        if (d.b_w && xp.sk_sg) {
+          // the 1x1 skip first, into an fp32 residual: K-expanded split of the raw input on the small-grid kernel
+          if ((rc = cwdm::split3_prep(reinterpret_cast<const float*>(d.b0), d.b_c0, reinterpret_cast<const float*>(d.b1),
+                                      d.b_c1, nullptr, B, d.D * d.H * d.W, 0, x3, s)))
+            return rc;
+          cwdm_conv3d_desc k = xp.ek;
+          k.b0 = x3; k.b_w = pk + cs.xsplit_sk_off;
+          if ((rc = cwdm::sg_skip_launch(&k, x3 + xp.x3_bytes, cwdm::sg_skip_ksplit(&k) > 1 ? part : nullptr, s)))
+            return rc;
+          res = x3 + xp.x3_bytes; rmode = 0;
+        } else if (d.b_w) {
+          // the 1x1 skip first, into an fp32 residual (pw_split: the split products of the 1x1 weights)
+          cwdm_conv3d_desc k = d;
+          k.a0 = k.a1 = nullptr; k.a_c0 = k.a_c1 = 0; k.a_gn = nullptr; k.a_w = nullptr; k.a_mode = 0;
+          k.bias = nullptr; k.bias_bstride = 0; k.stats = nullptr; k.res = nullptr; k.res_mode = -1;
+          k.out = x3 + xp.x3_bytes; k.out_dtype = CWDM_F32;
+          k.workspace = nullptr; k.ws_bytes = 0;
+          if ((rc = cwdm::pw_split_eligible(&k) ? cwdm::pw_split_forward(&k, s) : cwdm_conv3d_forward(&k, stream)))
+            return rc;
+          res = k.out; rmode = 0;
+        }
+        const int64_t sv = cs.amode == 1 ? (d.D / 2) * (d.H / 2) * (d.W / 2) : d.D * d.H * d.W;
+        if ((rc = cwdm::split3_prep(reinterpret_cast<const float*>(d.a0), d.a_c0, reinterpret_cast<const float*>(d.a1),
+                                    d.a_c1, d.a_gn, B, sv, 1, x3, s)))
+          return rc;
+        cwdm_conv3d_desc e = xp.e;
+        e.a0 = x3; e.a1 = nullptr; e.a_w = pk + cs.xsplit_off;
+        e.bias = d.bias; e.bias_bstride = d.bias_bstride;
+        e.res = res; e.res_mode = rmode;
+        e.out = d.out; e.stats = d.stats;
+        e.workspace = nullptr; e.ws_bytes = 0;
+        if ((rc = cwdm::v4_launch(&e, x3, e.a_c0, nullptr, 0, 1, res, rmode, cwdm::sg_ksplit(&e) > 1 ? part : nullptr, s)))
+          return rc;
       } else {
         cwdm::ActKeepScope ks(keep && L.keep_off[st.idx] >= 0 ? wb + L.keep_off[st.idx] : nullptr);
         cwdm::GnFinFuse ff{};

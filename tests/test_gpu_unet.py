@@ -93,9 +93,11 @@ def test_production_unet_forward_dma_kernel(grid):
 
 @pytest.mark.parametrize("grid", [(16, 16, 32), (32, 32, 64)])
 def test_production_unet_accurate_fast_mode_vs_oracle(grid):
-    """compute_dtype "fp32x" (fp32 storage, the wide-grid conv MFMAs on bf16
-    hi/lo splits, conv3d_v5s_kernel): the 81.5 M production U-Net within the
-    north star's 1e-3 of the oracle, and within 2e-5 of the exact-fp32 plan."""
+    """compute_dtype "fp32x" (fp32 storage, every 3x3x3 conv's MFMAs on bf16 hi/lo
+    splits: conv3d_v5s_kernel on the wide grids, the K-expanded small-grid kernel
+    below them, the K-expanded head): the 81.5 M production U-Net within the north
+    star's 1e-3 of the oracle, and within 4e-5 of the exact-fp32 plan (the three
+    products drop lo.lo, ~2^-16 of each product: 2.04e-5 measured at 32x32x64)."""
     P = ou.random_params(seed=14)
     cfg = dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4))
     g = torch.Generator().manual_seed(9)
@@ -107,7 +109,7 @@ def test_production_unet_accurate_fast_mode_vs_oracle(grid):
         ref = ou.unet_forward(P, x, t)
         assert rel_err(out, ref) < 1e-3
         m32 = _product_model(cfg, 32, P, "fp32")
-        assert rel_err(out, m32(x.to(DEV), t.to(DEV))) < 2e-5
+        assert rel_err(out, m32(x.to(DEV), t.to(DEV))) < 4e-5
 
 
 @pytest.mark.parametrize("half,tol", [("bf16", 6e-2), ("fp16", 1e-2)])
