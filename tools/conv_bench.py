@@ -116,7 +116,7 @@ def main():
     args = ap.parse_args()
     dt = _lib.CWDM_BF16 if args.dtype == "bf16" else _lib.CWDM_F32
     for name, spec in CASES.items():
-        if args.only and args.only not in name:
+        if args.only and not any(o == name for o in args.only.split(",")) and args.only not in name:
             continue
         run_case(name, spec, args.iters, dt)
 
