@@ -350,6 +350,9 @@ struct WgDmaParams {
   const unsigned char* act; long long act_bs;  // per-batch bytes of U (cin * SV * esz)
   const unsigned char* dy; long long dy_bs;    // per-batch bytes of dY (V * dy_cs * esz)
   float* part;                 // [S][cout][cin][27] partial slabs (dw's OIDHW order), one per brick range
+#ifdef CWDM_WG_DIAG
+  int diag;                    // timing-only decomposition (make WGDIAG=1, env CWDM_WG_DIAGMASK): 1 no MFMA loop, 2 no DMA
+#endif
 };
 
 // One LDS-DMA of 16 B per lane (lane l -> lds + 16 l), issued by inline asm so
@@ -521,13 +524,18 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
   };
 
   const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)smem;
-  if (bb < be) issue(lds0);
+#ifdef CWDM_WG_DIAG
+  const bool no_mfma = p.diag & 1, no_dma = p.diag & 2;
+#else
+  constexpr bool no_mfma = false, no_dma = false;
+#endif
+  if (bb < be && !no_dma) issue(lds0);
   for (long long bi = bb; bi < be; ++bi) {
     unsigned char* cur = smem + ((bi - bb) & 1) * BUF;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this brick's DMA (issued one brick ago) landed
     __syncthreads();                                  // ... for every wave; the other stage is free
-    if (bi + 1 < be) issue(lds0 + (unsigned)(((bi - bb + 1) & 1) * BUF));   // brick bi + 1
-    wg_brick_mfma<T, MC, 27>(cur, cur + C::DY_OFF, acc, toff, ntap, wv, lane);
+    if (bi + 1 < be && !no_dma) issue(lds0 + (unsigned)(((bi - bb + 1) & 1) * BUF));   // brick bi + 1
+    if (!no_mfma) wg_brick_mfma<T, MC, 27>(cur, cur + C::DY_OFF, acc, toff, ntap, wv, lane);
   }
   // the partial tile -> the brick range's slab in dw's OIDHW order: per 32-channel
   // half m of the tile the four waves' taps meet in LDS as [co 32][ci 32][tap 27]
@@ -891,6 +899,10 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
     q.tx = p.tx; q.ty = p.ty; q.tz = p.tz; q.nbricks = p.nbricks; q.per = p.per; q.nco = p.nco;
     q.cin = cin; q.cout = d->cout; q.dy_cs = d->dy_cs;
     q.units = (int)(S * tiles); q.upx = (q.units + 7) / 8;
+#ifdef CWDM_WG_DIAG
+    static const int wg_diag = [] { const char* e = std::getenv("CWDM_WG_DIAGMASK"); return e ? std::atoi(e) : 0; }();
+    q.diag = wg_diag;
+#endif
     const long long sv = (long long)q.SD * q.SH * q.SW, V = d->D * d->H * d->W;
     q.act = reinterpret_cast<const unsigned char*>(d->u0); q.act_bs = sv * cin * 2;
     q.dy = reinterpret_cast<const unsigned char*>(d->dy); q.dy_bs = V * d->dy_cs * 2;
