@@ -351,7 +351,7 @@ struct WgDmaParams {
   const unsigned char* dy; long long dy_bs;    // per-batch bytes of dY (V * dy_cs * esz)
   float* part;                 // [S][cout][cin][27] partial slabs (dw's OIDHW order), one per brick range
 #ifdef CWDM_WG_DIAG
-  int diag;                    // timing-only decomposition (make WGDIAG=1, env CWDM_WG_DIAGMASK): 1 no MFMA loop, 2 no DMA
+  int diag;                    // timing-only decomposition (make WGDIAG=1, env CWDM_WG_DIAGMASK): 1 no MFMA loop, 2 no DMA after the first two bricks
 #endif
 };
 
@@ -529,12 +529,13 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
 #else
   constexpr bool no_mfma = false, no_dma = false;
 #endif
-  if (bb < be && !no_dma) issue(lds0);
+  // (no_dma: both stages are filled once, so the MFMAs run on real data -- their clock depends on it)
+  if (bb < be) issue(lds0);
   for (long long bi = bb; bi < be; ++bi) {
     unsigned char* cur = smem + ((bi - bb) & 1) * BUF;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this brick's DMA (issued one brick ago) landed
     __syncthreads();                                  // ... for every wave; the other stage is free
-    if (bi + 1 < be && !no_dma) issue(lds0 + (unsigned)(((bi - bb + 1) & 1) * BUF));   // brick bi + 1
+    if (bi + 1 < be && (!no_dma || bi == bb)) issue(lds0 + (unsigned)(((bi - bb + 1) & 1) * BUF));   // brick bi + 1
     if (!no_mfma) wg_brick_mfma<T, MC, 27>(cur, cur + C::DY_OFF, acc, toff, ntap, wv, lane);
   }
   // the partial tile -> the brick range's slab in dw's OIDHW order: per 32-channel
