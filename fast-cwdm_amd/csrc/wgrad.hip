@@ -869,7 +869,12 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
   p.part = reinterpret_cast<float*>(d->workspace);
   p.tx = (int)ceil_div(d->W, WBX); p.ty = (int)ceil_div(d->H, WBY); p.tz = (int)ceil_div(d->D, WBZ);
   p.nbricks = d->B * (long long)p.tx * p.ty * p.tz;
+#ifdef CWDM_WG_DIAG
+  static const bool force_mc1 = [] { const char* e = std::getenv("CWDM_WG_MC1"); return e && e[0] == '1'; }();
+  const int mc = (d->cout > 32 && !(force_mc1 && d->u_cm)) ? 2 : 1;
+#else
   const int mc = d->cout > 32 ? 2 : 1;
+#endif
   p.nco = (int)ceil_div(d->cout, 32 * mc);
   const long long tiles = (long long)p.nco * (cin / 32);
   // one workgroup per CU (LDS / 224 accumulators): S brick ranges x tiles <= 256,
