@@ -381,8 +381,12 @@ __device__ __forceinline__ void wg_dma16(__amdgpu_buffer_rsrc_t r, unsigned lds,
 }
 #pragma clang diagnostic pop
 
-template <typename T, int MC, int MODE>
-__global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
+// WS (warp-specialised, r05): 512 threads -- waves 0-3 run the MFMAs (MC = 1: their 7 taps x 32 co
+// x 32 ci = 112 accumulators fit two waves per SIMD), waves 4-7 issue and wait for the LDS-DMA of
+// the next brick.  Issued by the MFMA waves themselves (WS = false) the DMA cost them ~180 cycles per
+// instruction at every brick start (r05 decomposition): here it runs beside the MFMAs.
+template <typename T, int MC, int MODE, bool WS = false>
+__global__ void __launch_bounds__(WS ? 512 : 256) wgrad_dma_kernel(WgDmaParams p) {
   using C = WgCfg<T, MC>;
   constexpr int NCH = C::NCH, EPQ = 16 / (int)sizeof(T), QPV = C::DYP / 16;
   constexpr int BUF = C::SMEM;           // one stage: the halo images + the dY rows
@@ -393,6 +397,10 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // (wv wave-uniform in an SGPR: the DMAs' LDS destinations are scalar adds)
   const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const bool mw = !WS || wv < 4;     // this wave runs MFMAs
+  const bool dw = !WS || wv >= 4;    // this wave issues the DMA
+  const int iw = WS ? (wv & 3) : wv;  // its index among the issuing waves
+  constexpr int NT = WS ? 512 : 256;
   // XCD-aware map of the 1-D grid: workgroups are dealt to the 8 XCDs round
   // robin, so the k-th workgroup of XCD j takes unit j * upx + k of the
   // range-major (brick range, channel tile) list -- the channel tiles of a
@@ -434,14 +442,14 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
   int hrel[HJ], drel[DJ];
 #pragma unroll
   for (int j = 0; j < HJ; ++j) {
-    const int pc = (wv + 4 * j) * 64 + lane, hv = pc >> 1, q = pc & 1;
+    const int pc = (iw + 4 * j) * 64 + lane, hv = pc >> 1, q = pc & 1;
     int hx = hv % WHX - 1, hy = (hv / WHX) % WHY - 1, hz = hv / (WHX * WHY) - 1;
     if (MODE == 1) { hx >>= 1; hy >>= 1; hz >>= 1; }
     hrel[j] = ((hz * p.SH + hy) * p.SW + hx) * 32 + q * 16;
   }
 #pragma unroll
   for (int j = 0; j < DJ; ++j) {
-    const int pc = (wv + 4 * j) * 64 + lane, v = pc / QPV, pos = pc % QPV;
+    const int pc = (iw + 4 * j) * 64 + lane, v = pc / QPV, pos = pc % QPV;
     const int qd = dy_quad<T, MC>(pos, v);
     drel[j] = ((((v >> 6) * p.H + ((v >> 4) & 3)) * p.W + (v & 15)) * p.dy_cs + qd * EPQ) * ESZ;
   }
@@ -473,7 +481,7 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
       const int dbase = (((z0 * p.H + y0) * p.W + x0) * p.dy_cs + co0) * ESZ;
 #pragma unroll
       for (int j = 0; j < HJ; ++j) {
-        const int k = wv + 4 * j;
+        const int k = iw + 4 * j;
         if (k < HI && (k * 64 + lane) / 2 < WHV) {
 #pragma unroll
           for (int c = 0; c < NCH; ++c)
@@ -482,13 +490,13 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
         }
       }
 #pragma unroll
-      for (int j = 0; j < DJ; ++j) wg_dma16(rd, lb + C::DY_OFF + (wv + 4 * j) * 1024, (unsigned)(dbase + drel[j]));
+      for (int j = 0; j < DJ; ++j) wg_dma16(rd, lb + C::DY_OFF + (iw + 4 * j) * 1024, (unsigned)(dbase + drel[j]));
       return;
     }
     // halo: instruction k of a chunk image covers pieces 64 k .. +63 = voxel slots 32 k .. +31, both quads
 #pragma unroll
     for (int j = 0; j < (HI + 3) / 4; ++j) {
-      const int k = wv + 4 * j;
+      const int k = iw + 4 * j;
       if (k < HI) {
         const int pc = k * 64 + lane, hv = pc >> 1, q = pc & 1;
         unsigned vb = 0xFFFFFFF0u;
@@ -511,7 +519,7 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
     // dY rows: instruction k covers pieces 64 k .. +63 = (voxel v, LDS quad position pos)
 #pragma unroll
     for (int j = 0; j < DI / 4; ++j) {
-      const int k = wv + 4 * j;
+      const int k = iw + 4 * j;
       const int pc = k * 64 + lane, v = pc / QPV, pos = pc % QPV;
       const int qd = dy_quad<T, MC>(pos, v);  // the swizzle is an involution
       const int x = x0 + (v & 15), y = y0 + ((v >> 4) & 3), z = z0 + (v >> 6);
@@ -530,13 +538,13 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
   constexpr bool no_mfma = false, no_dma = false;
 #endif
   // (no_dma: both stages are filled once, so the MFMAs run on real data -- their clock depends on it)
-  if (bb < be) issue(lds0);
+  if (bb < be && dw) issue(lds0);
   for (long long bi = bb; bi < be; ++bi) {
     unsigned char* cur = smem + ((bi - bb) & 1) * BUF;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this brick's DMA (issued one brick ago) landed
+    if (dw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this brick's DMA (issued one brick ago) landed
     __syncthreads();                                  // ... for every wave; the other stage is free
-    if (bi + 1 < be && (!no_dma || bi == bb)) issue(lds0 + (unsigned)(((bi - bb + 1) & 1) * BUF));   // brick bi + 1
-    if (!no_mfma) wg_brick_mfma<T, MC, 27>(cur, cur + C::DY_OFF, acc, toff, ntap, wv, lane);
+    if (dw && bi + 1 < be && (!no_dma || bi == bb)) issue(lds0 + (unsigned)(((bi - bb + 1) & 1) * BUF));   // brick bi + 1
+    if (mw && !no_mfma) wg_brick_mfma<T, MC, 27>(cur, cur + C::DY_OFF, acc, toff, ntap, wv, lane);
   }
   // the partial tile -> the brick range's slab in dw's OIDHW order: per 32-channel
   // half m of the tile the four waves' taps meet in LDS as [co 32][ci 32][tap 27]
@@ -550,7 +558,7 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
     __syncthreads();  // the previous half's rows are out (m = 0: the last brick's reads are done)
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-      if (k < ntap) {
+      if (mw && k < ntap) {
         const int tap = wv + 4 * k;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -564,7 +572,7 @@ __global__ void __launch_bounds__(256) wgrad_dma_kernel(WgDmaParams p) {
     float* slab = p.part + sx * ((long long)p.cout * p.cin * 27);
     for (int r = 0; r < ncol; ++r) {
       float* row = slab + ((long long)(co0 + 32 * m + r) * p.cin + ci0) * 27;
-      for (int e = tid; e < nci * 27; e += 256) row[e] = T3[r * 864 + e];
+      for (int e = tid; e < nci * 27; e += NT) row[e] = T3[r * 864 + e];
     }
   }
 }
@@ -816,16 +824,16 @@ int dispatch_wg(const WgradParams& p, int mode, bool gn, dim3 grid, hipStream_t 
   return gn ? launch_wg<T, MC, 0, true, 27>(p, grid, s) : launch_wg<T, MC, 0, false, 27>(p, grid, s);
 }
 
-template <typename T, int MC, int MODE>
+template <typename T, int MC, int MODE, bool WS = false>
 int launch_wg_dma(const WgDmaParams& p, dim3, hipStream_t s) {
   constexpr int smem = 2 * WgCfg<T, MC>::SMEM;
   static_assert(smem <= 160 * 1024, "wgrad DMA LDS");
-  auto k = wgrad_dma_kernel<T, MC, MODE>;
+  auto k = wgrad_dma_kernel<T, MC, MODE, WS>;
   CWDM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, smem));
   // 1-D: 8 XCDs x upx units of (brick range grid.x, channel tile grid.y)
   const long long n = 8LL * p.upx;
   CWDM_REQUIRE(n < (1LL << 31), CWDM_E_UNSUPPORTED, "cwdm_conv3d_wgrad: grid too large");
-  hipLaunchKernelGGL(k, dim3((unsigned)n), dim3(256), smem, s, p);
+  hipLaunchKernelGGL(k, dim3((unsigned)n), dim3(WS ? 512 : 256), smem, s, p);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }
@@ -869,11 +877,17 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
   p.part = reinterpret_cast<float*>(d->workspace);
   p.tx = (int)ceil_div(d->W, WBX); p.ty = (int)ceil_div(d->H, WBY); p.tz = (int)ceil_div(d->D, WBZ);
   p.nbricks = d->B * (long long)p.tx * p.ty * p.tz;
+  // the DMA-staged kernel's warp-specialised form takes 32-output tiles, where it measured faster:
+  // cin <= cout (r05 A/B, profiles/r05/k_wgrad_ws_ab.txt: 64->64 477 -> 440 us, 64^3 128->128 219 ->
+  // 205, the upsampling 128->128 1519 -> 1489; 192->64 / 128->64 / 384->128 1-4 % slower).  Env
+  // CWDM_WG_WS=0: never, 2: every kept-activation call (A/B)
+  static const int ws_mode = [] { const char* e = std::getenv("CWDM_WG_WS"); return e ? std::atoi(e) : 1; }();
+  const bool ws = d->u_cm && (ws_mode == 2 || (ws_mode == 1 && cin <= d->cout));
 #ifdef CWDM_WG_DIAG
   static const bool force_mc1 = [] { const char* e = std::getenv("CWDM_WG_MC1"); return e && e[0] == '1'; }();
-  const int mc = (d->cout > 32 && !(force_mc1 && d->u_cm)) ? 2 : 1;
+  const int mc = (d->cout > 32 && !((force_mc1 || ws) && d->u_cm)) ? 2 : 1;
 #else
-  const int mc = d->cout > 32 ? 2 : 1;
+  const int mc = (d->cout > 32 && !ws) ? 2 : 1;
 #endif
   p.nco = (int)ceil_div(d->cout, 32 * mc);
   const long long tiles = (long long)p.nco * (cin / 32);
@@ -915,11 +929,17 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
     q.part = p.part;
     CWDM_REQUIRE(q.act_bs < (1LL << 31) && q.dy_bs < (1LL << 31), CWDM_E_UNSUPPORTED,
                  "cwdm_conv3d_wgrad: u_cm sources above 2 GB per batch");
-    rc = d->dtype == CWDM_F16
-             ? (mc == 2 ? (d->u_mode ? launch_wg_dma<f16_t, 2, 1>(q, grid, s) : launch_wg_dma<f16_t, 2, 0>(q, grid, s))
-                        : (d->u_mode ? launch_wg_dma<f16_t, 1, 1>(q, grid, s) : launch_wg_dma<f16_t, 1, 0>(q, grid, s)))
-             : (mc == 2 ? (d->u_mode ? launch_wg_dma<bf16_t, 2, 1>(q, grid, s) : launch_wg_dma<bf16_t, 2, 0>(q, grid, s))
-                        : (d->u_mode ? launch_wg_dma<bf16_t, 1, 1>(q, grid, s) : launch_wg_dma<bf16_t, 1, 0>(q, grid, s)));
+    if (ws) {
+      rc = d->dtype == CWDM_F16
+               ? (d->u_mode ? launch_wg_dma<f16_t, 1, 1, true>(q, grid, s) : launch_wg_dma<f16_t, 1, 0, true>(q, grid, s))
+               : (d->u_mode ? launch_wg_dma<bf16_t, 1, 1, true>(q, grid, s) : launch_wg_dma<bf16_t, 1, 0, true>(q, grid, s));
+    } else {
+      rc = d->dtype == CWDM_F16
+               ? (mc == 2 ? (d->u_mode ? launch_wg_dma<f16_t, 2, 1>(q, grid, s) : launch_wg_dma<f16_t, 2, 0>(q, grid, s))
+                          : (d->u_mode ? launch_wg_dma<f16_t, 1, 1>(q, grid, s) : launch_wg_dma<f16_t, 1, 0>(q, grid, s)))
+               : (mc == 2 ? (d->u_mode ? launch_wg_dma<bf16_t, 2, 1>(q, grid, s) : launch_wg_dma<bf16_t, 2, 0>(q, grid, s))
+                          : (d->u_mode ? launch_wg_dma<bf16_t, 1, 1>(q, grid, s) : launch_wg_dma<bf16_t, 1, 0>(q, grid, s)));
+    }
     if (rc) return rc;
     return launch_wg_reduce(p.part, S, nw, d->dw, d->cout, cin, 27, false, s);
   }
