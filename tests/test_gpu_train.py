@@ -92,6 +92,11 @@ CM_CASES = [c for c in WG_CASES + RANDOM_WG_CASES if c[8] == 3] + [
     ("cm_interior_up", 1, (16, 16, 48), 32, 0, 64, 1, False, 3, 64),
     ("cm_interior_ragged", 1, (12, 16, 40), 32, 0, 32, 0, True, 3, 48),
     ("cm_interior_cs_short", 2, (12, 12, 48), 32, 0, 40, 0, False, 3, 48),
+    # cin <= cout: the warp-specialised form (32-output tiles, DMA waves); cin > cout: the
+    # 64-output tiles with the DMA issued by the MFMA waves (r05)
+    ("cm_ws_square", 1, (12, 12, 48), 64, 0, 64, 0, False, 3, 64),
+    ("cm_ws_up_wide", 1, (16, 16, 32), 64, 0, 128, 1, False, 3, 128),
+    ("cm_mc2_cin_gt_cout", 1, (12, 12, 48), 128, 0, 64, 0, False, 3, 64),
 ]
 
 
