@@ -423,19 +423,42 @@ __global__ void __launch_bounds__(256) channel_sum_kernel(const T* __restrict__ 
   }
 }
 
+// maxabs (optional): max |p| before the update and max |g| (TrainLoop.run_step's norm/param_max and
+// norm/grad_max, train_util.py:370-375 of the reference) from the same pass, as the bit patterns of
+// non-negative floats -- unsigned order = float order, a NaN above +inf, so NaN propagates -- one
+// atomic max per workgroup (exact whatever the order)
 __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long long n,
                                                    float decay, float w1, float b2, float w2, float neg_step,
-                                                   float bc2_sqrt, float eps) {
+                                                   float bc2_sqrt, float eps, unsigned* __restrict__ maxabs) {
   const long long stride = (long long)gridDim.x * blockDim.x;
+  unsigned mp = 0u, mg = 0u;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const float gi = g[i];
-    float pi = p[i] * decay;
+    const float p0 = p[i];
+    mp = max(mp, __float_as_uint(fabsf(p0)));
+    mg = max(mg, __float_as_uint(fabsf(gi)));
+    float pi = p0 * decay;
     const float mi = m[i] + w1 * (gi - m[i]);
     const float vi = v[i] * b2 + w2 * (gi * gi);
     const float den = sqrtf(vi) / bc2_sqrt + eps;
     pi = pi + neg_step * (mi / den);
     p[i] = pi; m[i] = mi; v[i] = vi;
+  }
+  if (!maxabs) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mp = max(mp, (unsigned)__shfl_xor((int)mp, o, 64));
+    mg = max(mg, (unsigned)__shfl_xor((int)mg, o, 64));
+  }
+  __shared__ unsigned red[2][4];
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = mp; red[1][threadIdx.x >> 6] = mg; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mp = max(max(red[0][0], red[0][1]), max(red[0][2], red[0][3]));
+    mg = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
+    atomicMax(maxabs, mp);
+    atomicMax(maxabs + 1, mg);
   }
 }
 
@@ -817,10 +840,12 @@ extern "C" int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V
   return CWDM_OK;
 }
 
-extern "C" int cwdm_adamw(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
-                          double beta2, double eps, double weight_decay, int64_t step, cwdm_stream_t stream) {
+namespace {
+int adamw_launch(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
+                 double eps, double weight_decay, int64_t step, float* maxabs, cwdm_stream_t stream) {
   CWDM_REQUIRE(p && g && m && v, CWDM_E_INVALID, "cwdm_adamw: null pointer");
   CWDM_REQUIRE(n >= 0 && step >= 1, CWDM_E_INVALID, "cwdm_adamw: bad size/step");
+  if (maxabs) CWDM_HIP(hipMemsetAsync(maxabs, 0, 2 * sizeof(float), (hipStream_t)stream));
   if (n == 0) return CWDM_OK;
   // scalars as torch computes them (Python doubles, cast to float at the kernel)
   const double bc1 = 1.0 - std::pow(beta1, (double)step);
@@ -831,7 +856,21 @@ extern "C" int cwdm_adamw(float* p, const float* g, float* m, float* v, int64_t 
   long long blocks = ceil_div(n, 256);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long long)n,
-                     decay, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), neg_step, bc2s, (float)eps);
+                     decay, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), neg_step, bc2s, (float)eps,
+                     reinterpret_cast<unsigned*>(maxabs));
   CWDM_LAUNCHED();
   return CWDM_OK;
+}
+}  // namespace
+
+extern "C" int cwdm_adamw(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
+                          double beta2, double eps, double weight_decay, int64_t step, cwdm_stream_t stream) {
+  return adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step, nullptr, stream);
+}
+
+extern "C" int cwdm_adamw_maxabs(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
+                                 double beta2, double eps, double weight_decay, int64_t step, float* maxabs,
+                                 cwdm_stream_t stream) {
+  CWDM_REQUIRE(maxabs, CWDM_E_INVALID, "cwdm_adamw_maxabs: null maxabs");
+  return adamw_launch(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step, maxabs, stream);
 }

@@ -40,6 +40,10 @@ class FlatAdamW(torch.optim.Optimizer):
         self._m = torch.zeros_like(flat)
         self._v = torch.zeros_like(flat)
         self._step = 0
+        # track_maxabs: step() also leaves last_maxabs = [max |p| before the update, max |g|]
+        # (a fresh 2-element device tensor per step, cwdm_adamw_maxabs: the same pass)
+        self.track_maxabs = False
+        self.last_maxabs = None
         self._bind_state()
 
     def _bind_state(self):
@@ -61,9 +65,13 @@ class FlatAdamW(torch.optim.Optimizer):
         grp = self.param_groups[0]
         b1, b2 = grp["betas"]
         self._step += 1
-        check(lib().cwdm_adamw(self._flat.data_ptr(), g.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
-                               self._flat.numel(), float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
-                               float(grp["weight_decay"]), self._step, _stream()), "AdamW.step")
+        args = (self._flat.data_ptr(), g.data_ptr(), self._m.data_ptr(), self._v.data_ptr(), self._flat.numel(),
+                float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), float(grp["weight_decay"]), self._step)
+        if self.track_maxabs:
+            self.last_maxabs = torch.empty(2, device=self._flat.device)
+            check(lib().cwdm_adamw_maxabs(*args, self.last_maxabs.data_ptr(), _stream()), "AdamW.step")
+        else:
+            check(lib().cwdm_adamw(*args, _stream()), "AdamW.step")
         # the kernel wrote through raw pointers: the model must re-pack its
         # kernel-layout weights (the parameters' own version counters do not
         # see writes to the flat buffer)

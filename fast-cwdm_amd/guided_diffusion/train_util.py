@@ -175,8 +175,15 @@ class TrainLoop:
         lossmse, sample, sample_idwt = self.forward_backward(batch, cond, label)
         if self.grad_scaler.is_enabled():
             self.grad_scaler.unscale_(self.opt)
+        # native, no loss scaler: max |p| (before the update) and max |g| come out of the AdamW
+        # pass itself (cwdm_adamw_maxabs), not two more passes over the 326 MB buffers
+        # (env CWDM_FUSED_NORMS=0: the two separate reductions, A/B)
+        fused_norms = (self.native and not self.grad_scaler.is_enabled() and hasattr(self.opt, "track_maxabs")
+                       and os.environ.get("CWDM_FUSED_NORMS", "1") != "0")
         with th.no_grad():
-            if self.native:
+            if fused_norms:
+                self.opt.track_maxabs = True
+            elif self.native:
                 # max |p| over the flat buffers without a temporary (abs().max() wrote
                 # a 326 MB |p| first: ~0.4 ms per step at 81.5 M parameters)
                 inf = float("inf")
@@ -195,6 +202,9 @@ class TrainLoop:
             info["scale"] = sc.detach().clone() if sc is not None else self.grad_scaler.get_scale()
         else:
             self.opt.step()
+        if fused_norms:
+            info["norm/param_max"] = self.opt.last_maxabs[0]
+            info["norm/grad_max"] = self.opt.last_maxabs[1]
         self._anneal_lr()
         self.log_step()
         self.last_info = info

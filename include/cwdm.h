@@ -481,6 +481,12 @@ int cwdm_channel_sum(const void* src, int dtype, int64_t B, int64_t V, int C, in
 int cwdm_adamw(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
                double eps, double weight_decay, int64_t step, cwdm_stream_t stream);
 
+/* The same step, also writing maxabs[0] = max |p| before the update and maxabs[1] = max |g|
+ * (TrainLoop.run_step's norm/param_max and norm/grad_max, guided_diffusion/train_util.py:370-375):
+ * one pass over the buffers instead of the step plus two reductions.  NaN propagates. */
+int cwdm_adamw_maxabs(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
+                      double eps, double weight_decay, int64_t step, float* maxabs, cwdm_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * U-Net plan: the whole UNetModel.forward (guided_diffusion/unet.py:754-800)
  * for the run.sh configuration family (no attention, resblock_updown=True,

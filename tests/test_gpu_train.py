@@ -405,6 +405,37 @@ def test_adamw_matches_torch():
     assert rel_err(v, st["exp_avg_sq"]) < 1e-6
 
 
+def test_adamw_maxabs_matches_separate_reductions():
+    """cwdm_adamw_maxabs: the same update bit for bit as cwdm_adamw, plus max |p| before
+    the update and max |g| exactly (the reference's norm/param_max, norm/grad_max,
+    train_util.py:370-375); a NaN gradient propagates to the max."""
+    from cwdm_hip._lib import check, lib
+    g = torch.Generator().manual_seed(12)
+    n = 300007
+    p0 = torch.randn(n, generator=g).to(DEV) * 3
+    gd = torch.randn(n, generator=g).to(DEV)
+    outs = []
+    for fused in (False, True):
+        p, m, v = p0.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+        mx = torch.full((2,), -1.0, device=DEV)
+        if fused:
+            check(lib().cwdm_adamw_maxabs(p.data_ptr(), gd.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9,
+                                          0.999, 1e-8, 0.01, 1, mx.data_ptr(), None))
+            assert float(mx[0]) == float(p0.abs().max()) and float(mx[1]) == float(gd.abs().max())
+        else:
+            check(lib().cwdm_adamw(p.data_ptr(), gd.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999,
+                                   1e-8, 0.01, 1, None))
+        outs.append((p, m, v))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    gd[n // 2] = float("nan")
+    p, m, v = p0.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    mx = torch.zeros(2, device=DEV)
+    check(lib().cwdm_adamw_maxabs(p.data_ptr(), gd.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999,
+                                  1e-8, 0.01, 1, mx.data_ptr(), None))
+    assert torch.isnan(mx[1]) and float(mx[0]) == float(p0.abs().max())
+
+
 # --------------------------------------------------------------------------- whole U-Net backward
 def _product_model(cfg, groups, params, dtype):
     from guided_diffusion.unet import UNetModel
@@ -618,6 +649,11 @@ def test_trainloop_runs_and_learns(tmp_path, monkeypatch):
     assert not torch.equal(p0, model.flat_params)
     assert torch.isfinite(model.flat_params).all()
     assert float(loop.last_info["norm/grad_max"]) > 0
+    # the fused norms (cwdm_adamw_maxabs) == the reference's reductions over the same buffers
+    pb = model.flat_params.detach().clone()
+    loop.run_step({k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in batch.items()}, {}, info={})
+    assert float(loop.last_info["norm/param_max"]) == float(pb.abs().max())
+    assert float(loop.last_info["norm/grad_max"]) == float(model.flat_grad().abs().max())
     assert os.path.exists(os.path.join(tmp_path, "checkpoints", "brats_t1n_BEST_direct_1000.pt"))
     sd = torch.load(os.path.join(tmp_path, "checkpoints", "brats_t1n_BEST_direct_1000.pt"), weights_only=True)
     assert set(sd) == set(P)
