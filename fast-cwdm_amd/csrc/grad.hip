@@ -468,12 +468,12 @@ __device__ __forceinline__ float dsilu_ref(float z) {
   return s * (1.0f + z * (1.0f - s));
 }
 
-// emb projection of one ResBlock (rows [0, n) of the block; dEb stride R)
-__global__ void __launch_bounds__(256) emb_bwd_w_kernel(const float* __restrict__ dEb, int R, int n, int B,
-                                                       const float* __restrict__ temb, int E,
-                                                       float* __restrict__ dw, float* __restrict__ db,
-                                                       float* __restrict__ dcb, int acc) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+// emb projection of one ResBlock (rows [0, n) of the block; dEb stride R), one element per
+// thread of workgroup blk (of 1024 threads)
+__device__ __forceinline__ void emb_bwd_w(const float* __restrict__ dEb, int R, int n, int B,
+                                          const float* __restrict__ temb, int E, float* __restrict__ dw,
+                                          float* __restrict__ db, float* __restrict__ dcb, int acc, int blk) {
+  const long long i = (long long)blk * 1024 + threadIdx.x;
   if (i >= (long long)n * E) return;
   const int r = (int)(i / E), e = (int)(i % E);
   float s = 0.f, sb = 0.f;
@@ -492,12 +492,10 @@ __global__ void __launch_bounds__(256) emb_bwd_w_kernel(const float* __restrict_
 // dsil[b][e] += sum_r W[r][e] * dEb[b][r]: one 1024-thread block per (16 e, b),
 // 64 row groups over all n rows, the group sums added in group order -- one
 // writer per element, a fixed summation order (no atomics: deterministic)
-__global__ void __launch_bounds__(1024) emb_bwd_x_kernel(const float* __restrict__ dEb, int R, int n,
-                                                        const float* __restrict__ W, int E,
-                                                        float* __restrict__ dsil) {
+__device__ __forceinline__ void emb_bwd_x(const float* __restrict__ dEb, int R, int n, const float* __restrict__ W,
+                                          int E, float* __restrict__ dsil, int bx, int b) {
   __shared__ float red[1024];
-  const int b = blockIdx.y;
-  const int e = blockIdx.x * 16 + (threadIdx.x & 15), rg = threadIdx.x >> 4;
+  const int e = bx * 16 + (threadIdx.x & 15), rg = threadIdx.x >> 4;
   float s = 0.f;
   if (e < E)
     for (int r = rg; r < n; r += 64) s += W[(long long)r * E + e] * dEb[(long long)b * R + r];
@@ -507,6 +505,22 @@ __global__ void __launch_bounds__(1024) emb_bwd_x_kernel(const float* __restrict
     float t = 0.f;
     for (int q = 0; q < 64; ++q) t += red[threadIdx.x + 16 * q];
     dsil[(long long)b * E + e] += t;
+  }
+}
+
+// both halves of a ResBlock's emb_layers backward in ONE launch (they read dEb and write
+// disjoint outputs): workgroups [0, nwb) the weight / bias gradient, the rest (16 e, b) of dsil
+__global__ void __launch_bounds__(1024) emb_bwd_kernel(const float* __restrict__ dEb, int R, int n, int B,
+                                                      const float* __restrict__ temb, int E,
+                                                      const float* __restrict__ W, float* __restrict__ dw,
+                                                      float* __restrict__ db, float* __restrict__ dcb, int acc,
+                                                      float* __restrict__ dsil, int nwb, int nxe) {
+  const int blk = (int)blockIdx.x;
+  if (blk < nwb) {
+    emb_bwd_w(dEb, R, n, B, temb, E, dw, db, dcb, acc, blk);
+  } else {
+    const int x = blk - nwb;
+    emb_bwd_x(dEb, R, n, W, E, dsil, x % nxe, x / nxe);
   }
 }
 
@@ -597,10 +611,9 @@ long long gn_bwd_blocks(int C, long long V) {
 
 int launch_emb_bwd(const float* dEb, int R, int n, int B, const float* temb, int E, const float* W, float* dw,
                    float* db, float* dcb, float* dsil, hipStream_t s, int acc) {
-  hipLaunchKernelGGL(emb_bwd_w_kernel, dim3((unsigned)ceil_div((long long)n * E, 256)), dim3(256), 0, s, dEb, R, n,
-                     B, temb, E, dw, db, dcb, acc);
-  CWDM_LAUNCHED();
-  hipLaunchKernelGGL(emb_bwd_x_kernel, dim3((unsigned)ceil_div(E, 16), B), dim3(1024), 0, s, dEb, R, n, W, E, dsil);
+  const int nwb = (int)ceil_div((long long)n * E, 1024), nxe = (int)ceil_div(E, 16);
+  hipLaunchKernelGGL(emb_bwd_kernel, dim3((unsigned)(nwb + nxe * B)), dim3(1024), 0, s, dEb, R, n, B, temb, E, W, dw,
+                     db, dcb, acc, dsil, nwb, nxe);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }
