@@ -524,7 +524,12 @@ __global__ void __launch_bounds__(1024) emb_bwd_kernel(const float* __restrict__
   }
 }
 
-// time_embed MLP backward (unet.py:534-539): one workgroup, batch looped.
+// time_embed MLP backward (unet.py:534-539).  TEMB_G workgroups: each recomputes the
+// batch's sinusoids, layer-1 pre-activation and dt = dsil * SiLU'(temb) (B x E values, a
+// 64-term dot each), then owns a slice of TEMB_R rows of E: dh for its slice (each 256-term
+// dot split over 16 lanes, lane sums added in a fixed butterfly order), dw2 / dw1 / db2 / db1
+// rows of its slice.  One workgroup ran the whole MLP serially: 130 us per training step.
+constexpr int TEMB_R = 16;
 __global__ void __launch_bounds__(256) temb_bwd_kernel(const float* __restrict__ t, int B, int mc,
                                                       const float* __restrict__ w1, const float* __restrict__ b1,
                                                       const float* __restrict__ w2,
@@ -537,7 +542,8 @@ __global__ void __launch_bounds__(256) temb_bwd_kernel(const float* __restrict__
   float* sinb = sm;                 // [B][mc]
   float* hid = sinb + B * mc;       // [B][E] pre-activation of layer 1
   float* dt = hid + B * E;          // [B][E] gradient of temb
-  float* dh = dt + B * E;           // [B][E] gradient of the layer-1 pre-activation
+  float* dh = dt + B * E;           // [B][TEMB_R] gradient of the layer-1 pre-activation, this slice
+  const int r0 = blockIdx.x * TEMB_R;
   for (int b = 0; b < B; ++b) {
     const float tv = t[b];
     for (int k = threadIdx.x; k < half; k += blockDim.x) {
@@ -557,28 +563,40 @@ __global__ void __launch_bounds__(256) temb_bwd_kernel(const float* __restrict__
     dt[i] = dsil[i] * dsilu_ref(temb[i]);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < B * E; i += blockDim.x) {
-    const int b = i / E, k = i % E;
-    float s = 0.f;
-    for (int o = 0; o < E; ++o) s += w2[(long long)o * E + k] * dt[b * E + o];
-    dh[i] = s * dsilu_ref(hid[i]);
+  // dh[b][k] = SiLU'(hid[b][k]) sum_o w2[o][k] dt[b][o], k in this slice: 16 lanes per (b, k),
+  // lane l the terms o = l, l + 16, ...
+  {
+    const int l = threadIdx.x & 15, kk = threadIdx.x >> 4;   // 16 (b, k) pairs per pass
+    for (int q = kk; q < B * TEMB_R; q += 16) {
+      const int b = q / TEMB_R, k = r0 + q % TEMB_R;
+      float sacc = 0.f;
+      if (k < E)
+        for (int o = l; o < E; o += 16) sacc += w2[(long long)o * E + k] * dt[b * E + o];
+#pragma unroll
+      for (int m = 8; m > 0; m >>= 1) sacc += __shfl_xor(sacc, m, 16);
+      if (l == 0 && k < E) dh[q] = sacc * dsilu_ref(hid[b * E + k]);
+    }
   }
   __syncthreads();
-  for (long long i = threadIdx.x; i < (long long)E * E; i += blockDim.x) {
-    const int o = (int)(i / E), k = (int)(i % E);
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dt[b * E + o] * silu_ref(hid[b * E + k]);
-    dw2[i] = s;
+  for (int i = threadIdx.x; i < TEMB_R * E; i += blockDim.x) {
+    const int o = r0 + i / E, k = i % E;
+    if (o >= E) continue;
+    float s2 = 0.f;
+    for (int b = 0; b < B; ++b) s2 += dt[b * E + o] * silu_ref(hid[b * E + k]);
+    dw2[(long long)o * E + k] = s2;
   }
-  for (long long i = threadIdx.x; i < (long long)E * mc; i += blockDim.x) {
-    const int o = (int)(i / mc), k = (int)(i % mc);
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dh[b * E + o] * sinb[b * mc + k];
-    dw1[i] = s;
+  for (int i = threadIdx.x; i < TEMB_R * mc; i += blockDim.x) {
+    const int ol = i / mc, o = r0 + ol, k = i % mc;
+    if (o >= E) continue;
+    float s1 = 0.f;
+    for (int b = 0; b < B; ++b) s1 += dh[b * TEMB_R + ol] * sinb[b * mc + k];
+    dw1[(long long)o * mc + k] = s1;
   }
-  for (int o = threadIdx.x; o < E; o += blockDim.x) {
+  for (int ol = threadIdx.x; ol < TEMB_R; ol += blockDim.x) {
+    const int o = r0 + ol;
+    if (o >= E) continue;
     float s2 = 0.f, s1 = 0.f;
-    for (int b = 0; b < B; ++b) { s2 += dt[b * E + o]; s1 += dh[b * E + o]; }
+    for (int b = 0; b < B; ++b) { s2 += dt[b * E + o]; s1 += dh[b * TEMB_R + ol]; }
     db2[o] = s2;
     db1[o] = s1;
   }
@@ -622,10 +640,10 @@ int launch_temb_bwd(const float* t, int B, int mc, const float* w1, const float*
                     const float* temb, const float* dsil, float* dw1, float* db1, float* dw2, float* db2,
                     hipStream_t s) {
   const int E = 4 * mc;
-  const size_t sm = (size_t)(B * mc + 3 * B * E) * sizeof(float);
+  const size_t sm = (size_t)(B * mc + 2 * B * E + B * TEMB_R) * sizeof(float);
   CWDM_REQUIRE(sm <= 64 * 1024, CWDM_E_SHAPE, "time_embed backward: batch too large for one workgroup");
-  hipLaunchKernelGGL(temb_bwd_kernel, dim3(1), dim3(256), sm, s, t, B, mc, w1, b1, w2, temb, dsil, dw1, db1, dw2,
-                     db2);
+  hipLaunchKernelGGL(temb_bwd_kernel, dim3((unsigned)ceil_div(E, TEMB_R)), dim3(256), sm, s, t, B, mc, w1, b1, w2,
+                     temb, dsil, dw1, db1, dw2, db2);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }
