@@ -669,40 +669,54 @@ def test_gn_apply_matches_torch():
     assert rel_err(out, ref) < 1e-5
 
 
-# (parts of source 0, parts of source 1, B, C0, C1, grid): 4 parts -- one workgroup per group; >= 512 --
-# the two-level finalize (slices of part rows into an fp64 slab, then per group), with the two
-# sources' part counts different as for a decoder concat
+# (parts of source 0, parts of source 1, B, C0, C1, grid): 4 to 4096 part rows, the two sources'
+# part counts different as for a decoder concat
 @pytest.mark.parametrize("p0,p1,B,C0,C1,n", [(4, 4, 2, 64, 32, 8), (1024, 512, 2, 64, 128, 16),
-                                             (4096, 4096, 1, 192, 0, 16), (2048, 1024, 1, 128, 64, 16)])
+                                             (4096, 4096, 1, 192, 0, 16), (2048, 1024, 1, 128, 64, 16),
+                                             (4096, 4096, 1, 64, 0, 16), (512, 4096, 1, 384, 128, 16),
+                                             (2048, 2048, 4, 128, 0, 16)])
 def test_gn_finalize_matches_group_norm(p0, p1, B, C0, C1, n):
+    """cwdm_gn_finalize vs F.group_norm, three calls on fresh data (no state carried
+    between calls) and a repeat on the same data that must be bit-identical (fixed
+    reduction order), up to the 128^3 levels' 4096 part rows and concat sources with
+    different part counts."""
     from cwdm_hip import _lib
     from cwdm_hip._lib import check, lib
-    g = torch.Generator().manual_seed(3)
     G = 32
     D = H = W = n
-    x = torch.randn(B, C0 + C1, D, H, W, generator=g) * 2 + 0.5
-    # fake per-tile partials: the voxels split into p0 (source 0) / p1 (source 1) parts
-    def parts_of(xs, P):
-        xv = xs.reshape(B, xs.shape[1], P, -1)
-        return torch.stack([xv.sum(-1), (xv ** 2).sum(-1)], -1).permute(0, 2, 1, 3).contiguous()  # B, P, C, 2
-    s0 = parts_of(x[:, :C0], p0).to(DEV)
-    s1 = parts_of(x[:, C0:], p1).to(DEV) if C1 else None
-    gamma = (1 + 0.1 * torch.randn(C0 + C1, generator=g)).to(DEV)
-    beta = (0.1 * torch.randn(C0 + C1, generator=g)).to(DEV)
-    out = torch.empty(B, C0 + C1, 2, device=DEV)
-    mr = torch.empty(B, G, 2, device=DEV)
-    check(lib().cwdm_gn_finalize(ctypes.c_void_p(s0.data_ptr()), p0, C0,
-                                 ctypes.c_void_p(s1.data_ptr()) if C1 else None, p1, C1,
-                                 ctypes.c_void_p(gamma.data_ptr()), ctypes.c_void_p(beta.data_ptr()), G, B,
-                                 D * H * W, 1e-5, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(mr.data_ptr()),
-                                 None))
-    o = out.cpu()
-    y = x * o[..., 0][:, :, None, None, None] + o[..., 1][:, :, None, None, None]
-    ref = F.group_norm(x, G, gamma.cpu(), beta.cpu(), eps=1e-5)
-    assert rel_err(y, ref) < 1e-5
-    xg = x.double().view(B, G, -1)
-    assert torch.allclose(mr.cpu()[..., 0].double(), xg.mean(-1), rtol=1e-5, atol=1e-6)
-    assert torch.allclose(mr.cpu()[..., 1].double(), 1 / torch.sqrt(xg.var(-1, unbiased=False) + 1e-5), rtol=1e-5)
+    prev = None
+    for rep in range(3):
+        g = torch.Generator().manual_seed(3 + rep)
+        x = torch.randn(B, C0 + C1, D, H, W, generator=g) * (2 + rep) + 0.5 - rep
+        # fake per-tile partials: the voxels split into p0 (source 0) / p1 (source 1) parts
+        def parts_of(xs, P):
+            xv = xs.reshape(B, xs.shape[1], P, -1)
+            return torch.stack([xv.sum(-1), (xv ** 2).sum(-1)], -1).permute(0, 2, 1, 3).contiguous()  # B, P, C, 2
+        s0 = parts_of(x[:, :C0], p0).to(DEV)
+        s1 = parts_of(x[:, C0:], p1).to(DEV) if C1 else None
+        gamma = (1 + 0.1 * torch.randn(C0 + C1, generator=g)).to(DEV)
+        beta = (0.1 * torch.randn(C0 + C1, generator=g)).to(DEV)
+        outs = []
+        for _ in range(2):
+            out = torch.empty(B, C0 + C1, 2, device=DEV)
+            mr = torch.empty(B, G, 2, device=DEV)
+            check(lib().cwdm_gn_finalize(ctypes.c_void_p(s0.data_ptr()), p0, C0,
+                                         ctypes.c_void_p(s1.data_ptr()) if C1 else None, p1, C1,
+                                         ctypes.c_void_p(gamma.data_ptr()), ctypes.c_void_p(beta.data_ptr()), G, B,
+                                         D * H * W, 1e-5, ctypes.c_void_p(out.data_ptr()),
+                                         ctypes.c_void_p(mr.data_ptr()), None))
+            outs.append((out.cpu(), mr.cpu()))
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+        o, mr = outs[0]
+        if prev is not None:
+            assert not torch.equal(o, prev)
+        prev = o
+        y = x * o[..., 0][:, :, None, None, None] + o[..., 1][:, :, None, None, None]
+        ref = F.group_norm(x, G, gamma.cpu(), beta.cpu(), eps=1e-5)
+        assert rel_err(y, ref) < 1e-5
+        xg = x.double().view(B, G, -1)
+        assert torch.allclose(mr[..., 0].double(), xg.mean(-1), rtol=1e-5, atol=1e-6)
+        assert torch.allclose(mr[..., 1].double(), 1 / torch.sqrt(xg.var(-1, unbiased=False) + 1e-5), rtol=1e-5)
 
 
 @pytest.mark.parametrize("dtype_name", ["bf16", "fp16"])

@@ -286,13 +286,26 @@ def test_conv3d_pointwise_two_sources_bias_vs_torch(dtype_name):
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("chans", [(64, 0), (32, 32)])
 def test_gn_silu_bwd_vs_autograd(chans, mode, dtype_name):
+    _gn_silu_bwd_case(chans, mode, dtype_name, (4, 8, 6), 2, 8)
+
+
+# grids with 384-1024 reduce blocks (the wide levels' finalize loads), 8 and 32 groups,
+# a concat and a pooled source; two seeds per case
+@pytest.mark.parametrize("chans,mode,dtype_name,grid,B,G", [
+    ((64, 0), 0, "fp32", (32, 32, 48), 2, 8), ((64, 64), 0, "bf16", (32, 32, 32), 1, 32),
+    ((128, 0), 2, "fp32", (32, 64, 64), 1, 32), ((64, 0), 0, "bf16", (64, 64, 32), 1, 32)])
+def test_gn_silu_bwd_two_level_finalize_vs_autograd(chans, mode, dtype_name, grid, B, G):
+    _gn_silu_bwd_case(chans, mode, dtype_name, grid, B, G)
+    _gn_silu_bwd_case(chans, mode, dtype_name, grid, B, G, seed=10)
+
+
+def _gn_silu_bwd_case(chans, mode, dtype_name, grid, B, G, seed=9):
     from cwdm_hip import _lib
     from cwdm_hip._lib import check, lib
     dtype, tdt = _dt(dtype_name)
     c0, c1 = chans
-    C, G, B = c0 + c1, 8, 2
-    grid = (4, 8, 6)
-    g = torch.Generator().manual_seed(9)
+    C = c0 + c1
+    g = torch.Generator().manual_seed(seed)
     x = (1.5 * torch.randn(B, C, *grid, generator=g) + 0.3).to(tdt).float()
     gamma = 1 + 0.1 * torch.randn(C, generator=g)
     beta = 0.1 * torch.randn(C, generator=g)
