@@ -334,6 +334,49 @@ def test_fullsize_training_step_fp32_vs_oracle():
     assert top[0][1] < 1e-3, top
 
 
+def test_fullsize_training_step_half_close_to_fp32():
+    """The benchmarked training dtype at the config-3 size: one bf16 (and fp16)
+    128^3 step -- training_losses (reference gaussian_diffusion.py:1131-1166)
+    + native backward (train_util.py:396-470) -- against the fp32 native step
+    on the same weights, batch, t and noise.  The fp32 step is itself pinned to
+    the oracle's autograd at 1e-3 (test_fullsize_training_step_fp32_vs_oracle),
+    so this bounds the 16-bit gradients against the reference's fp32 ones.
+    Bounds are documented regression bounds, not parity: the
+    16-bit activations round every stored tensor of forward and backward."""
+    P = ou.random_params(seed=7)
+    vols, t, noise = _train_case()
+    vols = {k: v.to(DEV) for k, v in vols.items()}
+    res = {}
+    for dt in ("fp32", "bf16", "fp16"):
+        model, diffusion = _production(dt, P)
+        terms, _, _ = diffusion.training_losses(model, vols, t.to(DEV), mode="i2i", contr="t1n", noise=noise.to(DEV))
+        loss = terms["mse_wav"].mean()
+        loss.backward()
+        res[dt] = (float(loss), {n: p.grad.detach().double().cpu() for n, p in model.named_parameters()},
+                   model.flat_grad().detach().double().cpu())
+        del model, terms, loss
+        torch.cuda.empty_cache()
+    l32, g32, f32 = res["fp32"]
+    # measured (r06): see DESIGN.md §4 (printed below); bounds ~2x the measured values
+    bounds = {"bf16": dict(loss=2e-2, flat=6e-2, median=8e-2, worst=0.5),
+              "fp16": dict(loss=4e-3, flat=1e-2, median=1.5e-2, worst=0.1)}
+    for dt, bd in bounds.items():
+        lh, gh, fh = res[dt]
+        lrel = abs(lh - l32) / abs(l32)
+        flat = float((fh - f32).norm() / f32.norm())
+        per = {k: float((gh[k] - g32[k]).norm() / g32[k].norm().clamp_min(1e-30)) for k in g32}
+        vals = sorted(per.values())
+        med = vals[len(vals) // 2]
+        top = sorted(per.items(), key=lambda kv: -kv[1])[:5]
+        print(f"config-3 128^3 training step, {dt} vs fp32: loss rel {lrel:.3e}, flat gradient rel L2 {flat:.3e}, "
+              f"per-parameter rel L2 median {med:.3e}, worst {top}")
+        assert all(torch.isfinite(v).all() for v in gh.values())
+        assert lrel < bd["loss"], (dt, lrel)
+        assert flat < bd["flat"], (dt, flat)
+        assert med < bd["median"], (dt, med)
+        assert top[0][1] < bd["worst"], (dt, top)
+
+
 @pytest.mark.parametrize("dtype", ["bf16"])
 def test_fullsize_training_two_steps_bitwise_reproducible(dtype):
     """The config-3 benchmark step itself (bf16, 128^3, kept activations,
