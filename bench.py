@@ -448,6 +448,7 @@ def main():
     sync()
     elapsed = max_over_ranks(time.perf_counter() - t0)
     loop.close()
+    ops.check_device_status("bench timed loop")   # (after the timed region: it synchronises)
 
     # roofline of the dominant kernel -- the implicit-GEMM MFMA conv kernels:
     # hipEvents around each of their launches over one extra (eager) step, on

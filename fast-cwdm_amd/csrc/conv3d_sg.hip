@@ -501,6 +501,10 @@ int sg_skip_ksplit(const cwdm_conv3d_desc* d) { return sg_skip_eligible(d) ? sg_
 
 // bytes of the K-split counter block a lone launch keeps behind its slices (0 without a split)
 int64_t sg_sync_bytes(int ksplit) { return ksplit > 1 ? kSgSyncWords * 4 : 0; }
+// the U-Net plan's zeroed sync block: the small-grid K-split counters, then the
+// warp-specialised conv's apply-ahead sweep counters (kV5AaWords)
+int64_t plan_sync_bytes() { return kSgSyncWords * 4 + kV5AaWords * 4; }
+unsigned* plan_aa_counters() { return g_sg_sync ? g_sg_sync + kSgSyncWords : nullptr; }
 
 namespace {
 // counters of a K-split launch: the plan's pre-zeroed block, else `own` (the

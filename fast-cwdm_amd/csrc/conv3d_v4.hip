@@ -221,6 +221,7 @@ bool v5_eligible(const cwdm_conv3d_desc* d, bool gn);
 int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
               const float* agn, const void* res, int rmode, hipStream_t s, const V5Aa* aa = nullptr);
 int v5_aa_units(const cwdm_conv3d_desc* d, int* lead);
+unsigned* plan_aa_counters();
 
 int64_t v4_items(const cwdm_conv3d_desc* d) {
   return d->B * ((d->W + 31) / 32) * (d->H / 4) * (d->D / 4) * (d->cout / 64);
@@ -294,6 +295,8 @@ int64_t v4_workspace_bytes(const cwdm_conv3d_desc* d) {
   }
   // (+ the small-grid kernel's K-split arrival counters behind the slices)
   if (S > 1) ws += align256(S * d->B * ksplit_slice_voxels(d) * d->cout * 4) + sg_sync_bytes(S);
+  // (+ a lone launch's apply-ahead sweep counters, last: conv3d_v4_forward)
+  if (d->a_gn) ws += kV5AaWords * 4;
   return ws;
 }
 
@@ -557,6 +560,14 @@ int conv3d_v4_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     }
     if (aa.units) {
       aa.x0 = a0; aa.c0 = c0; aa.x1 = a1; aa.c1 = c1; aa.gn = d->a_gn;
+      // the sweep counters: the plan's zeroed sync block, else this launch's workspace tail (zeroed here)
+      aa.cnt = plan_aa_counters();
+      if (!aa.cnt) {
+        const int64_t need = v4_workspace_bytes(d);
+        CWDM_REQUIRE(d->workspace && d->ws_bytes >= need, CWDM_E_WORKSPACE, "conv3d (apply-ahead): workspace too small");
+        aa.cnt = reinterpret_cast<unsigned*>(reinterpret_cast<unsigned char*>(d->workspace) + need - kV5AaWords * 4);
+        CWDM_HIP(hipMemsetAsync(aa.cnt, 0, kV5AaWords * 4, s));
+      }
     } else if (fin) {
       fin->used = true;
       if ((rc = gn_fin_apply(*fin, a0, c0, a1, c1, d->B, SV, d->dtype, act, s))) return rc;

@@ -86,6 +86,9 @@ struct V4Params {
   const void* ax0; const void* ax1; int axc0, axc1; int aa_lead;
   int aa_units;   // steps of the share per chunk (<= the instance's AA loads)
   int aa_prio;    // helpers at s_setprio 1 for the share's transform (env CWDM_V5_AA_PRIO, A/B knob)
+  unsigned* aa_cnt;   // this launch's sweep counters (kV5AaCnt words, zero at launch; the last workgroup out re-zeroes them)
+  int aa_spin;        // bound of a counter wait (s_sleep rounds); a wait that runs out sets CWDM_DEV_E_AA_TIMEOUT
+  int aa_extra;       // debug (cwdm_debug_v5_aa_timeout): arrivals a wait needs beyond the grid (forces the timeout path)
 };
 
 
@@ -93,7 +96,8 @@ __device__ unsigned g_v4_cu_arrivals[8 * 256];
 
 // conv3d_v5 apply-ahead arguments (conv3d_v5.hip): the raw sources of a GroupNorm'd input, their
 // scale / shift, the sweep lead and the per-chunk share of the kernel instance (v5_aa_units)
-struct V5Aa { const void* x0; int c0; const void* x1; int c1; const float* gn; int lead, units; };
+constexpr int kV5AaWords = 4096;   // apply-ahead sweep counters of one launch (conv3d_v5.hip kV5AaCnt)
+struct V5Aa { const void* x0; int c0; const void* x1; int c1; const float* gn; int lead, units; unsigned* cnt; };
 
 struct V4Cfg {
   static constexpr int HX = 34, HY = 6, HZ = 6, HV = HX * HY * HZ;  // 1224 halo voxels

@@ -93,11 +93,46 @@ static_assert(V5Cfg::SMEM <= 163840, "v5 LDS");
 // memory: sc1); a counter per range collects the G workgroups' completions,
 // and a helper waits on R(it)'s counter before it issues tile it's first
 // DMA.  R(0 .. L - 1) is transformed by all eight waves before the first tile
-// (the one grid-wide wait).  The workgroup that exits last re-zeroes the
-// counters for the next launch.  Batch 1, same-grid sources.
+// (the one grid-wide wait).  Batch 1, same-grid sources.
+// Counters: per launch (p.aa_cnt: the U-Net plan's sync block, zeroed once per
+// forward, or a lone launch's workspace tail, zeroed by a memset node before
+// it), so launches on other streams never share them; the workgroup that exits
+// last re-zeroes them for the plan's next AA launch.
+// Visibility (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms):
+// the transformed bytes are stored write-through (sc1: they leave the writer's
+// L2), every storing wave drains them (s_waitcnt vmcnt(0)) before the
+// workgroup barrier behind which ONE lane adds to the range counter (agent
+// scope); the reader polls that counter with agent-scope (sc1) loads.  The
+// reader's halo LDS-DMA is not an sc1 load, and no acquire fence follows the
+// poll (an agent acquire only invalidates this CU's L1: ~1.7 us per tile; an
+// agent release on the writer would write back the XCD's dirty L2 per range):
+// what makes a plain load safe here is that no CU reads a byte of range r + 1
+// before r + 1 is published -- the sweep reads prefixes of the source, range
+// boundaries fall on whole z planes (H W voxels x 32 B: 128-B aligned), and L1 /
+// L2 hold nothing of the copy from earlier launches (kernel boundaries write
+// back and invalidate) -- so neither cache can hold a stale line of it.
+// Residency: every wait needs all G workgroups resident at once; G <= the CUs
+// x the instance's occupancy (v5_aa_grid).  A wait that still runs out (CUs
+// held by another process, CU masking) sets CWDM_DEV_E_AA_TIMEOUT in the
+// device error word (cwdm_device_status) instead of failing silently.
 // ---------------------------------------------------------------------------
-constexpr int kV5AaCnt = 4096;                 // [0] the prologue ranges, [r] range r, [kV5AaCnt - 1] exits
-__device__ unsigned g_v5aa_cnt[kV5AaCnt];
+constexpr int kV5AaCnt = kV5AaWords;           // [0] the prologue ranges, [r] range r, [kV5AaCnt - 1] exits
+__device__ unsigned g_cwdm_dev_err;            // sticky CWDM_DEV_E_* bits (cwdm_device_status)
+
+// bounded wait for `need` arrivals on counter c (agent-scope sc1 polls); false (and the
+// device error word set) when the bound runs out
+__device__ __forceinline__ bool v5aa_wait(unsigned* c, unsigned need, int spin, int sleep2) {
+  for (int n = 0; __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need; ++n) {
+    if (n >= spin) {
+      __hip_atomic_fetch_or(&g_cwdm_dev_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if (sleep2) __builtin_amdgcn_s_sleep(2);
+    else __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");   // nothing that reads the range is hoisted above the poll
+  return true;
+}
 
 __device__ __forceinline__ int v5aa_pos() {
   const int G = gridDim.x;
@@ -212,10 +247,8 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      __hip_atomic_fetch_add(&g_v5aa_cnt[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int n = 0; __hip_atomic_load(&g_v5aa_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)G &&
-                      n < (1 << 24); ++n)
-        __builtin_amdgcn_s_sleep(2);
+      __hip_atomic_fetch_add(&p.aa_cnt[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v5aa_wait(&p.aa_cnt[0], (unsigned)(G + p.aa_extra), p.aa_spin, 1);
     }
     __syncthreads();
   }
@@ -578,9 +611,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
 #ifdef CWDM_CONV_STAMPS
           const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-          for (int n = 0; __hip_atomic_load(&g_v5aa_cnt[pit], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)G &&
-                          n < (1 << 24); ++n)
-            __builtin_amdgcn_s_sleep(1);
+          v5aa_wait(&p.aa_cnt[pit], (unsigned)(G + p.aa_extra), p.aa_spin, 0);
           chk = false;
 #ifdef CWDM_CONV_STAMPS
           if (p.stamps && tid == 256) p.stamps[(long long)blockIdx.x * 64 + 56] += __builtin_amdgcn_s_memtime() - t0;
@@ -588,7 +619,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
         }
         // the previous tile's AA share is retired in every helper (chunk 0's wait + barrier): publish it
         if (cc == 1 && it > 0 && it - 1 + L < aa_nit && tid == 256)
-          __hip_atomic_fetch_add(&g_v5aa_cnt[it - 1 + L], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(&p.aa_cnt[it - 1 + L], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int d0 = 0, k0 = 0, k1 = 0;
         if (pend == 2) {
           drain(dt, 0, (gch + 2) % 3, 0, 8);
@@ -662,12 +693,12 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
     // the last workgroup out re-zeroes the sweep counters for the next launch
     if (h == 0) {
       unsigned old = 0;
-      if (lane == 0) old = __hip_atomic_fetch_add(&g_v5aa_cnt[kV5AaCnt - 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) old = __hip_atomic_fetch_add(&p.aa_cnt[kV5AaCnt - 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       old = __builtin_amdgcn_readfirstlane(old);
       if (old == (unsigned)G - 1u) {
         for (int r = lane; r < aa_nit; r += 64)
-          __hip_atomic_store(&g_v5aa_cnt[r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lane == 0) __hip_atomic_store(&g_v5aa_cnt[kV5AaCnt - 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&p.aa_cnt[r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(&p.aa_cnt[kV5AaCnt - 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     return;
@@ -767,7 +798,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
 // ---------------------------------------------------------------------------
 // The accurate fast mode: fp32 activations, conv MFMAs on bf16 hi/lo splits,
 // three bf16 products per fp32 product: hi(x) hi(w) + lo(x) hi(w) + hi(x) lo(w)
-// (lo(x) lo(w) is below fp32 rounding: dropped).  Same warp-specialised
+// (lo(x) lo(w), ~2^-18 of the product -- about 64x fp32 epsilon -- is dropped).  Same warp-specialised
 // pipeline as conv3d_v5_kernel, but per PAIR of fp32 chunks (16 channels):
 //   * helpers DMA both chunks (8 fp32 channels = 32 B per voxel slot each) and
 //     convert each in place (the GroupNorm+SiLU applied first when agn is set)
@@ -1108,6 +1139,33 @@ std::atomic<int> g_v5_aa{[] { const char* e = std::getenv("CWDM_V5_AA"); return 
 std::atomic<int> g_v5_aa_launches{0};
 int64_t v4_items(const cwdm_conv3d_desc* d);
 bool gbwd_grid_ok(const cwdm_conv3d_desc* d);
+std::atomic<int> g_v5_aa_extra{0};
+std::atomic<int> g_v5_aa_spin{0};
+
+namespace {
+int v5_ncu() {
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  return ncu;
+}
+// the persistent grid of an apply-ahead launch: every workgroup must be resident at once (its counter
+// waits span the grid), so never more than the CUs x the instance's occupancy, whatever the debug cap
+int v5_aa_grid(int64_t nblk) {
+  static const int occ = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv3d_v5_kernel<bf16_t, 0, false, 8>, 512, 0) != hipSuccess)
+      return 1;
+    return n > 0 ? n : 1;
+  }();
+  const int cap = g_v5_grid.load(std::memory_order_relaxed);
+  const int64_t lim = (int64_t)v5_ncu() * occ;
+  return (int)std::min<int64_t>(nblk, cap > 0 ? std::min<int64_t>(cap, lim) : v5_ncu());
+}
+}  // namespace
 
 // the warp-specialised kernel takes a conv of the DMA path when it is a 16-bit
 // fast-epilogue conv without K split and with at least one tile per CU (CWDM_V5_MIN_TPC)
@@ -1182,16 +1240,9 @@ int v5_aa_units(const cwdm_conv3d_desc* d, int* lead) {
   if (mode == 1 && (d->a_c0 + d->a_c1) / 16 < minch) return 0;
   const int64_t V = d->D * d->H * d->W;
   if (V * C * 2 >= 0x7FFFF000LL) return 0;
-  static const int ncu = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return n > 0 ? n : 256;
-  }();
-  const int cap = g_v5_grid.load(std::memory_order_relaxed);
   const int tx = (int)((d->W + 31) / 32), ty = (int)(d->H / 4), tz = (int)(d->D / 4), nct = d->cout / 64;
   const int64_t nblk = (int64_t)tx * ty * tz * nct;
-  const int G = (int)std::min<int64_t>(nblk, cap > 0 ? cap : ncu);
+  const int G = v5_aa_grid(nblk);
   const int nit = (int)((nblk + G - 1) / G);
   if (nit > kV5AaCnt - 2) return 0;
   const int nch = C / 16;
@@ -1247,6 +1298,11 @@ int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
     p.aa_units = aa->units;
     static const int prio = [] { const char* e = std::getenv("CWDM_V5_AA_PRIO"); return e ? std::atoi(e) : 0; }();
     p.aa_prio = prio;
+    CWDM_REQUIRE(aa->cnt, CWDM_E_INVALID, "conv3d_v5: apply-ahead counters missing");
+    p.aa_cnt = aa->cnt;
+    const int spin = g_v5_aa_spin.load(std::memory_order_relaxed);
+    p.aa_spin = spin > 0 ? spin : (1 << 24);
+    p.aa_extra = g_v5_aa_extra.load(std::memory_order_relaxed);
   }
 #ifdef CWDM_V5_DIAG
   static const int diag = [] { const char* e = std::getenv("CWDM_V5_DIAGMASK"); return e ? std::atoi(e) : 0; }();
@@ -1262,7 +1318,7 @@ int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
     return n > 0 ? n : 256;
   }();
   const int cap = g_v5_grid.load(std::memory_order_relaxed);
-  const dim3 grid((unsigned)std::min<long long>(nblk, cap > 0 ? cap : ncu));
+  const dim3 grid(aa ? (unsigned)v5_aa_grid(nblk) : (unsigned)std::min<long long>(nblk, cap > 0 ? cap : ncu));
   prof_begin(s);
   auto go = [&](auto tag) {
     using T = decltype(tag);
@@ -1325,6 +1381,24 @@ template __global__ void conv3d_v5s_kernel<1, false>(V4Params);
 extern "C" int cwdm_debug_v5_aa(int on) {
   if (on < 0) return cwdm::g_v5_aa_launches.load(std::memory_order_relaxed);
   return cwdm::g_v5_aa.exchange(on > 2 ? 2 : on);
+}
+
+extern "C" int cwdm_debug_v5_aa_timeout(int extra, int spin) {
+  CWDM_REQUIRE(extra >= 0 && spin >= 0, CWDM_E_INVALID, "cwdm_debug_v5_aa_timeout: extra, spin >= 0");
+  cwdm::g_v5_aa_extra.store(extra);
+  cwdm::g_v5_aa_spin.store(spin);
+  return CWDM_OK;
+}
+
+extern "C" int cwdm_device_status(int clear) {
+  unsigned v = 0;
+  CWDM_HIP(hipDeviceSynchronize());
+  CWDM_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(cwdm::g_cwdm_dev_err), sizeof(v), 0, hipMemcpyDeviceToHost));
+  if (clear && v) {
+    const unsigned z = 0;
+    CWDM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(cwdm::g_cwdm_dev_err), &z, sizeof(z), 0, hipMemcpyHostToDevice));
+  }
+  return (int)v;
 }
 
 extern "C" int cwdm_debug_v5_grid(int n) {

@@ -630,6 +630,7 @@ int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
               const void* res, int rmode, void* partial, hipStream_t s);
 extern thread_local unsigned* g_sg_sync;
 int64_t sg_sync_bytes(int ksplit);
+int64_t plan_sync_bytes();
 bool head_eligible(const cwdm_conv3d_desc* d);
 extern thread_local std::vector<PackJob>* g_pack_batch;  // conv3d.hip
 int pack_batch_run(std::vector<PackJob>& jobs, int dtype, PackJob* table, std::vector<PackJob>& cache, hipStream_t s);
@@ -756,7 +757,7 @@ Layout layout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) {
   Layout L;
   int64_t off = 0;
   auto take = [&](int64_t bytes) { int64_t o = off; off = align_up(off + bytes); return o; };
-  L.sync = take(cwdm::sg_sync_bytes(2));   // first: a memset block at a 256-byte boundary
+  L.sync = take(cwdm::plan_sync_bytes());   // first: a memset block at a 256-byte boundary
   L.temb = take(B * u->E * 4);
   L.ebias = take(B * (int64_t)u->R * 4);
   const int es = esize(u->cfg.dtype);
@@ -1080,7 +1081,7 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
   hipStream_t s = (hipStream_t)stream;
   auto* pk = reinterpret_cast<const unsigned char*>(packed);
   auto* wb = reinterpret_cast<unsigned char*>(ws);
-  CWDM_HIP(hipMemsetAsync(wb + L.sync, 0, cwdm::sg_sync_bytes(2), s));
+  CWDM_HIP(hipMemsetAsync(wb + L.sync, 0, cwdm::plan_sync_bytes(), s));
   SgSyncScope sync_scope(wb + L.sync);
   float* temb = reinterpret_cast<float*>(wb + L.temb);
   float* ebias = reinterpret_cast<float*>(wb + L.ebias);
@@ -1429,7 +1430,7 @@ GLayout glayout(const cwdm_unet* u, int64_t B, int64_t D, int64_t H, int64_t W) 
   int64_t off = 0;
   auto take = [&](int64_t bytes) { int64_t o = off; off = align_up(off + bytes); return o; };
   const int es = esize(u->cfg.dtype);
-  G.sync = take(cwdm::sg_sync_bytes(2));
+  G.sync = take(cwdm::plan_sync_bytes());
   for (size_t i = 0; i < u->tensors.size(); ++i) {
     const auto& t = u->tensors[i];
     if ((int)i == u->input_tensor) { G.g_off.push_back(-1); continue; }
@@ -1575,7 +1576,7 @@ extern "C" int cwdm_unet_backward(cwdm_unet* u, const void* packed, const void* 
   auto* wb = reinterpret_cast<const unsigned char*>(ws);
   auto* gb = reinterpret_cast<unsigned char*>(gws);
   // (every call: a caller may run segments on a fresh grad workspace)
-  CWDM_HIP(hipMemsetAsync(gb + G.sync, 0, cwdm::sg_sync_bytes(2), s));
+  CWDM_HIP(hipMemsetAsync(gb + G.sync, 0, cwdm::plan_sync_bytes(), s));
   SgSyncScope sync_scope(gb + G.sync);
   auto P = [&](int64_t off) { return reinterpret_cast<const float*>(pk + off); };
   auto GR = [&](int pi) { return grads + u->goff[pi]; };

@@ -152,6 +152,8 @@ _PROTOS = {
     "cwdm_conv3d_set_path": (ctypes.c_int, [ctypes.c_int]),
     "cwdm_debug_v5_grid": (ctypes.c_int, [ctypes.c_int]),
     "cwdm_debug_v5_aa": (ctypes.c_int, [ctypes.c_int]),
+    "cwdm_debug_v5_aa_timeout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "cwdm_device_status": (ctypes.c_int, [ctypes.c_int]),
     "cwdm_debug_gn_fin_apply": (ctypes.c_int, [vp, i64, ctypes.c_int, vp, i64, ctypes.c_int, vp, vp, ctypes.c_int,
                                                i64, i64, ctypes.c_float, vp, vp, ctypes.c_int, vp, vp, vp, vp]),
     "cwdm_debug_head2": (ctypes.c_int, [ctypes.c_int]),

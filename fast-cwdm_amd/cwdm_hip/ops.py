@@ -26,6 +26,18 @@ def _need_cuda(*ts):
                                "(no CPU fallback in the product path)")
 
 
+def check_device_status(where):
+    """Raise if a kernel flagged a condition it could not return (cwdm_device_status,
+    e.g. an apply-ahead counter wait that ran out: that conv's output is invalid).
+    Synchronises the device: call once per sampling loop, not per step."""
+    st = lib().cwdm_device_status(1)
+    if st < 0:
+        check(st, where)
+    if st:
+        raise RuntimeError(f"{where}: device error word {st:#x} (CWDM_DEV_E_AA_TIMEOUT = 1: a persistent conv's "
+                           f"workgroups were not all resident; results of this call are invalid)")
+
+
 def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 

@@ -68,7 +68,7 @@ class FlatAdamW(torch.optim.Optimizer):
         args = (self._flat.data_ptr(), g.data_ptr(), self._m.data_ptr(), self._v.data_ptr(), self._flat.numel(),
                 float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), float(grp["weight_decay"]), self._step)
         if self.track_maxabs:
-            self.last_maxabs = torch.empty(2, device=self._flat.device)
+            self.last_maxabs = torch.empty(2, dtype=torch.float32, device=self._flat.device)
             check(lib().cwdm_adamw_maxabs(*args, self.last_maxabs.data_ptr(), _stream()), "AdamW.step")
         else:
             check(lib().cwdm_adamw(*args, _stream()), "AdamW.step")

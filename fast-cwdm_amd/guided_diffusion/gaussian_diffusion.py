@@ -475,6 +475,8 @@ class GaussianDiffusion:
                     new = th.empty_like(img)
                     pred = th.empty_like(img) if need_pred else None
                     step(img, new, pred, None)
+                    if i == indices[-1]:
+                        ops.check_device_status("p_sample_loop")
                     yield {"sample": new, "pred_xstart": pred}
                     img = new
                 return
@@ -502,6 +504,8 @@ class GaussianDiffusion:
                 t.fill_(i)
                 t_model.fill_(self._model_timestep(i))
                 graphs[n % 2].replay()
+                if n == len(indices) - 2:
+                    ops.check_device_status("p_sample_loop")
                 dst = bufs[0] if n % 2 == 0 else bufs[1]
                 yield {"sample": fresh(dst), "pred_xstart": fresh(pred)}
 

@@ -292,8 +292,9 @@ typedef struct {
   int accumulate;           /* out += result instead of out = result */
   const void* a_w_split;    /* fp32 convs (optional): cwdm_conv3d_pack_split weights -- the accurate fast
                                mode: the conv MFMAs run on bf16 hi/lo splits of the fp32 operands (every
-                               product hi.hi + lo.hi + hi.lo, fp32 accumulation; lo.lo is below fp32
-                               rounding) where the shape takes the warp-specialised kernel (a_c0, a_c1
+                               product hi.hi + lo.hi + hi.lo, fp32 accumulation; the dropped lo.lo term
+                               is ~2^-18 of each product, about 64x fp32 epsilon: see DESIGN.md §4)
+                               where the shape takes the warp-specialised kernel (a_c0, a_c1
                                multiples of 16); fp32 in, fp32 out */
 } cwdm_conv3d_desc;
 int64_t cwdm_conv3d_packed_bytes(int cout, int cin, int ksize, int dtype);
@@ -373,6 +374,21 @@ int cwdm_debug_v5_grid(int n);
  * for any eligible conv, 0 off; returns the previous setting.  -1: changes
  * nothing, returns the number of apply-ahead launches so far. */
 int cwdm_debug_v5_aa(int on);
+
+/* Diagnostics / tests only: make every apply-ahead counter wait require `extra`
+ * arrivals beyond the grid and give up after `spin` s_sleep rounds (0, 0 =
+ * defaults: no extra, 1 << 24 rounds) -- forces the timeout path, which must
+ * report CWDM_DEV_E_AA_TIMEOUT through cwdm_device_status. */
+int cwdm_debug_v5_aa_timeout(int extra, int spin);
+
+/* Device-side error word (sticky, OR of CWDM_DEV_E_* bits) set by kernels that
+ * detect a condition they cannot return (an apply-ahead counter wait that ran
+ * out: the workgroups of the persistent grid were not all resident, e.g. CUs
+ * held by another process or masked; the conv's output is then not valid).
+ * Synchronises the device; clear != 0 resets the word.  Returns the bits, or a
+ * negative CWDM_E_* code. */
+enum { CWDM_DEV_E_AA_TIMEOUT = 1 };
+int cwdm_device_status(int clear);
 
 /* Diagnostics / tests only: the fused GroupNorm finalize + pre-pass the plan
  * offers a small-level consumer conv (GnFinFuse): the finalize of

@@ -571,6 +571,75 @@ def test_conv3d_v5_apply_ahead_bitexact_vs_prepass(case, dtype_name):
         assert torch.equal(s0, s1), name
 
 
+def test_conv3d_v5_apply_ahead_timeout_reported():
+    """A counter wait of the apply-ahead sweep that runs out (forced here: every
+    wait needs one arrival more than the grid has, 256 sleep rounds) is reported
+    through the device error word (cwdm_device_status), not swallowed; the next
+    normal launch is clean and equals the pre-pass conv again.  A debug grid cap
+    above the CU count is clamped to what can be resident at once (the waits span
+    the whole grid)."""
+    from cwdm_hip._lib import check, lib
+    L = lib()
+    name, (D, H, W), c0, c1, cout, rmode, cap = AA_CASES[0]
+    dtype, tdt = _DTN["bf16"]
+    g = torch.Generator().manual_seed(29)
+    a0 = torch.randn(1, D, H, W, c0, generator=g).to(DEV, tdt)
+    w = (torch.randn(cout, c0, 3, 3, 3, generator=g) / math.sqrt(27 * c0)).to(DEV)
+    bias = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    gn = torch.stack([1 + 0.2 * torch.randn(1, c0, generator=g), 0.2 * torch.randn(1, c0, generator=g)],
+                     -1).contiguous().to(DEV)
+    res = torch.randn(1, D, H, W, cout, generator=g).to(DEV, tdt)
+    assert L.cwdm_device_status(1) >= 0
+    assert L.cwdm_device_status(0) == 0
+
+    def run(aa, capn):
+        prev, prevg, preva = L.cwdm_conv3d_set_path(2), L.cwdm_debug_v5_grid(capn), L.cwdm_debug_v5_aa(2 * aa)
+        try:
+            return _conv_call(dtype, (1, D, H, W), a0, None, 0, gn, w, bias, res=res, rmode=rmode)
+        finally:
+            L.cwdm_conv3d_set_path(prev)
+            L.cwdm_debug_v5_grid(prevg)
+            L.cwdm_debug_v5_aa(preva)
+
+    ref = run(0, cap)
+    n0 = L.cwdm_debug_v5_aa(-1)
+    check(L.cwdm_debug_v5_aa_timeout(1, 256))
+    try:
+        run(1, cap)
+    finally:
+        check(L.cwdm_debug_v5_aa_timeout(0, 0))
+    assert L.cwdm_debug_v5_aa(-1) - n0 == 1
+    st = L.cwdm_device_status(1)
+    assert st & 1, f"forced apply-ahead timeout not reported (status {st})"
+    assert L.cwdm_device_status(0) == 0
+    # clean again, bit-identical to the pre-pass conv
+    o, s = run(1, cap)
+    assert L.cwdm_device_status(0) == 0
+    assert torch.equal(o.view(torch.int16), ref[0].view(torch.int16))
+    assert torch.equal(s, ref[1])
+    # 512 tiles with the debug cap far above the CU count: the grid is clamped to what is resident
+    # (unclamped, 512 workgroups would wait on each other with only one per CU resident)
+    name, (D, H, W), c0, c1, cout, rmode, _ = AA_CASES[4]
+    a0 = torch.randn(1, D, H, W, c0, generator=g).to(DEV, tdt)
+    a1 = torch.randn(1, D, H, W, c1, generator=g).to(DEV, tdt)
+    w = (torch.randn(cout, c0 + c1, 3, 3, 3, generator=g) / math.sqrt(27 * (c0 + c1))).to(DEV)
+    bias = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    gn = torch.stack([1 + 0.2 * torch.randn(1, c0 + c1, generator=g), 0.2 * torch.randn(1, c0 + c1, generator=g)],
+                     -1).contiguous().to(DEV)
+    outs = []
+    for aa, capn in ((0, 0), (1, 1 << 20)):
+        prev, prevg, preva = L.cwdm_conv3d_set_path(2), L.cwdm_debug_v5_grid(capn), L.cwdm_debug_v5_aa(2 * aa)
+        try:
+            outs.append(_conv_call(dtype, (1, D, H, W), a0, a1, 0, gn, w, bias))
+        finally:
+            L.cwdm_conv3d_set_path(prev)
+            L.cwdm_debug_v5_grid(prevg)
+            L.cwdm_debug_v5_aa(preva)
+    assert L.cwdm_device_status(0) == 0
+    assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16))
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 SG_CASES = [
     # name, B, grid(out), c0, c1, cout, amode, gn, skip1x1, rmode  (16-bit; W < 32, cout % 64 == 0,
     # 32-channel K chunks: the small-grid kernel, conv3d_sg.hip, incl. its 1x1 skip mode and K split)
