@@ -82,7 +82,15 @@ struct SGParams {
   // streams or plans would share tiles' counters.
   unsigned* count;
   int xcd;   // 1: XCD-aware work map (below), 0: plain (env CWDM_SG_XCD=0, A/B)
+  int diag;  // timing-only diagnostics build (make SGDIAG=1, env CWDM_SG_DIAGMASK): SG_DIAG bits below
 };
+// timing-only diagnostics (results are garbage): 1 no MFMAs, 2 no halo DMA, 4 no weight DMA,
+// 8 no operand LDS reads
+#ifdef CWDM_SG_DIAG
+#define SG_DIAG(bit) ((q.diag & (bit)) != 0)
+#else
+#define SG_DIAG(bit) false
+#endif
 
 // counter block pre-zeroed by the caller (the U-Net plan, per forward /
 // backward, thread-local for the duration of its launch list) or null
@@ -145,6 +153,7 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   // all: 16-channel sub-chunk 2c + pc / (2 PCS), 32-slot block pc % (2 PCS)),
   // lane = (slot 32 blk + lane / 2, quad lane & 1)
   auto issue_halo = [&](int c, int hbuf) {
+    if (SG_DIAG(2)) return;
     unsigned char* hb = smem + hbuf * C::BUF;
 #pragma unroll
     for (int j = 0; j < C::PCS; ++j) {
@@ -186,6 +195,7 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.aw + (long long)ct64 * p.nch * TAPS * 2048), (short)0, p.nch * TAPS * 2048, 0x00020000);
   auto issue_w = [&](int c, int wbuf) {
+    if (SG_DIAG(4)) return;
     unsigned char* wb = smem + 2 * C::BUF + wbuf * C::WBUF;
     const unsigned cb = (unsigned)((2 * c + (kq >> 1)) * TAPS) * 2048u + wlane;
 #pragma unroll
@@ -223,6 +233,7 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
     const unsigned char* wb = smem + 2 * C::BUF + buf * C::WBUF + lane * 16;
     u32x4 av[2][C::NR], aw[2][3];
     auto read_group = [&](u32x4 (&a)[C::NR], u32x4 (&w)[3], int g) {
+      if (SG_DIAG(8)) return;
       const int dz = g / 3, dx = g % 3;
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy) w[dy] = *reinterpret_cast<const u32x4*>(wb + (dz * 9 + dy * 3 + dx) * 1024);
@@ -254,7 +265,8 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-          for (int m = 0; m < 4; ++m) sg_mfma(acc[m], aw[g & 1][dy], av[g & 1][m * C::LPO + dy], (T*)nullptr);
+          for (int m = 0; m < 4; ++m)
+            if (!SG_DIAG(1)) sg_mfma(acc[m], aw[g & 1][dy], av[g & 1][m * C::LPO + dy], (T*)nullptr);
         __builtin_amdgcn_sched_barrier(0);
       }
     } else {
@@ -546,6 +558,10 @@ int sg_go(const SGParams& q0, const cwdm_conv3d_desc* d, int taps, double flops,
   static const int xcd_map = [] { const char* e = std::getenv("CWDM_SG_XCD"); return !(e && e[0] == '0'); }();
   SGParams q = q0;
   q.xcd = xcd_map;
+#ifdef CWDM_SG_DIAG
+  static const int diag = [] { const char* e = std::getenv("CWDM_SG_DIAGMASK"); return e ? std::atoi(e) : 0; }();
+  q.diag = diag;
+#endif
   prof_begin(s);
   if (d->dtype == CWDM_F16) sg_go_t<f16_t>(q, d, taps, s);
   else sg_go_t<bf16_t>(q, d, taps, s);
