@@ -85,7 +85,8 @@ struct SGParams {
   int diag;  // timing-only diagnostics build (make SGDIAG=1, env CWDM_SG_DIAGMASK): SG_DIAG bits below
 };
 // timing-only diagnostics (results are garbage): 1 no MFMAs, 2 no halo DMA, 4 no weight DMA,
-// 8 no operand LDS reads
+// 8 no operand LDS reads, 16 no epilogue (return after the K loop), 32 no bias loads, 64 no K-split
+// hand-off (every slice runs the epilogue)
 #ifdef CWDM_SG_DIAG
 #define SG_DIAG(bit) ((q.diag & (bit)) != 0)
 #else
@@ -216,7 +217,7 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
     float bi[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      bi[i] = (p.bias && q.ksplit == 1) ? p.bias[(long long)b * p.bias_bs + t16 * 16 + 4 * kq + i] : 0.f;
+      bi[i] = (p.bias && q.ksplit == 1 && !SG_DIAG(32)) ? p.bias[(long long)b * p.bias_bs + t16 * 16 + 4 * kq + i] : 0.f;
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc[m] = sg_f32x4{bi[0], bi[1], bi[2], bi[3]};
   }
@@ -282,8 +283,9 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
     if (c - cb0 < 8) V4_STAMP(4 + c - cb0);
   }
   V4_STAMP(12);
+  if (SG_DIAG(16)) return;
 
-  if (q.ksplit > 1) {
+  if (q.ksplit > 1 && !SG_DIAG(64)) {
     // K split: publish this slice, the tile's last arrival finishes it.  Hand-off
     // across XCDs without fences: the in-launch split-K recipe of
     // cdna_hip_programming.md §5 item 2 ("sc1 (write-through) slab stores, which
