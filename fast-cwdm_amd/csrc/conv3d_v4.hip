@@ -627,8 +627,7 @@ struct ApplySkipParams {
   void* skip;          // [B][vpb][cout]
 };
 
-// DEPTH: blocks of x rows in flight in registers ahead of the one being computed (1 or 2)
-template <typename T, int NF, int QT, int DEPTH = 1>
+template <typename T, int NF, int QT>
 __global__ void __launch_bounds__(256) gn_apply_skip_kernel(ApplySkipParams p) {
   constexpr int CK = ConvTr<T>::CK, EPQ = ConvTr<T>::EPQ, ES = sizeof(T);
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -647,7 +646,7 @@ __global__ void __launch_bounds__(256) gn_apply_skip_kernel(ApplySkipParams p) {
   // the next block's 128 x rows are loaded into registers while this block
   // computes (consecutive lanes read consecutive 16-byte quads), then copied
   // to LDS: HBM latency hides under the MFMA / store work
-  u32x4 pfa[QT], pfb[QT];
+  u32x4 pf[QT];
   // quad i = tid + 256 j of a block: source 0 rows first (nq0 quads), then
   // source 1; its global offset within the block's rows is i (or i - nq0) x 16
   // bytes, its LDS offset (row vl, column) is fixed per thread: computed once,
@@ -663,7 +662,7 @@ __global__ void __launch_bounds__(256) gn_apply_skip_kernel(ApplySkipParams p) {
   }
   const unsigned char* xb0 = reinterpret_cast<const unsigned char*>(p.x0);
   const unsigned char* xb1 = reinterpret_cast<const unsigned char*>(p.x1);
-  auto fetch = [&](u32x4 (&pf)[QT], long long blk) {
+  auto fetch = [&](long long blk) {
     const unsigned char* s0 = xb0 + blk * 128 * q0 * 16;
     const unsigned char* s1 = xb1 + blk * 128 * q1 * 16 - (long long)nq0 * 16;
 #pragma unroll
@@ -673,29 +672,20 @@ __global__ void __launch_bounds__(256) gn_apply_skip_kernel(ApplySkipParams p) {
       pf[j] = *reinterpret_cast<const u32x4*>((i < nq0 ? s0 : s1) + (long long)i * 16);
     }
   };
-  auto put = [&](const u32x4 (&pf)[QT]) {
+  auto put = [&]() {
 #pragma unroll
     for (int j = 0; j < QT; ++j) {
       if (j >= nqt) break;
       *reinterpret_cast<u32x4*>(xt + loff[j]) = pf[j];
     }
   };
-  const long long G = gridDim.x;
-  if ((long long)blockIdx.x < nblocks) fetch(pfa, blockIdx.x);
-  if (DEPTH > 1 && (long long)blockIdx.x + G < nblocks) fetch(pfb, blockIdx.x + G);
-  // block n of this workgroup: its rows come from register set n % DEPTH, which is refilled with
-  // block n + DEPTH right after the rows land in LDS
-  for (long long blk = blockIdx.x, n = 0; blk < nblocks; blk += G, ++n) {
+  if ((long long)blockIdx.x < nblocks) fetch(blockIdx.x);
+  for (long long blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
     const long long v0 = blk * 128;
-    const bool setb = DEPTH > 1 && (n & 1);
     __syncthreads();  // previous block's column reads are done (and W / gn staged, first time)
-    if (setb) put(pfb);
-    else put(pfa);
+    put();
     __syncthreads();
-    if (blk + DEPTH * G < nblocks) {
-      if (setb) fetch(pfb, blk + DEPTH * G);
-      else fetch(pfa, blk + DEPTH * G);
-    }
+    if (blk + gridDim.x < nblocks) fetch(blk + gridDim.x);
     const int vl = wv * 32 + lr;
     const long long v = v0 + vl;
     const int b = (int)(v0 / p.vpb);
@@ -771,12 +761,6 @@ int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* g
   int rc;
   rc = dispatch_dtype(dtype, [&](auto tag) -> int {
     using T = decltype(tag);
-    // prefetch depth (env CWDM_SKIP_DEPTH, A/B knob): x rows of 1 or 2 blocks in flight in registers
-    static const int depth = [] { const char* e = std::getenv("CWDM_SKIP_DEPTH"); return e ? std::atoi(e) : 1; }();
-    // (two register sets: only where a block's rows fit 12 quads per thread, so the kernel keeps two
-    // waves per SIMD: the R0 decoder's 128- / 192-channel inputs with the 64-channel skip)
-    const int qt = (c0 + c1) * (int)sizeof(T) / 32;
-    if (depth >= 2 && cout == 64 && qt <= 12) return go(gn_apply_skip_kernel<T, 2, 12, 2>);
     return cout == 64 ? go(gn_apply_skip_kernel<T, 2, 16>) : go(gn_apply_skip_kernel<T, 4, 16>);
   });
   if (rc) return rc;
