@@ -323,7 +323,9 @@ bool gn_fin_fusable(const GnFinFuse& f, int dtype, int c0, int c1) {
   const int C = c0 + c1;
   if (!dtype_half(dtype) || C % 16 || c0 % 16 || f.c0 != c0 || f.c1 != c1 || f.groups <= 0 || C % f.groups) return false;
   const int cpg = C / f.groups;
-  return cpg <= 16 && 16 % cpg == 0 && f.p0 <= 256 && (c1 == 0 || f.p1 <= 256);
+  // (env CWDM_GNFIN_MAXV, A/B knob: the largest grid, in voxels, whose finalize the pre-pass takes)
+  static const long long maxv = [] { const char* e = std::getenv("CWDM_GNFIN_MAXV"); return e ? std::atoll(e) : (1LL << 40); }();
+  return cpg <= 16 && 16 % cpg == 0 && f.p0 <= 256 && (c1 == 0 || f.p1 <= 256) && f.voxels <= maxv;
 }
 
 int gn_fin_apply(const GnFinFuse& f, const void* x0, int c0, const void* x1, int c1, int64_t B, int64_t V, int dtype,

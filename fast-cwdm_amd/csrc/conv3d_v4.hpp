@@ -89,6 +89,10 @@ struct V4Params {
   unsigned* aa_cnt;   // this launch's sweep counters (kV5AaCnt words, zero at launch; the last workgroup out re-zeroes them)
   int aa_spin;        // bound of a counter wait (s_sleep rounds); a wait that runs out sets CWDM_DEV_E_AA_TIMEOUT
   int aa_extra;       // debug (cwdm_debug_v5_aa_timeout): arrivals a wait needs beyond the grid (forces the timeout path)
+  // warp-specialised conv, batch 1, <= 2 channel tiles: GroupNorm partials per WORKGROUP instead of per
+  // tile -- row blockIdx.x of stats holds the sums over the workgroup's tiles (in its tile order), every
+  // channel of the row written (zeros for a channel tile it never ran): gridDim.x rows for the finalize
+  int stats_wg;
 };
 
 

@@ -50,7 +50,8 @@ struct V5Cfg {
   static constexpr int SCR = BIAS + 512;                // statistics partials [4 helper][64 ch][2] fp32
   static constexpr int GSS = SCR + 2048;                // GroupNorm (sc, sh) [3 buffers][4 helpers][16 ch][2] fp32
   static constexpr int CNT = GSS + 1536;                // statistics arrival counters
-  static constexpr int SMEM = CNT + 256;                // 162048 of the CU's 163840
+  static constexpr int RUN = CNT + 256;                 // per-workgroup statistics (stats_wg): [2 ch tiles][64][2] fp32
+  static constexpr int SMEM = RUN + 1024;               // 163072 of the CU's 163840
 };
 static_assert(V5Cfg::SMEM <= 163840, "v5 LDS");
 
@@ -437,6 +438,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   const long long HW = (long long)p.H * p.W, VV = (long long)p.D * HW;
   const unsigned rowb = (unsigned)p.W * (unsigned)p.cout * 2u, planeb = (unsigned)HW * (unsigned)p.cout * 2u;
   float s1[8], s2[8];   // this lane's statistics over both drain parts of a tile
+  bool wg_final = false;   // stats_wg: the drain of this workgroup's last tile (writes the row)
   u32x4 dq[8];          // a drain slice's output rows and their byte offsets (drain -> drain_put)
   unsigned doff[8];
   // the residual rows of drain part `part` of tile tt (this lane's rows i = 8 part .. + 7): loaded
@@ -535,8 +537,22 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
         float su = 0.f, sq = 0.f;
 #pragma unroll
         for (int k = 0; k < 4; ++k) { su += s0[k * 128]; sq += s0[k * 128 + 1]; }
-        const long long pidx = ((long long)tt.b * tiles + tt.sl) * p.cout + tt.ct * 64 + lane;
-        *reinterpret_cast<float2*>(p.stats + pidx * 2) = make_float2(su, sq);
+        if (p.stats_wg) {
+          // this workgroup's running sums (its tiles in order: deterministic); the last tile's
+          // last arriver writes the row -- both channel tiles, zeros where it ran none
+          float2* run = reinterpret_cast<float2*>(smem + V5Cfg::RUN);
+          float2 r = run[tt.ct * 64 + lane];
+          r.x += su; r.y += sq;
+          run[tt.ct * 64 + lane] = r;
+          if (wg_final) {
+            for (int ct = 0; ct < p.nct; ++ct)
+              *reinterpret_cast<float2*>(p.stats + ((long long)blockIdx.x * p.cout + ct * 64 + lane) * 2) =
+                  run[ct * 64 + lane];
+          }
+        } else {
+          const long long pidx = ((long long)tt.b * tiles + tt.sl) * p.cout + tt.ct * 64 + lane;
+          *reinterpret_cast<float2*>(p.stats + pidx * 2) = make_float2(su, sq);
+        }
       }
     }
   };
@@ -584,6 +600,9 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
     };
     V4Tile cur = tile_of(0);
     if (h == 0 && lane == 0) *cnt = 0u;
+    if (p.stats_wg && h == 0) {
+      reinterpret_cast<float4*>(smem + V5Cfg::RUN)[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     issue_aa(0);
     issue_bias(cur, 0);
     issue_aa(1);
@@ -687,6 +706,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
     drain(dt, 0, (gch + 2) % 3, 0, 8);
     drain_put(dt, 0, 8);
     drain_load(dt, 1);
+    wg_final = true;
     drain(dt, 1, 0, 0, 8);
     drain_put(dt, 0, 8);
     V5_STAMP(52, tid == 256);
@@ -707,6 +727,9 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   // prologue: chunk 0 and tile 0's bias, chunk 1; transform chunk 0
   V4Tile cur = tile_of(0);
   if (h == 0 && lane == 0) *cnt = 0u;
+  if (p.stats_wg && h == 0) {
+    reinterpret_cast<float4*>(smem + V5Cfg::RUN)[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   issue_next(0);
   issue_bias(cur, 0);
   issue_next(1);
@@ -789,6 +812,7 @@ __global__ void __launch_bounds__(512) conv3d_v5_kernel(V4Params p) {
   drain(dt, 0, (gch + 2) % 3, 0, 8);
   drain_put(dt, 0, 8);
   drain_load(dt, 1);
+  wg_final = true;
   drain(dt, 1, 0, 0, 8);
   drain_put(dt, 0, 8);
   V5_STAMP(52, tid == 256);
@@ -1141,6 +1165,10 @@ int64_t v4_items(const cwdm_conv3d_desc* d);
 bool gbwd_grid_ok(const cwdm_conv3d_desc* d);
 std::atomic<int> g_v5_aa_extra{0};
 std::atomic<int> g_v5_aa_spin{0};
+// the U-Net plan asks for per-workgroup GroupNorm partials (V4Params::stats_wg) around its convs and
+// reads back how many rows a launch wrote (0: the per-tile layout of cwdm_conv3d_parts)
+thread_local int g_stats_wg = 0;
+thread_local int64_t g_stats_rows = 0;
 
 namespace {
 int v5_ncu() {
@@ -1319,6 +1347,13 @@ int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   }();
   const int cap = g_v5_grid.load(std::memory_order_relaxed);
   const dim3 grid(aa ? (unsigned)v5_aa_grid(nblk) : (unsigned)std::min<long long>(nblk, cap > 0 ? cap : ncu));
+  // per-workgroup statistics rows (16-bit kernel, batch 1, <= 2 channel tiles, no more rows than the
+  // per-tile layout has): the finalize then reduces gridDim.x rows instead of one per tile
+  if (g_stats_wg && d->stats && d->dtype != CWDM_F32 && p.B == 1 && p.nct <= 2 &&
+      (long long)grid.x <= (long long)p.tx * p.ty * p.tz) {
+    p.stats_wg = 1;
+    g_stats_rows = grid.x;
+  }
   prof_begin(s);
   auto go = [&](auto tag) {
     using T = decltype(tag);

@@ -629,6 +629,8 @@ int gn_apply_skip(const void* x0, int c0, const void* x1, int c1, const float* g
 int v4_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1, int c1, int a0_cm,
               const void* res, int rmode, void* partial, hipStream_t s);
 extern thread_local unsigned* g_sg_sync;
+extern thread_local int g_stats_wg;         // conv3d_v5.hip: per-workgroup GroupNorm partials wanted
+extern thread_local int64_t g_stats_rows;   // ... and the rows the last launch wrote (0: per tile)
 int64_t sg_sync_bytes(int ksplit);
 int64_t plan_sync_bytes();
 bool head_eligible(const cwdm_conv3d_desc* d);
@@ -1122,13 +1124,21 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
   // first).  A pending one whose consumer is not the next step runs on its own.
   // Env CWDM_GNFIN=0: every finalize as its own launch (A/B switch).
   static const bool fin_on = [] { const char* e = std::getenv("CWDM_GNFIN"); return !(e && e[0] == '0'); }();
+  // statistics partial rows per tensor: the per-tile layout, or the rows of a warp-specialised conv
+  // that summed them per workgroup (cwdm::g_stats_rows; env CWDM_STATS_WG=0: per tile everywhere)
+  static const int stats_wg = [] { const char* e = std::getenv("CWDM_STATS_WG"); return !(e && e[0] == '0'); }();
+  std::vector<int64_t> srows(L.s_parts);
+  struct StatsWgScope {
+    StatsWgScope() { cwdm::g_stats_wg = stats_wg; cwdm::g_stats_rows = 0; }
+    ~StatsWgScope() { cwdm::g_stats_wg = 0; cwdm::g_stats_rows = 0; }
+  } stats_wg_scope;
   int fin_pend = -1;
   auto fin_args = [&](int gi, cwdm::GnFinFuse& f) {
     const auto& g = u->gns[gi];
-    f.s0 = reinterpret_cast<const float*>(wb + L.s_off[g.src0]); f.p0 = L.s_parts[g.src0];
+    f.s0 = reinterpret_cast<const float*>(wb + L.s_off[g.src0]); f.p0 = srows[g.src0];
     f.c0 = u->tensors[g.src0].channels;
     f.s1 = g.src1 >= 0 ? reinterpret_cast<const float*>(wb + L.s_off[g.src1]) : nullptr;
-    f.p1 = g.src1 >= 0 ? L.s_parts[g.src1] : 0; f.c1 = g.src1 >= 0 ? u->tensors[g.src1].channels : 0;
+    f.p1 = g.src1 >= 0 ? srows[g.src1] : 0; f.c1 = g.src1 >= 0 ? u->tensors[g.src1].channels : 0;
     f.gamma = P(g.gamma_off); f.beta = P(g.beta_off); f.groups = u->cfg.num_groups;
     f.voxels = (D >> g.level) * (H >> g.level) * (W >> g.level); f.eps = 1e-5f;
     f.ss = reinterpret_cast<float*>(wb + L.ss_off[g.ss_id]); f.mr = reinterpret_cast<float*>(wb + L.mr_off[g.ss_id]);
@@ -1311,6 +1321,10 @@ static int unet_forward_impl(cwdm_unet* u, const void* packed, const void* x, co
         CWDM_REQUIRE(!ks.ptr || ks.used(), CWDM_E_INVALID,
                      "cwdm_unet_forward: conv " + std::to_string(st.idx) + " did not keep its activated input");
       }
+    }
+    if (cwdm::g_stats_rows > 0) {
+      if (cs.out >= 0) srows[cs.out] = cwdm::g_stats_rows;
+      cwdm::g_stats_rows = 0;
     }
     if (u->profiling) {
       cwdm::g_prof = nullptr;
