@@ -323,8 +323,11 @@ bool gn_fin_fusable(const GnFinFuse& f, int dtype, int c0, int c1) {
   const int C = c0 + c1;
   if (!dtype_half(dtype) || C % 16 || c0 % 16 || f.c0 != c0 || f.c1 != c1 || f.groups <= 0 || C % f.groups) return false;
   const int cpg = C / f.groups;
-  // (env CWDM_GNFIN_MAXV, A/B knob: the largest grid, in voxels, whose finalize the pre-pass takes)
-  static const long long maxv = [] { const char* e = std::getenv("CWDM_GNFIN_MAXV"); return e ? std::atoll(e) : (1LL << 40); }();
+  // the largest grid, in voxels, whose finalize the pre-pass takes (env CWDM_GNFIN_MAXV, A/B knob):
+  // 32^3 -- with per-workgroup partials the 64^3 / 128^3 finalizes qualify too, but the fused pass
+  // (~512 workgroups, each re-reducing its chunk's partials) streams the big grids far below the plain
+  // pre-pass: r06 same box, 15.33 ms per step without the fusion there vs 15.52 (64^3) / 15.96 (128^3)
+  static const long long maxv = [] { const char* e = std::getenv("CWDM_GNFIN_MAXV"); return e ? std::atoll(e) : 32768LL; }();
   return cpg <= 16 && 16 % cpg == 0 && f.p0 <= 256 && (c1 == 0 || f.p1 <= 256) && f.voxels <= maxv;
 }
 
