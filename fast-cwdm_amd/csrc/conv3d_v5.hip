@@ -848,7 +848,8 @@ struct V5sCfg {
   static constexpr int SCR = BIAS + 512;         // statistics partials
   static constexpr int GSS = SCR + 2048;         // GroupNorm (sc, sh) [4 buffers][4 helpers][8 ch][2] fp32 (128 B rows)
   static constexpr int CNT = GSS + 2048;         // statistics arrival counters
-  static constexpr int SMEM = CNT + 256;         // 161536 of the CU's 163840
+  static constexpr int RUN = CNT + 256;          // per-workgroup statistics (stats_wg): [2 ch tiles][64][2] fp32
+  static constexpr int SMEM = RUN + 1024;        // 162560 of the CU's 163840
 };
 static_assert(V5sCfg::SMEM <= 163840, "v5s LDS");
 
@@ -1023,8 +1024,21 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
               const int h2 = (lane >> 2) & 1, i = 4 * (lane >> 3) + (lane & 3);
               const float* s0 = reinterpret_cast<const float*>(smem + S::SCR) + f * 64 + h2 * 16 + i;
               const float su = s0[0] + s0[32], sq = s0[256] + s0[256 + 32];
-              const long long pidx = ((long long)cur.b * tiles + cur.sl) * p.cout + c0w + lane;
-              *reinterpret_cast<float2*>(p.stats + pidx * 2) = make_float2(su, sq);
+              if (p.stats_wg) {
+                // per-workgroup running sums (tile order: deterministic); the last tile writes the row,
+                // both channel tiles (zeros where this workgroup ran none)
+                float2* run = reinterpret_cast<float2*>(smem + S::RUN);
+                float2 r = run[cur.ct * 64 + f * 32 + lane];
+                r.x += su; r.y += sq;
+                run[cur.ct * 64 + f * 32 + lane] = r;
+                if (it + 1 == ntile)
+                  for (int ct = 0; ct < p.nct; ++ct)
+                    *reinterpret_cast<float2*>(p.stats + ((long long)blockIdx.x * p.cout + ct * 64 + f * 32 + lane) * 2) =
+                        run[ct * 64 + f * 32 + lane];
+              } else {
+                const long long pidx = ((long long)cur.b * tiles + cur.sl) * p.cout + c0w + lane;
+                *reinterpret_cast<float2*>(p.stats + pidx * 2) = make_float2(su, sq);
+              }
             }
           }
         }
@@ -1116,6 +1130,7 @@ __global__ void __launch_bounds__(512) conv3d_v5s_kernel(V4Params p) {
   };
   V4Tile cur = tile_of(0);
   if (h == 0 && lane < 2) cnt[lane] = 0u;
+  if (p.stats_wg && h == 0) reinterpret_cast<float4*>(smem + S::RUN)[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
   issue_pair(0);
   issue_bias(cur, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1349,7 +1364,7 @@ int v5_launch(const cwdm_conv3d_desc* d, const void* a0, int c0, const void* a1,
   const dim3 grid(aa ? (unsigned)v5_aa_grid(nblk) : (unsigned)std::min<long long>(nblk, cap > 0 ? cap : ncu));
   // per-workgroup statistics rows (16-bit kernel, batch 1, <= 2 channel tiles, no more rows than the
   // per-tile layout has): the finalize then reduces gridDim.x rows instead of one per tile
-  if (g_stats_wg && d->stats && d->dtype != CWDM_F32 && p.B == 1 && p.nct <= 2 &&
+  if (g_stats_wg && d->stats && p.B == 1 && p.nct <= 2 &&
       (long long)grid.x <= (long long)p.tx * p.ty * p.tz) {
     p.stats_wg = 1;
     g_stats_rows = grid.x;

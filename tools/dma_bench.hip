@@ -11,7 +11,9 @@
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-template <int FORM, int NI>
+// NR > 0: after issuing a round's fills every wave also runs NR ds_read_b128 of the previous round's
+// image (the small-grid conv's MFMA-phase operand traffic) before it waits for the fills
+template <int FORM, int NI, int NR = 0>
 __global__ void __launch_bounds__(256) fill(const unsigned char* src, unsigned long long src_bytes, int rounds,
                                             unsigned* sink) {
   __shared__ __attribute__((aligned(1024))) unsigned char sm[144 * 1024];
@@ -36,6 +38,15 @@ __global__ void __launch_bounds__(256) fill(const unsigned char* src, unsigned l
         *reinterpret_cast<u32x4*>(dst + lane * 16) = v;
       }
     }
+    if constexpr (NR > 0) {
+      u32x4 t = {0u, 0u, 0u, 0u};
+#pragma unroll 8
+      for (int k = 0; k < NR; ++k) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(sm + ((wv * NR + k) * 1024 + lane * 16) % (144 * 1024));
+        t ^= v;
+      }
+      acc += t[0] ^ t[1] ^ t[2] ^ t[3];
+    }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
     acc += *reinterpret_cast<const unsigned*>(sm + (tid * 64) % (144 * 1024));
@@ -44,15 +55,15 @@ __global__ void __launch_bounds__(256) fill(const unsigned char* src, unsigned l
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
-template <int FORM, int NI>
+template <int FORM, int NI, int NR = 0>
 double run(const unsigned char* src, unsigned long long bytes, int grid, unsigned* sink) {
   const int rounds = 200;
-  hipLaunchKernelGGL((fill<FORM, NI>), dim3(grid), dim3(256), 0, 0, src, bytes, 4, sink);
+  hipLaunchKernelGGL((fill<FORM, NI, NR>), dim3(grid), dim3(256), 0, 0, src, bytes, 4, sink);
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
   hipEventRecord(a, 0);
-  hipLaunchKernelGGL((fill<FORM, NI>), dim3(grid), dim3(256), 0, 0, src, bytes, rounds, sink);
+  hipLaunchKernelGGL((fill<FORM, NI, NR>), dim3(grid), dim3(256), 0, 0, src, bytes, rounds, sink);
   hipEventRecord(b, 0);
   hipEventSynchronize(b);
   float ms = 0;
@@ -79,5 +90,13 @@ int main() {
              run<2, 16>(src, sizes[si], grid, sink), run<3, 16>(src, sizes[si], grid, sink));
     }
   }
+  // contention: 16 fills per wave in flight while the wave reads NR x 1 KB of LDS (the small-grid conv
+  // reads ~81 per wave per chunk in its MFMA phase), 64 MB source
+  printf("64MB(MALL)  grid 256  NI=16 buf, LDS reads per wave per round: 0 %.1f | 32 %.1f | 81 %.1f | 160 %.1f GB/s per CU\n",
+         run<0, 16, 0>(src, sizes[1], 256, sink), run<0, 16, 32>(src, sizes[1], 256, sink),
+         run<0, 16, 81>(src, sizes[1], 256, sink), run<0, 16, 160>(src, sizes[1], 256, sink));
+  printf("2MB(L2)     grid 256  NI=16 buf, LDS reads per wave per round: 0 %.1f | 32 %.1f | 81 %.1f | 160 %.1f GB/s per CU\n",
+         run<0, 16, 0>(src, sizes[0], 256, sink), run<0, 16, 32>(src, sizes[0], 256, sink),
+         run<0, 16, 81>(src, sizes[0], 256, sink), run<0, 16, 160>(src, sizes[0], 256, sink));
   return 0;
 }
