@@ -37,7 +37,7 @@ for _p in (os.path.join(ROOT, "fast-cwdm_amd"), ROOT):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r05", "r04", "r03", "r02", "r01")]
+TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r06", "r05", "r04", "r03", "r02", "r01")]
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3
 
