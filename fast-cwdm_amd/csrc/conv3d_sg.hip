@@ -110,20 +110,13 @@ __device__ __forceinline__ void sg_mfma(sg_f32x4& acc, const u32x4& a, const u32
 // TAPS = 27: the 3x3x3 conv; TAPS = 1: the 1x1 skip conv of a ResBlock (the
 // centre tap of the same halo image and weight buffer, packed with k = 1).
 // T: the 16-bit storage type (bf16 or fp16; v_mfma_f32_16x16x32_{bf16,f16})
-// WR (3x3x3 only): the A fragments go straight to registers by ordinary loads -- all 27 taps of the
-// next chunk in flight during the current chunk's MFMAs, each tap reloaded right after its last use --
-// instead of through LDS.  Why: the LDS-DMA fills and the MFMA phase's LDS operand reads serialize on
-// the CU's LDS (tools/dma_bench.hip: a 64 KB fill with 81 KB of reads per wave runs at half the rate
-// of the fill alone), and the weights were 27 of each chunk's 72 KB of fills and 108 of its 324 KB of
-// reads (every wave read the same fragments)
-template <typename T, int BX, int BY, int MODE, int TAPS, bool WR = false>
+template <typename T, int BX, int BY, int MODE, int TAPS>
 __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   static_assert(TAPS == 27 || TAPS == 1, "3x3x3 or 1x1");
   constexpr int PAD = TAPS == 27 ? 1 : 0;
-  constexpr bool WREG = WR && TAPS == 27;
   using C = SGCfg<BX, BY, PAD>;
   const V4Params& p = q.v;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[WREG ? 2 * C::BUF : C::SMEM];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, kq = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   V4_STAMP(0);
@@ -202,16 +195,8 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
   const unsigned wlane = (unsigned)(row * 32 + (((kq & 1) ^ ((row >> 3) & 1)) << 4));
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.aw + (long long)ct64 * p.nch * TAPS * 2048), (short)0, p.nch * TAPS * 2048, 0x00020000);
-  // the register path: tap t of chunk c, this lane's 16 B of the packed A fragment.  Compiler-invisible
-  // asm loads, issued straight-line and retired only by the chunk-end wait that names every wf register
-  // (SG_WAIT_WF): a compiler-tracked load used a chunk later made the compiler wait vmcnt(1) inside the
-  // MFMA phase -- for the next chunk's halo DMA too
-  auto wload = [&](u32x4& dst, int c, int t) {
-    const unsigned char* base = p.aw + (long long)ct64 * p.nch * TAPS * 2048;
-    v4_gload(dst, base + (size_t)((2 * c + (kq >> 1)) * TAPS + t) * 2048u + wlane);
-  };
   auto issue_w = [&](int c, int wbuf) {
-    if (WREG || SG_DIAG(4)) return;
+    if (SG_DIAG(4)) return;
     unsigned char* wb = smem + 2 * C::BUF + wbuf * C::WBUF;
     const unsigned cb = (unsigned)((2 * c + (kq >> 1)) * TAPS) * 2048u + wlane;
 #pragma unroll
@@ -237,25 +222,9 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
     for (int m = 0; m < 4; ++m) acc[m] = sg_f32x4{bi[0], bi[1], bi[2], bi[3]};
   }
 
-  u32x4 wf[WREG ? 27 : 1];
-#define SG_WAIT_WF()                                                                                          \
-  asm volatile("s_waitcnt vmcnt(0)"                                                                           \
-               : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]), "+v"(wf[5]), "+v"(wf[6]),   \
-                 "+v"(wf[7]), "+v"(wf[8]), "+v"(wf[9]), "+v"(wf[10]), "+v"(wf[11]), "+v"(wf[12]),            \
-                 "+v"(wf[13]), "+v"(wf[14]), "+v"(wf[15]), "+v"(wf[16]), "+v"(wf[17]), "+v"(wf[18]),          \
-                 "+v"(wf[19]), "+v"(wf[20]), "+v"(wf[21]), "+v"(wf[22]), "+v"(wf[23]), "+v"(wf[24]),          \
-                 "+v"(wf[25]), "+v"(wf[26])                                                                   \
-               :                                                                                              \
-               : "memory")
   issue_halo(cb0, 0);
   issue_w(cb0, 0);
-  if constexpr (WREG) {
-#pragma unroll
-    for (int t = 0; t < 27; ++t) wload(wf[t], cb0, t);
-    SG_WAIT_WF();
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   V4_STAMP(1);
   for (int c = cb0; c < cb1; ++c) {
@@ -267,12 +236,8 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
     auto read_group = [&](u32x4 (&a)[C::NR], u32x4 (&w)[3], int g) {
       if (SG_DIAG(8)) return;
       const int dz = g / 3, dx = g % 3;
-      if constexpr (!WREG) {
 #pragma unroll
-        for (int dy = 0; dy < 3; ++dy) w[dy] = *reinterpret_cast<const u32x4*>(wb + (dz * 9 + dy * 3 + dx) * 1024);
-      } else {
-        (void)w;
-      }
+      for (int dy = 0; dy < 3; ++dy) w[dy] = *reinterpret_cast<const u32x4*>(wb + (dz * 9 + dy * 3 + dx) * 1024);
 #pragma unroll
       for (int s = 0; s < C::NR; ++s)
         a[s] = *reinterpret_cast<const u32x4*>(hb + ((dz * C::HY + s) * C::HX + dx) * 32);
@@ -302,27 +267,17 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
         for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
           for (int m = 0; m < 4; ++m)
-            if (!SG_DIAG(1))
-              sg_mfma(acc[m], WREG ? wf[(g / 3) * 9 + dy * 3 + g % 3] : aw[g & 1][dy], av[g & 1][m * C::LPO + dy],
-                      (T*)nullptr);
+            if (!SG_DIAG(1)) sg_mfma(acc[m], aw[g & 1][dy], av[g & 1][m * C::LPO + dy], (T*)nullptr);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (WREG) {
-          // this group's taps are free: the next chunk's go in (a whole chunk of latency to hide); the
-          // last chunk reloads its own (straight-line: no branch between an asm load and its wait)
-          const int cn = has_next ? c + 1 : c;
-#pragma unroll
-          for (int dy = 0; dy < 3; ++dy) wload(wf[(g / 3) * 9 + dy * 3 + g % 3], cn, (g / 3) * 9 + dy * 3 + g % 3);
-        }
       }
     } else {
 #pragma unroll
       for (int m = 0; m < 4; ++m) sg_mfma(acc[m], aw[0][0], av[0][m * C::LPO], (T*)nullptr);
     }
-    if constexpr (WREG) SG_WAIT_WF();   // (the last chunk's dummy reloads too)
     if (has_next) {
       // the next chunk's halo and weights have landed; every wave is past this
       // chunk's reads of the buffers the chunk after next will fill
-      if constexpr (!WREG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
     if (c - cb0 < 8) V4_STAMP(4 + c - cb0);
@@ -484,14 +439,6 @@ template __global__ void conv3d_sg_kernel<f16_t, 16, 4, 0, 1>(SGParams);
 template __global__ void conv3d_sg_kernel<f16_t, 8, 8, 0, 27>(SGParams);
 template __global__ void conv3d_sg_kernel<f16_t, 8, 8, 1, 27>(SGParams);
 template __global__ void conv3d_sg_kernel<f16_t, 8, 8, 0, 1>(SGParams);
-template __global__ void conv3d_sg_kernel<bf16_t, 16, 4, 0, 27, true>(SGParams);
-template __global__ void conv3d_sg_kernel<bf16_t, 16, 4, 1, 27, true>(SGParams);
-template __global__ void conv3d_sg_kernel<bf16_t, 8, 8, 0, 27, true>(SGParams);
-template __global__ void conv3d_sg_kernel<bf16_t, 8, 8, 1, 27, true>(SGParams);
-template __global__ void conv3d_sg_kernel<f16_t, 16, 4, 0, 27, true>(SGParams);
-template __global__ void conv3d_sg_kernel<f16_t, 16, 4, 1, 27, true>(SGParams);
-template __global__ void conv3d_sg_kernel<f16_t, 8, 8, 0, 27, true>(SGParams);
-template __global__ void conv3d_sg_kernel<f16_t, 8, 8, 1, 27, true>(SGParams);
 
 extern std::atomic<int> g_conv_path;
 // set by the U-Net plan around the accurate fast mode's K-expanded small-grid convs: a 16-bit conv
@@ -595,26 +542,17 @@ template <typename T>
 void sg_go_t(const SGParams& q, const cwdm_conv3d_desc* d, int taps, hipStream_t s) {
   const dim3 grid((unsigned)(d->B * q.parts * q.ntile16 * q.ksplit));
   const bool w8 = sg_geom(d).bx == 8;
-  // A fragments in registers (env CWDM_SG_WREG=0: through LDS, the r02-r05 kernel; A/B knob)
-  static const bool wreg = [] { const char* e = std::getenv("CWDM_SG_WREG"); return !(e && e[0] == '0'); }();
   if (w8 && taps == 1) {
     hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 0, 1>), grid, dim3(256), 0, s, q);
   } else if (w8) {
-    if (q.v.amode == 1) {
-      if (wreg) hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 1, 27, true>), grid, dim3(256), 0, s, q);
-      else hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 1, 27>), grid, dim3(256), 0, s, q);
-    } else {
-      if (wreg) hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 0, 27, true>), grid, dim3(256), 0, s, q);
-      else hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 0, 27>), grid, dim3(256), 0, s, q);
-    }
+    if (q.v.amode == 1) hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 1, 27>), grid, dim3(256), 0, s, q);
+    else hipLaunchKernelGGL((conv3d_sg_kernel<T, 8, 8, 0, 27>), grid, dim3(256), 0, s, q);
   } else if (taps == 1) {
     hipLaunchKernelGGL((conv3d_sg_kernel<T, 16, 4, 0, 1>), grid, dim3(256), 0, s, q);
   } else if (q.v.amode == 1) {
-    if (wreg) hipLaunchKernelGGL((conv3d_sg_kernel<T, 16, 4, 1, 27, true>), grid, dim3(256), 0, s, q);
-    else hipLaunchKernelGGL((conv3d_sg_kernel<T, 16, 4, 1, 27>), grid, dim3(256), 0, s, q);
+    hipLaunchKernelGGL((conv3d_sg_kernel<T, 16, 4, 1, 27>), grid, dim3(256), 0, s, q);
   } else {
-    if (wreg) hipLaunchKernelGGL((conv3d_sg_kernel<T, 16, 4, 0, 27, true>), grid, dim3(256), 0, s, q);
-    else hipLaunchKernelGGL((conv3d_sg_kernel<T, 16, 4, 0, 27>), grid, dim3(256), 0, s, q);
+    hipLaunchKernelGGL((conv3d_sg_kernel<T, 16, 4, 0, 27>), grid, dim3(256), 0, s, q);
   }
 }
 
