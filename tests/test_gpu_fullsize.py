@@ -362,10 +362,11 @@ def test_fullsize_training_step_half_close_to_fp32():
         del model, terms, loss
         torch.cuda.empty_cache()
     l32, g32, f32 = res["fp32"]
-    # measured (r06): bf16 loss 1.1e-4, flat gradient 4.5e-3, per-parameter median
-    # 1.22e-2, worst 2.41e-2 (input_blocks.11.0.in_layers.0.weight); bounds ~2x the measured values
+    # measured (r06): bf16 loss 1.1e-4, flat gradient 4.4-4.5e-3, per-parameter median
+    # 1.21-1.22e-2, worst 2.3-2.4e-2 (GroupNorm affine weights of the 8^3-16^3 blocks); fp16 loss 8.4e-5,
+    # flat 5.2e-4, median 1.21e-3, worst 2.6e-3; bounds ~2x the measured values
     bounds = {"bf16": dict(loss=5e-4, flat=1e-2, median=2.5e-2, worst=5e-2),
-              "fp16": dict(loss=5e-4, flat=1e-2, median=2.5e-2, worst=5e-2)}
+              "fp16": dict(loss=5e-4, flat=1.5e-3, median=3e-3, worst=6e-3)}
     for dt, bd in bounds.items():
         lh, gh, fh = res[dt]
         lrel = abs(lh - l32) / abs(l32)
