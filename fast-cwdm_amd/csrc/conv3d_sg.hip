@@ -83,6 +83,10 @@ struct SGParams {
   unsigned* count;
   int xcd;   // 1: XCD-aware work map (below), 0: plain (env CWDM_SG_XCD=0, A/B)
   int diag;  // timing-only diagnostics build (make SGDIAG=1, env CWDM_SG_DIAGMASK): SG_DIAG bits below
+  // 3x3x3: the next chunk's fills go out after (dz, dx) group `late` - 1 of this chunk's MFMA phase
+  // (0: before it).  The fills and the MFMA phase's LDS operand reads serialize on the CU's LDS
+  // (tools/dma_bench.hip), so overlapping them is not free (env CWDM_SG_LATE, A/B knob)
+  int late;
 };
 // timing-only diagnostics (results are garbage): 1 no MFMAs, 2 no halo DMA, 4 no weight DMA,
 // 8 no operand LDS reads, 16 no epilogue (return after the K loop), 32 no bias loads, 64 no K-split
@@ -254,7 +258,8 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
     }
     // the next chunk's halo and weights go to the other buffers (last read by
     // chunk c - 1, which every wave finished before the previous barrier)
-    if (has_next) {
+    const int late = TAPS == 27 ? q.late : 0;
+    if (has_next && late == 0) {
       issue_halo(c + 1, buf ^ 1);
       issue_w(c + 1, buf ^ 1);
     }
@@ -269,6 +274,10 @@ __global__ void __launch_bounds__(256) conv3d_sg_kernel(SGParams q) {
           for (int m = 0; m < 4; ++m)
             if (!SG_DIAG(1)) sg_mfma(acc[m], aw[g & 1][dy], av[g & 1][m * C::LPO + dy], (T*)nullptr);
         __builtin_amdgcn_sched_barrier(0);
+        if (has_next && late == g + 1) {
+          issue_halo(c + 1, buf ^ 1);
+          issue_w(c + 1, buf ^ 1);
+        }
       }
     } else {
 #pragma unroll
@@ -560,6 +569,8 @@ int sg_go(const SGParams& q0, const cwdm_conv3d_desc* d, int taps, double flops,
   static const int xcd_map = [] { const char* e = std::getenv("CWDM_SG_XCD"); return !(e && e[0] == '0'); }();
   SGParams q = q0;
   q.xcd = xcd_map;
+  static const int late = [] { const char* e = std::getenv("CWDM_SG_LATE"); return e ? std::atoi(e) : 0; }();
+  q.late = late < 0 ? 0 : (late > 9 ? 9 : late);
 #ifdef CWDM_SG_DIAG
   static const int diag = [] { const char* e = std::getenv("CWDM_SG_DIAGMASK"); return e ? std::atoi(e) : 0; }();
   q.diag = diag;
