@@ -569,7 +569,9 @@ int sg_go(const SGParams& q0, const cwdm_conv3d_desc* d, int taps, double flops,
   static const int xcd_map = [] { const char* e = std::getenv("CWDM_SG_XCD"); return !(e && e[0] == '0'); }();
   SGParams q = q0;
   q.xcd = xcd_map;
-  static const int late = [] { const char* e = std::getenv("CWDM_SG_LATE"); return e ? std::atoi(e) : 0; }();
+  // default 4: after the 4th of 9 groups (r06 same box: 16^3 convs 567 -> 523 us per step, 8^3 347 -> 332,
+  // 15.36 -> 15.28 ms; conv_bench 16^3 -8 %, all-after-the-phase (9) -5 %)
+  static const int late = [] { const char* e = std::getenv("CWDM_SG_LATE"); return e ? std::atoi(e) : 4; }();
   q.late = late < 0 ? 0 : (late > 9 ? 9 : late);
 #ifdef CWDM_SG_DIAG
   static const int diag = [] { const char* e = std::getenv("CWDM_SG_DIAGMASK"); return e ? std::atoi(e) : 0; }();
