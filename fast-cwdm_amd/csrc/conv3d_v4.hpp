@@ -141,6 +141,11 @@ __device__ __forceinline__ void v4_gload(u32x4& dst, const unsigned char* src) {
 #else
 #define V4_STAMP(k) do { } while (0)
 #endif
+// the (dz, dx) weight group of a chunk after whose weight loads the next chunk's halo DMA goes out
+// (1..7; a build knob: the fills and the MFMA phase's LDS operand reads serialize on the CU's LDS)
+#ifndef V4_HALO_GI
+#define V4_HALO_GI 1
+#endif
 #define V4_WAIT_W(n, w) \
   asm volatile("s_waitcnt vmcnt(" #n ")" : "+v"((w)[0]), "+v"((w)[1]), "+v"((w)[2]) :: "memory")
 
@@ -705,14 +710,16 @@ __global__ void __launch_bounds__(256, 2) conv3d_v4_kernel(V4Params p) {
           /* group: a load nobody waits for would land in registers the epilogue reuses */                    \
           if (GI + 1 < 9) load_w(wr[(GI + 1) % 3], cur.ct, c, GI + 1);                                        \
           else if (!LAST) load_w(wr[(GI + 1) % 3], cur.ct, c + 1, 0);                                         \
-          if (GI == 1 && has_next) issue_halo(cur, c + 1, (gch + 1) & 1);                                     \
+          if (GI == V4_HALO_GI && has_next) issue_halo(cur, c + 1, (gch + 1) & 1);                            \
         }                                                                                                     \
         if (KN < 18) v4_read_step<KN % 18>(av[BC ^ 1], hb);                                                   \
         /* W(G) is retired with the younger weight group (and at group 2 the next */                          \
         /* chunk's halo pieces) still in flight; W(0) landed before the chunk */                              \
-        if (PL == 0 && GI == 1) { if (has_next) V4_WAIT_W(13, wr[1]); else V4_WAIT_W(3, wr[1]); }             \
-        if (PL == 0 && GI == 2) { if (has_next) V4_WAIT_W(13, wr[2]); else V4_WAIT_W(3, wr[2]); }             \
-        if (PL == 0 && GI >= 3 && (GI < 8 || !LAST)) V4_WAIT_W(3, wr[GI % 3]);                                \
+        /* (the halo's 10 pieces are younger than W(GI) at groups V4_HALO_GI and V4_HALO_GI + 1) */           \
+        if (PL == 0 && GI >= 1 && (GI < 8 || !LAST)) {                                                        \
+          if (has_next && (GI == V4_HALO_GI || GI == V4_HALO_GI + 1)) V4_WAIT_W(13, wr[GI % 3]);              \
+          else V4_WAIT_W(3, wr[GI % 3]);                                                                      \
+        }                                                                                                     \
         if (PL == 0 && GI == 8 && LAST) V4_WAIT_W(0, wr[2]);  /* nothing younger in flight */                 \
         __builtin_amdgcn_sched_barrier(0);                                                                    \
         _Pragma("unroll") for (int dy = 0; dy < 3; ++dy)                                                      \
