@@ -16,7 +16,7 @@ done
 cd /tmp && export TMPDIR=/tmp
 i=0
 for cfg in "$@"; do
-  i=$((i+1)); e=$cfg; [ "$e" = "-" ] && e=""
+  i=$((i+1)); e=$cfg; [ "$e" = "-" ] && e=""; e=${e//=ablib\//=$R/ablib/}
   env $e timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tr_$i -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 $SIDE > $O/tr_$i.log 2>&1
   python3 $R/tools/trace_step.py $O/tr_$i --last > $O/step_$i.txt
   echo "== $cfg"; grep -A14 '^total' $O/step_$i.txt
