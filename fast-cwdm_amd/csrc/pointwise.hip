@@ -15,6 +15,7 @@
 // halves so the epilogue stores (and, accumulating, loads) 16 bytes = 8
 // channels per lane.  The brick kernels this replaces ran the R0 skip dgrads
 // at ~0.06 PF (690-910 us each, ~3 ms per training step).
+#include <atomic>
 #include "conv3d_kernels.hpp"
 
 namespace cwdm {
@@ -35,6 +36,9 @@ struct PwParams {
 };
 
 thread_local GapplyFuse* g_gapply = nullptr;
+// the fused-apply skip dgrad's row-major epilogue on / off (cwdm_debug_pw_lt), and its launches
+std::atomic<int> g_pw_lt{[] { const char* e = std::getenv("CWDM_PW_LT"); return (e && e[0] == '0') ? 0 : 1; }()};
+std::atomic<int> g_pw_lt_launches{0};
 
 namespace {
 
@@ -56,12 +60,20 @@ __device__ __forceinline__ float pw_dsilu(float z, float du) {
 // NM: 32-channel output blocks per workgroup (4: 128 channels, 2 waves / SIMD;
 // 2: 64 channels, the fused-apply instance -- 3 waves / SIMD to keep more of
 // its three input streams in flight)
-template <typename T, bool GA, int NM>
+// LT: the row-major epilogue (accumulators transposed through LDS, every load / store a
+// run of whole rows) and the XCD-grouped block order (the nnb channel blocks of a voxel
+// tile on one XCD, so its dout rows come from that XCD's L2 after the first)
+template <typename T, bool GA, int NM, bool LT = false>
 __global__ void __launch_bounds__(256, NM == 2 ? 3 : 2) pw_kernel(PwParams p) {
   constexpr int NC = 32 * NM;                      // output channels per workgroup
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const long long vt = blockIdx.x / p.nnb;
-  const int nb = blockIdx.x % p.nnb;
+  long long wid = blockIdx.x;
+  if constexpr (LT) {
+    const unsigned G = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+    wid = (long long)(xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  }
+  const long long vt = wid / p.nnb;
+  const int nb = (int)(wid % p.nnb);
   const long long row0 = vt * 256 + wv * 64;       // this wave's first voxel row (over B * V)
   const int n0 = nb * NC;
   // fused GroupNorm-backward apply (GA): the block's NC channels' (sc, sh, k0,
@@ -138,6 +150,108 @@ __global__ void __launch_bounds__(256, NM == 2 ? 3 : 2) pw_kernel(PwParams p) {
   // dgrads ran at 1.5-2.2 TB/s).  The swaps run on every lane (no divergence
   // around a cross-lane op); only the loads / stores are predicated.
   const bool f8 = p.N % 8 == 0 && (!p.out1 || p.out_c0 % 8 == 0);
+  if constexpr (LT) {
+    // (the host takes LT only with f8)  Wave wv's 32 x NC accumulator block j goes to its
+    // LDS slice as fp32 (row = voxel, 4 pad words: the 16-byte writes of lanes col and
+    // col + 1 land 4 banks apart); then lane (rl, cg) owns channels n0 + 8 cg .. + 8 of rows
+    // RPI it + rl: every load / store instruction covers RPI whole NC-channel row segments.
+    // Same arithmetic, same order as the swapped-lane epilogue below (bitwise equal).
+    constexpr int LPR = NC / 8, RPI = 64 / LPR, NIT = 32 / RPI, SROW = NC + 4;
+    constexpr int NIH = NM == 4 ? NIT / 2 : NIT;   // row groups whose loads are in flight together (registers)
+    __shared__ __attribute__((aligned(16))) float stg[4 * 32 * SROW];
+    float* const ws = stg + wv * 32 * SROW;
+    const int rl = lane / LPR, cg = lane % LPR, cl = 8 * cg, c = n0 + cl;
+    const bool cok = c < p.N;
+    const bool second = p.out1 && c >= p.out_c0;
+    const long long ost = second ? p.N - p.out_c0 : (p.out1 ? p.out_c0 : p.N);
+    T* const ob = second ? reinterpret_cast<T*>(p.out1) + (c - p.out_c0) : reinterpret_cast<T*>(p.out) + c;
+    const T* const xb = !GA ? nullptr
+                            : second ? reinterpret_cast<const T*>(p.gx1) + (c - p.out_c0)
+                                     : reinterpret_cast<const T*>(p.gx0) + c;
+    const T* const db = GA ? reinterpret_cast<const T*>(p.gdu) + c : nullptr;
+    // 16-lane groups read rows' 8-word runs: lanes cg and cg + 8 start in opposite halves
+    const int hs = (cg >> 3) & 1;
+    int kb = -1;
+    float kc[5][8];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(ws + col * SROW + 32 * m + 8 * g + 4 * kg) =
+              float4{acc[j][m][4 * g], acc[j][m][4 * g + 1], acc[j][m][4 * g + 2], acc[j][m][4 * g + 3]};
+      __syncthreads();
+#pragma unroll
+      for (int i0 = 0; i0 < NIT; i0 += NIH) {
+      u32x4 qo[NIT], qx[NIT], qd[NIT];
+#pragma unroll
+      for (int it = i0; it < i0 + NIH; ++it) {
+        const long long r = row0 + 32 * j + RPI * it + rl;
+        const bool ok = cok && r < p.rows;
+        qo[it] = qx[it] = qd[it] = u32x4{0u, 0u, 0u, 0u};
+        if (ok && p.accumulate) qo[it] = *reinterpret_cast<const u32x4*>(ob + r * ost);
+        if (GA && ok) {
+          qx[it] = *reinterpret_cast<const u32x4*>(xb + r * ost);
+          qd[it] = *reinterpret_cast<const u32x4*>(db + r * p.N);
+        }
+      }
+#pragma unroll
+      for (int it = i0; it < i0 + NIH; ++it) {
+        const long long r = row0 + 32 * j + RPI * it + rl;
+        const bool rin = r < p.rows, ok = cok && rin;
+        const float* sp = ws + (RPI * it + rl) * SROW + cl;
+        const float4 h0 = *reinterpret_cast<const float4*>(sp + 4 * hs);
+        const float4 h1 = *reinterpret_cast<const float4*>(sp + 4 - 4 * hs);
+        float v[8] = {hs ? h1.x : h0.x, hs ? h1.y : h0.y, hs ? h1.z : h0.z, hs ? h1.w : h0.w,
+                      hs ? h0.x : h1.x, hs ? h0.y : h1.y, hs ? h0.z : h1.z, hs ? h0.w : h1.w};
+        const int bb = rin ? (int)(r / p.V) : 0;
+        if (p.bias && ok) {
+          const float* bs = p.bias + (long long)bb * p.bias_bs + c;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bs[e];
+        }
+        auto unpack = [&](const u32x4& q, float (&f)[8]) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) { f[2 * i] = lo2f<T>(q[i]); f[2 * i + 1] = hi2f<T>(q[i]); }
+        };
+        if (p.accumulate) {
+          float f[8];
+          unpack(qo[it], f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += f[e];
+        }
+        if (GA) {
+          const int bl = rin ? (int)(bb - b_lo) : 0;
+          if (bl != kb) {
+#pragma unroll
+            for (int t = 0; t < 5; ++t) {
+              const float4 k0 = *reinterpret_cast<const float4*>(&gk[bl][t][cl]);
+              const float4 k1 = *reinterpret_cast<const float4*>(&gk[bl][t][cl + 4]);
+              kc[t][0] = k0.x; kc[t][1] = k0.y; kc[t][2] = k0.z; kc[t][3] = k0.w;
+              kc[t][4] = k1.x; kc[t][5] = k1.y; kc[t][6] = k1.z; kc[t][7] = k1.w;
+            }
+            kb = bl;
+          }
+          float xv[8], dv[8];
+          unpack(qx[it], xv);
+          unpack(qd[it], dv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float dz = pw_dsilu(xv[e] * kc[0][e] + kc[1][e], dv[e]);
+            v[e] += kc[2][e] * dz + kc[3][e] * xv[e] + kc[4][e];
+          }
+        }
+        u32x4 w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = pack2<T>(v[2 * i], v[2 * i + 1]);
+        if (ok) *reinterpret_cast<u32x4*>(ob + r * ost) = w;
+      }
+      }
+      __syncthreads();   // (block j + 1 reuses the slice)
+    }
+    return;
+  }
   if (f8) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -413,6 +527,9 @@ int pw_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
     g_gapply->used = true;
   }
   const bool ga = p.gdu != nullptr;
+  // row-major LDS epilogue (pw_kernel LT): cwdm_debug_pw_lt / env CWDM_PW_LT = 0 restores the swapped-lane one
+  const bool lt = g_pw_lt.load(std::memory_order_relaxed) && ga;
+  if (lt) g_pw_lt_launches.fetch_add(1, std::memory_order_relaxed);
   // the fused apply on 64-channel blocks where 128-channel ones would leave a
   // half-empty block (N = 192: 916 -> 770 us at 128^3; N = 128 stays on 128:
   // 491 vs 526 us); env CWDM_PW_GA_NM = 2 / 4 forces one (A/B knob)
@@ -423,11 +540,15 @@ int pw_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
   CWDM_REQUIRE(nblk < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d (pointwise): grid too large");
   prof_begin(s);
   if (d->dtype == CWDM_F16) {
-    if (ga && nm == 2) hipLaunchKernelGGL((pw_kernel<f16_t, true, 2>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    if (lt && nm == 2) hipLaunchKernelGGL((pw_kernel<f16_t, true, 2, true>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    else if (lt) hipLaunchKernelGGL((pw_kernel<f16_t, true, 4, true>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    else if (ga && nm == 2) hipLaunchKernelGGL((pw_kernel<f16_t, true, 2>), dim3((unsigned)nblk), dim3(256), 0, s, p);
     else if (ga) hipLaunchKernelGGL((pw_kernel<f16_t, true, 4>), dim3((unsigned)nblk), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((pw_kernel<f16_t, false, 4>), dim3((unsigned)nblk), dim3(256), 0, s, p);
   } else {
-    if (ga && nm == 2) hipLaunchKernelGGL((pw_kernel<bf16_t, true, 2>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    if (lt && nm == 2) hipLaunchKernelGGL((pw_kernel<bf16_t, true, 2, true>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    else if (lt) hipLaunchKernelGGL((pw_kernel<bf16_t, true, 4, true>), dim3((unsigned)nblk), dim3(256), 0, s, p);
+    else if (ga && nm == 2) hipLaunchKernelGGL((pw_kernel<bf16_t, true, 2>), dim3((unsigned)nblk), dim3(256), 0, s, p);
     else if (ga) hipLaunchKernelGGL((pw_kernel<bf16_t, true, 4>), dim3((unsigned)nblk), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((pw_kernel<bf16_t, false, 4>), dim3((unsigned)nblk), dim3(256), 0, s, p);
   }
@@ -470,3 +591,8 @@ int pw_split_forward(const cwdm_conv3d_desc* d, hipStream_t s) {
 }
 
 }  // namespace cwdm
+
+extern "C" int cwdm_debug_pw_lt(int on) {
+  if (on < 0) return cwdm::g_pw_lt_launches.load(std::memory_order_relaxed);
+  return cwdm::g_pw_lt.exchange(on ? 1 : 0);
+}

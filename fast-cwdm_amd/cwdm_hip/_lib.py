@@ -157,6 +157,7 @@ _PROTOS = {
     "cwdm_debug_gn_fin_apply": (ctypes.c_int, [vp, i64, ctypes.c_int, vp, i64, ctypes.c_int, vp, vp, ctypes.c_int,
                                                i64, i64, ctypes.c_float, vp, vp, ctypes.c_int, vp, vp, vp, vp]),
     "cwdm_debug_head2": (ctypes.c_int, [ctypes.c_int]),
+    "cwdm_debug_pw_lt": (ctypes.c_int, [ctypes.c_int]),
     "cwdm_debug_conv_stamps": (ctypes.c_int, [vp]),
     "cwdm_conv3d_wgrad": (ctypes.c_int, [ctypes.POINTER(WgradDesc), vp]),
     "cwdm_conv3d_wgrad_workspace_bytes": (i64, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),

@@ -410,6 +410,14 @@ int cwdm_debug_gn_fin_apply(const float* stats0, int64_t parts0, int c0, const f
  * Initial value: env CWDM_HEAD2=0 -> -1, else 0. */
 int cwdm_debug_head2(int mode);
 
+/* Diagnostics / tests only: the training backward's fused 1x1 skip dgrad +
+ * GroupNorm-backward apply (pointwise.hip pw_kernel) with its row-major
+ * epilogue (accumulators transposed through LDS, whole-row loads / stores; 1,
+ * default; env CWDM_PW_LT=0 starts it off) or the swapped-lane one (0): the
+ * same arithmetic in the same order.  Returns the previous setting; -1 changes
+ * nothing and returns the number of row-major launches so far. */
+int cwdm_debug_pw_lt(int on);
+
 /* Diagnostics only: per-workgroup timestamps of the DMA-staged conv kernel
  * (24 x u64 per workgroup: s_memtime at start, after the prologue, after each of
  * the first 16 chunks, at the end; [22] HW_ID, [23] XCC_ID) into the device

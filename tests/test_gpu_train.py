@@ -770,6 +770,32 @@ def test_production_unet_backward_kept_activations(dtype):
     assert top[0][1] < 5e-3, top
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_production_unet_backward_skip_dgrad_row_major_epilogue_bitwise(dtype):
+    """The fused 1x1 skip dgrad + GroupNorm-backward apply (pw_kernel) with the
+    row-major LDS epilogue (default) against the swapped-lane epilogue it
+    replaced: the same products summed in the same order, so every gradient is
+    bitwise equal -- and the row-major instance did run."""
+    from cwdm_hip._lib import lib
+    L = lib()
+    P, x, t, R = _prod_case()
+    prev, prevlt = L.cwdm_conv3d_set_path(0), L.cwdm_debug_pw_lt(1)
+    try:
+        n0 = L.cwdm_debug_pw_lt(-1)
+        out_a, g_a, _ = _unet_grads(PROD_CFG, 32, P, x, t, R, dtype)
+        n1 = L.cwdm_debug_pw_lt(-1)
+        L.cwdm_debug_pw_lt(0)
+        out_b, g_b, _ = _unet_grads(PROD_CFG, 32, P, x, t, R, dtype)
+        assert L.cwdm_debug_pw_lt(-1) == n1
+    finally:
+        L.cwdm_conv3d_set_path(prev)
+        L.cwdm_debug_pw_lt(prevlt)
+    assert n1 > n0, "the row-major skip dgrad did not run"
+    assert torch.equal(out_a, out_b)
+    bad = [k for k in g_b if not torch.equal(g_a[k], g_b[k])]
+    assert not bad, bad[:8]
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
 def test_production_training_two_steps_bitwise_reproducible(dtype):
     """Determinism of the training step: two runs of two steps each (forward with
