@@ -838,6 +838,204 @@ int launch_wg_dma(const WgDmaParams& p, dim3, hipStream_t s) {
   return CWDM_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Output-head weight gradient (the 64 -> out_channels conv of out[2], unet.py:
+// 793-797, with its GroupNorm+SiLU; 16-bit, 3x3x3, cout <= 8, cin 64):
+//
+//   dW[co][ci][t] = sum_u dY[u - (t - 1)][co] U[u][ci],   U = SiLU(GN(x))
+//
+// The brick kernel put cout on the MFMA's M side (a 32-row tile, 8 used) and
+// staged U's 3^3 halo for every 32-channel tile (the transform on 2.5x the
+// voxels, twice): 486 us at 128^3.  Here M = (tap, co) = 216 rows (7 tiles of 4
+// taps x 8 channels), N = ci (2 tiles), K = voxels: the SHIFT moves to dY (8
+// channels, its halo is small) and U is staged once per brick, without halo.
+// Both operands need 8 consecutive voxels per lane, so both LDS images are
+// channel-major: U [ci][z][y][16 x] (ci pitch 528 B: 16-lane groups of the B
+// reads hit distinct bank quads) and dY [x shift][co][6 z][6 y][16 x] (three
+// x-shifted copies keep every A read 16-byte aligned; co pitch 1168 B).  Wave w:
+// N tile w & 1, M tiles 0-3 (w < 2) or 4-6; per 16-voxel K step one B read and
+// 3-4 A reads feed 3-4 v_mfma_f32_32x32x16.  Two workgroups per CU (61.8 KB of
+// LDS each) overlap one's staging with the other's MFMAs.  Partial tiles go to
+// the workgroup's slab [27][cout][64]; wg_reduce_kernel adds the slabs in order.
+struct HwParams {
+  const void* x; const float* gn; const void* dy;
+  int dy_cs, cout;
+  int D, H, W, tx, ty, tz;
+  long long nbricks, per;
+  float* part;
+};
+constexpr int HW_CS = 16 * 32 + 16;          // U image: bytes per input channel
+constexpr int HW_UIMG = 64 * HW_CS;
+constexpr int HW_COS = 36 * 32 + 16;         // dY image: bytes per output channel (6 x 6 rows)
+constexpr int HW_KXS = 8 * HW_COS;           // one x-shifted copy
+constexpr int HW_SMEM = HW_UIMG + 3 * HW_KXS;
+constexpr long long HW_SMAX = 512;           // brick ranges (workgroups)
+
+template <typename T, bool GN>
+__global__ void __launch_bounds__(256, 2) head_wgrad_kernel(HwParams p) {
+  constexpr int EPQ = 8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* uimg = smem;
+  unsigned char* dimg = smem + HW_UIMG;
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, col = lane & 31, kh = lane >> 5;
+  const long long bb = (long long)blockIdx.x * p.per;
+  const long long be = bb + p.per < p.nbricks ? bb + p.per : p.nbricks;
+  const int nt = wv & 1, mt0 = (wv >> 1) * 4, nmt = (wv >> 1) ? 3 : 4;
+  // A rows: lane row m = col -> tap 4 mt + col / 8, co = col % 8; its dY row for K step
+  // (zz, yy) is (hz, hy) = (zz + 2 - kz, yy + 2 - ky) of copy kx
+  int aoff[4];
+  bool aok[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int tap = 4 * (mt0 + k) + (col >> 3);
+    aok[k] = k < nmt && tap < 27;
+    const int t = aok[k] ? tap : 0, kz = t / 9, ky = (t / 3) % 3, kx = t % 3;
+    aoff[k] = kx * HW_KXS + (col & 7) * HW_COS + ((2 - kz) * 6 + (2 - ky)) * 32 + kh * 16;
+  }
+  const int boff = (32 * nt + col) * HW_CS + kh * 16;
+  f32x16 acc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[k][i] = 0.f;
+  const int nb_vol = p.tx * p.ty * p.tz;
+  const int g = tid & 7, pr = tid >> 3;   // U staging: channels 8 g .. + 8 of voxel pairs pr + 32 j
+  const T* xs = reinterpret_cast<const T*>(p.x);
+  const T* ds = reinterpret_cast<const T*>(p.dy);
+
+  for (long long bi = bb; bi < be; ++bi) {
+    const int b = (int)(bi / nb_vol);
+    int r = (int)(bi % nb_vol);
+    const int x0 = (r % p.tx) * 16;
+    r /= p.tx;
+    const int y0 = (r % p.ty) * 4, z0 = (r / p.ty) * 4;
+    // global loads first: U's 8 16-byte pieces, dY's (up to) 3 halo voxels
+    u32x4 ur[4][2], dr[3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = pr + 32 * j, x = 2 * (q & 7), yy = (q >> 3) & 3, zz = q >> 5;
+      const long long vox = (((long long)b * p.D + z0 + zz) * p.H + y0 + yy) * p.W + x0 + x;
+      ur[j][0] = ldg16(xs + vox * 64 + 8 * g);
+      ur[j][1] = ldg16(xs + (vox + 1) * 64 + 8 * g);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int hv = tid + 256 * j;
+      const int hx = hv % 18, hy = (hv / 18) % 6, hz = hv / 108;
+      const int vx = x0 + hx - 1, vy = y0 + hy - 1, vz = z0 + hz - 1;
+      const bool in = hv < 648 && vx >= 0 && vy >= 0 && vz >= 0 && vx < p.W && vy < p.H && vz < p.D;
+      dr[j] = u32x4{0u, 0u, 0u, 0u};
+      if (in) dr[j] = ldg16(ds + ((((long long)b * p.D + vz) * p.H + vy) * p.W + vx) * p.dy_cs);
+    }
+    float sc[EPQ], sh[EPQ];
+#pragma unroll
+    for (int e = 0; e < EPQ; ++e) {
+      sc[e] = GN ? p.gn[((long long)b * 64 + 8 * g + e) * 2] : 1.f;
+      sh[e] = GN ? p.gn[((long long)b * 64 + 8 * g + e) * 2 + 1] : 0.f;
+    }
+    __syncthreads();   // the previous brick's operand reads are done
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = pr + 32 * j, x = 2 * (q & 7), yy = (q >> 3) & 3, zz = q >> 5;
+      u32x4 t2[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (GN) {
+          float f[EPQ];
+          unpack<T>(ur[j][h], f);
+#pragma unroll
+          for (int e = 0; e < EPQ; ++e) f[e] = silu(f[e] * sc[e] + sh[e]);
+          t2[h] = pack<T>(f);
+        } else {
+          t2[h] = ur[j][h];
+        }
+      }
+      // channel 8 g + e of voxels x, x + 1 -> one 32-bit word of row (ci, zz, yy)
+      unsigned char* dst = uimg + (8 * g) * HW_CS + ((zz * 4 + yy) * 16 + x) * 2;
+#pragma unroll
+      for (int e = 0; e < EPQ; ++e) {
+        const unsigned lo = (t2[0][e >> 1] >> (16 * (e & 1))) & 0xffffu;
+        const unsigned hi = (t2[1][e >> 1] >> (16 * (e & 1))) & 0xffffu;
+        *reinterpret_cast<unsigned*>(dst + e * HW_CS) = lo | (hi << 16);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int hv = tid + 256 * j;
+      if (hv < 648) {
+        const int hx = hv % 18, hy = (hv / 18) % 6, hz = hv / 108;
+        unsigned char* row = dimg + (hz * 6 + hy) * 32;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int jj = hx + kx - 2;   // element jj of copy kx is dY at halo x jj - kx + 2
+          if (jj >= 0 && jj < 16) {
+#pragma unroll
+            for (int co = 0; co < 8; ++co)
+              *reinterpret_cast<unsigned short*>(row + kx * HW_KXS + co * HW_COS + jj * 2) =
+                  (unsigned short)((dr[j][co >> 1] >> (16 * (co & 1))) & 0xffffu);
+          }
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int st = 0; st < 16; ++st) {
+      const int zz = st >> 2, yy = st & 3;
+      const u32x4 bv = *reinterpret_cast<const u32x4*>(uimg + boff + (zz * 4 + yy) * 32);
+      const int ro = (zz * 6 + yy) * 32;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k < nmt) {
+          u32x4 av = u32x4{0u, 0u, 0u, 0u};
+          if (aok[k]) av = *reinterpret_cast<const u32x4*>(dimg + aoff[k] + ro);
+          mfma_acc(acc[k], av, bv, (T*)nullptr);
+        }
+      }
+    }
+  }
+  // acc[k][i] = dW row m = 8 (i / 4) + 4 kh + i % 4 -> (tap 4 (mt0 + k) + i / 4, co 4 kh + i % 4), ci 32 nt + col
+  float* slab = p.part + (long long)blockIdx.x * 27 * p.cout * 64;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k < nmt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int tap = 4 * (mt0 + k) + (i >> 2), co = 4 * kh + (i & 3);
+        if (tap < 27 && co < p.cout) slab[((long long)tap * p.cout + co) * 64 + 32 * nt + col] = acc[k][i];
+      }
+    }
+  }
+}
+
+bool hw_shape_ok(int cout, int cin, int ksize) { return ksize == 3 && cout >= 1 && cout <= 8 && cin == 64; }
+
+// the output head's weight gradient kernel where it applies (env CWDM_HEAD_WG=0: the brick kernel, A/B)
+bool hw_eligible(const cwdm_wgrad_desc* d) {
+  static const bool on = [] { const char* e = std::getenv("CWDM_HEAD_WG"); return !(e && e[0] == '0'); }();
+  if (!on || !hw_shape_ok(d->cout, d->u_c0 + d->u_c1, d->ksize) || !dtype_half(d->dtype)) return false;
+  if (d->u_mode != 0 || d->u_cm || d->u1 || d->u_c1 != 0 || d->dy_cs < 8 || d->dy_cs % 8) return false;
+  if (d->W % 16 || d->H % 4 || d->D % 4) return false;
+  return d->B * d->D * d->H * d->W * 64 < (1LL << 40);
+}
+
+template <typename T>
+int launch_hw(const cwdm_wgrad_desc* d, hipStream_t s) {
+  HwParams q{};
+  q.x = d->u0; q.gn = d->u_gn; q.dy = d->dy; q.dy_cs = d->dy_cs; q.cout = d->cout;
+  q.D = (int)d->D; q.H = (int)d->H; q.W = (int)d->W;
+  q.tx = q.W / 16; q.ty = q.H / 4; q.tz = q.D / 4;
+  q.nbricks = d->B * (long long)q.tx * q.ty * q.tz;
+  long long S = std::min(HW_SMAX, q.nbricks);
+  q.per = ceil_div(q.nbricks, S);
+  S = ceil_div(q.nbricks, q.per);
+  q.part = reinterpret_cast<float*>(d->workspace);
+  auto k = d->u_gn ? head_wgrad_kernel<T, true> : head_wgrad_kernel<T, false>;
+  CWDM_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, HW_SMEM));
+  hipLaunchKernelGGL(k, dim3((unsigned)S), dim3(256), HW_SMEM, s, q);
+  CWDM_LAUNCHED();
+  return launch_wg_reduce(q.part, S, 27LL * d->cout * 64, d->dw, d->cout, 64, 27, true, s);
+}
+
 }  // namespace
 }  // namespace cwdm
 
@@ -905,6 +1103,7 @@ extern "C" int cwdm_conv3d_wgrad(const cwdm_wgrad_desc* d, cwdm_stream_t stream)
   const long long nw = (long long)d->cout * cin * p.taps;
   int rc;
   static const bool wg1_on = !std::getenv("CWDM_WG1_OFF");   // A/B knob: the brick kernel for 1x1
+  if (hw_eligible(d)) return d->dtype == CWDM_F16 ? launch_hw<f16_t>(d, s) : launch_hw<bf16_t>(d, s);
   if (wg1_on && wg1_eligible(d)) {
     // 1x1: the streaming kernel, accumulating straight into dw (no scratch)
     return d->dtype == CWDM_F16 ? launch_wg1<f16_t>(d, s) : launch_wg1<bf16_t>(d, s);
@@ -958,6 +1157,7 @@ extern "C" int64_t cwdm_conv3d_wgrad_workspace_bytes(int cout, int cin, int ksiz
   const int mc = cout > 32 ? 2 : 1;
   const int64_t tiles = ceil_div((int64_t)cout, 32 * mc) * ceil_div((int64_t)cin, 32);
   int64_t smax = std::max<int64_t>(1, 256 / tiles);                      // wgrad_kernel / wgrad_dma_kernel
+  if (hw_shape_ok(cout, cin, ksize)) smax = std::max<int64_t>(smax, HW_SMAX);   // head_wgrad_kernel
   if (ksize == 1) {
     const int64_t t1 = ceil_div((int64_t)cout, 64) * ceil_div((int64_t)cin, 128);
     smax = std::max(smax, std::max<int64_t>(1, 768 / t1));                // wgrad1_kernel

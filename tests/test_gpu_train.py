@@ -42,6 +42,11 @@ WG_CASES = [
     ("up", 1, (8, 8, 16), 32, 0, 64, 1, True, 3, 64),
     ("plain_in32", 1, (8, 4, 16), 32, 0, 64, 0, False, 3, 64),
     ("head_cout8", 1, (8, 8, 8), 64, 0, 8, 0, True, 3, 16),
+    # the output head's weight-gradient kernel (16-bit, W % 16, H % 4, D % 4; cout <= 8, cin 64):
+    # two batches over several bricks, a cout below 8, no GroupNorm prologue
+    ("head_hw_b2", 2, (8, 8, 32), 64, 0, 8, 0, True, 3, 16),
+    ("head_hw_cout3", 1, (4, 12, 16), 64, 0, 3, 0, True, 3, 16),
+    ("head_hw_nogn", 1, (8, 4, 16), 64, 0, 8, 0, False, 3, 16),
     ("skip1x1", 2, (4, 8, 16), 64, 32, 64, 0, False, 1, 64),
     ("tiny_grid", 1, (2, 2, 2), 64, 64, 128, 0, True, 3, 128),
     # 1x1 streaming kernel (wgrad1_kernel): R0-like concat 128 + 64 -> 64 over two
