@@ -855,7 +855,8 @@ int launch_wg_dma(const WgDmaParams& p, dim3, hipStream_t s) {
 // x-shifted copies keep every A read 16-byte aligned; co pitch 1168 B).  Wave w:
 // N tile w & 1, M tiles 0-3 (w < 2) or 4-6; per 16-voxel K step one B read and
 // 3-4 A reads feed 3-4 v_mfma_f32_32x32x16.  Two workgroups per CU (61.8 KB of
-// LDS each) overlap one's staging with the other's MFMAs.  Partial tiles go to
+// LDS each) overlap one's staging with the other's MFMAs, and a brick's global loads are
+// issued before the previous brick's MFMAs (register prefetch).  Partial tiles go to
 // the workgroup's slab [27][cout][64]; wg_reduce_kernel adds the slabs in order.
 struct HwParams {
   const void* x; const float* gn; const void* dy;
@@ -903,14 +904,17 @@ __global__ void __launch_bounds__(256, 2) head_wgrad_kernel(HwParams p) {
   const T* xs = reinterpret_cast<const T*>(p.x);
   const T* ds = reinterpret_cast<const T*>(p.dy);
 
-  for (long long bi = bb; bi < be; ++bi) {
+  // global -> registers for brick bi (U's 8 16-byte pieces, dY's up to 3 halo voxels): issued
+  // before the previous brick's MFMAs, so a brick's loads fly under them
+  u32x4 ur[4][2], dr[3];
+  int fb = 0;
+  auto fetch = [&](long long bi) {
     const int b = (int)(bi / nb_vol);
     int r = (int)(bi % nb_vol);
     const int x0 = (r % p.tx) * 16;
     r /= p.tx;
     const int y0 = (r % p.ty) * 4, z0 = (r / p.ty) * 4;
-    // global loads first: U's 8 16-byte pieces, dY's (up to) 3 halo voxels
-    u32x4 ur[4][2], dr[3];
+    fb = b;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int q = pr + 32 * j, x = 2 * (q & 7), yy = (q >> 3) & 3, zz = q >> 5;
@@ -927,11 +931,19 @@ __global__ void __launch_bounds__(256, 2) head_wgrad_kernel(HwParams p) {
       dr[j] = u32x4{0u, 0u, 0u, 0u};
       if (in) dr[j] = ldg16(ds + ((((long long)b * p.D + vz) * p.H + vy) * p.W + vx) * p.dy_cs);
     }
-    float sc[EPQ], sh[EPQ];
+  };
+  if (bb < be) fetch(bb);
+  int sb = -1;
+  float sc[EPQ], sh[EPQ];
+  for (long long bi = bb; bi < be; ++bi) {
+    const int b = fb;
+    if (b != sb) {
 #pragma unroll
-    for (int e = 0; e < EPQ; ++e) {
-      sc[e] = GN ? p.gn[((long long)b * 64 + 8 * g + e) * 2] : 1.f;
-      sh[e] = GN ? p.gn[((long long)b * 64 + 8 * g + e) * 2 + 1] : 0.f;
+      for (int e = 0; e < EPQ; ++e) {
+        sc[e] = GN ? p.gn[((long long)b * 64 + 8 * g + e) * 2] : 1.f;
+        sh[e] = GN ? p.gn[((long long)b * 64 + 8 * g + e) * 2 + 1] : 0.f;
+      }
+      sb = b;
     }
     __syncthreads();   // the previous brick's operand reads are done
 #pragma unroll
@@ -978,6 +990,7 @@ __global__ void __launch_bounds__(256, 2) head_wgrad_kernel(HwParams p) {
       }
     }
     __syncthreads();
+    if (bi + 1 < be) fetch(bi + 1);
 #pragma unroll 4
     for (int st = 0; st < 16; ++st) {
       const int zz = st >> 2, yy = st & 3;
