@@ -940,8 +940,9 @@ __global__ void __launch_bounds__(256, 2) head_wgrad_kernel(HwParams p) {
     if (b != sb) {
 #pragma unroll
       for (int e = 0; e < EPQ; ++e) {
-        sc[e] = GN ? p.gn[((long long)b * 64 + 8 * g + e) * 2] : 1.f;
-        sh[e] = GN ? p.gn[((long long)b * 64 + 8 * g + e) * 2 + 1] : 0.f;
+        // (the head's forward transform, silu_aff: U bit-identical to what the conv saw)
+        if (GN) silu_aff_coef(p.gn[((long long)b * 64 + 8 * g + e) * 2], p.gn[((long long)b * 64 + 8 * g + e) * 2 + 1],
+                              sc[e], sh[e]);
       }
       sb = b;
     }
@@ -956,7 +957,7 @@ __global__ void __launch_bounds__(256, 2) head_wgrad_kernel(HwParams p) {
           float f[EPQ];
           unpack<T>(ur[j][h], f);
 #pragma unroll
-          for (int e = 0; e < EPQ; ++e) f[e] = silu(f[e] * sc[e] + sh[e]);
+          for (int e = 0; e < EPQ; ++e) f[e] = silu_aff(f[e], sc[e], sh[e]);
           t2[h] = pack<T>(f);
         } else {
           t2[h] = ur[j][h];
@@ -965,11 +966,9 @@ __global__ void __launch_bounds__(256, 2) head_wgrad_kernel(HwParams p) {
       // channel 8 g + e of voxels x, x + 1 -> one 32-bit word of row (ci, zz, yy)
       unsigned char* dst = uimg + (8 * g) * HW_CS + ((zz * 4 + yy) * 16 + x) * 2;
 #pragma unroll
-      for (int e = 0; e < EPQ; ++e) {
-        const unsigned lo = (t2[0][e >> 1] >> (16 * (e & 1))) & 0xffffu;
-        const unsigned hi = (t2[1][e >> 1] >> (16 * (e & 1))) & 0xffffu;
-        *reinterpret_cast<unsigned*>(dst + e * HW_CS) = lo | (hi << 16);
-      }
+      for (int e = 0; e < EPQ; ++e)
+        *reinterpret_cast<unsigned*>(dst + e * HW_CS) =
+            __builtin_amdgcn_perm(t2[1][e >> 1], t2[0][e >> 1], (e & 1) ? 0x07060302u : 0x05040100u);
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
