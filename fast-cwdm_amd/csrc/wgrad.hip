@@ -854,7 +854,7 @@ int launch_wg_dma(const WgDmaParams& p, dim3, hipStream_t s) {
 // reads hit distinct bank quads) and dY [x shift][co][6 z][6 y][16 x] (three
 // x-shifted copies keep every A read 16-byte aligned; co pitch 1168 B).  Wave w:
 // N tile w & 1, M tiles 0-3 (w < 2) or 4-6; per 16-voxel K step one B read and
-// 3-4 A reads feed 3-4 v_mfma_f32_32x32x16.  Two workgroups per CU (61.8 KB of
+// 4 A reads feed 4 v_mfma_f32_32x32x16, software-pipelined one step ahead.  Two workgroups per CU (61.8 KB of
 // LDS each) overlap one's staging with the other's MFMAs, and a brick's global loads are
 // issued before the previous brick's MFMAs (register prefetch).  Partial tiles go to
 // the workgroup's slab [27][cout][64]; wg_reduce_kernel adds the slabs in order.
@@ -869,7 +869,8 @@ constexpr int HW_CS = 16 * 32 + 16;          // U image: bytes per input channel
 constexpr int HW_UIMG = 64 * HW_CS;
 constexpr int HW_COS = 36 * 32 + 16;         // dY image: bytes per output channel (6 x 6 rows)
 constexpr int HW_KXS = 8 * HW_COS;           // one x-shifted copy
-constexpr int HW_SMEM = HW_UIMG + 3 * HW_KXS;
+constexpr int HW_ZOFF = HW_UIMG + 3 * HW_KXS;  // zeros: the A rows of taps >= 27 read them (branch-free K loop)
+constexpr int HW_SMEM = HW_ZOFF + 704;
 constexpr long long HW_SMAX = 512;           // brick ranges (workgroups)
 
 template <typename T, bool GN>
@@ -881,18 +882,20 @@ __global__ void __launch_bounds__(256, 2) head_wgrad_kernel(HwParams p) {
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, col = lane & 31, kh = lane >> 5;
   const long long bb = (long long)blockIdx.x * p.per;
   const long long be = bb + p.per < p.nbricks ? bb + p.per : p.nbricks;
-  const int nt = wv & 1, mt0 = (wv >> 1) * 4, nmt = (wv >> 1) ? 3 : 4;
+  const int nt = wv & 1, mt0 = (wv >> 1) * 4, nmt = (wv >> 1) ? 3 : 4;   // M tiles 0-3 / 4-6
   // A rows: lane row m = col -> tap 4 mt + col / 8, co = col % 8; its dY row for K step
   // (zz, yy) is (hz, hy) = (zz + 2 - kz, yy + 2 - ky) of copy kx
+  // (every wave runs 4 M tiles: waves 2-3's fourth is taps 28-31, all zero rows -- the same MFMA
+  // count as waves 0-1 and no branch in the K loop)
   int aoff[4];
-  bool aok[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int tap = 4 * (mt0 + k) + (col >> 3);
-    aok[k] = k < nmt && tap < 27;
-    const int t = aok[k] ? tap : 0, kz = t / 9, ky = (t / 3) % 3, kx = t % 3;
-    aoff[k] = kx * HW_KXS + (col & 7) * HW_COS + ((2 - kz) * 6 + (2 - ky)) * 32 + kh * 16;
+    const int kz = tap / 9, ky = (tap / 3) % 3, kx = tap % 3;
+    aoff[k] = tap < 27 ? kx * HW_KXS + (col & 7) * HW_COS + ((2 - kz) * 6 + (2 - ky)) * 32 + kh * 16
+                       : HW_ZOFF - HW_UIMG + kh * 16;
   }
+  for (int i = tid; i < 704 / 16; i += 256) *reinterpret_cast<u32x4*>(smem + HW_ZOFF + 16 * i) = u32x4{0u, 0u, 0u, 0u};
   const int boff = (32 * nt + col) * HW_CS + kh * 16;
   f32x16 acc[4];
 #pragma unroll
@@ -990,19 +993,20 @@ __global__ void __launch_bounds__(256, 2) head_wgrad_kernel(HwParams p) {
     }
     __syncthreads();
     if (bi + 1 < be) fetch(bi + 1);
-#pragma unroll 4
-    for (int st = 0; st < 16; ++st) {
+    // K step st = (zz, yy): its 5 operand reads are issued before step st - 1's MFMAs
+    u32x4 bv[2], av[2][4];
+    auto rd = [&](int st, int q) {
       const int zz = st >> 2, yy = st & 3;
-      const u32x4 bv = *reinterpret_cast<const u32x4*>(uimg + boff + (zz * 4 + yy) * 32);
-      const int ro = (zz * 6 + yy) * 32;
+      bv[q] = *reinterpret_cast<const u32x4*>(uimg + boff + (zz * 4 + yy) * 32);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (k < nmt) {
-          u32x4 av = u32x4{0u, 0u, 0u, 0u};
-          if (aok[k]) av = *reinterpret_cast<const u32x4*>(dimg + aoff[k] + ro);
-          mfma_acc(acc[k], av, bv, (T*)nullptr);
-        }
-      }
+      for (int k = 0; k < 4; ++k) av[q][k] = *reinterpret_cast<const u32x4*>(dimg + aoff[k] + (zz * 6 + yy) * 32);
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      if (st + 1 < 16) rd(st + 1, (st + 1) & 1);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) mfma_acc(acc[k], av[st & 1][k], bv[st & 1], (T*)nullptr);
     }
   }
   // acc[k][i] = dW row m = 8 (i / 4) + 4 kh + i % 4 -> (tap 4 (mt0 + k) + i / 4, co 4 kh + i % 4), ci 32 nt + col
