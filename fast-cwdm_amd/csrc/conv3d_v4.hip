@@ -360,14 +360,11 @@ int gn_fin_apply(const GnFinFuse& f, const void* x0, int c0, const void* x1, int
 // epilogue's ~13 VALU + 2 transcendentals per output element cost the
 // MFMA-bound kernel more (+30 %) than the separate reduce pass it saves; at
 // 64^3 / 32^3 it is a net win (same-box kernel traces; env
-// CWDM_GBWD_MAXW, default 64).  A dgrad with at most CWDM_GBWD_MAXK input channels (default 16:
-// the output head's, 8 -> 64 over one 16-channel chunk) is epilogue-bound, not MFMA-bound, at
-// any grid: it takes the fusion at 128^3 too.  Elsewhere the dgrad is an ordinary conv (v5 may take it).
+// CWDM_GBWD_MAXW, default 64).  Elsewhere the dgrad is an ordinary conv (v5 may take it).
 bool gbwd_grid_ok(const cwdm_conv3d_desc* d) {
   static const int gb_maxw = [] { const char* e = std::getenv("CWDM_GBWD_MAXW"); return e ? std::atoi(e) : 64; }();
-  static const int gb_maxk = [] { const char* e = std::getenv("CWDM_GBWD_MAXK"); return e ? std::atoi(e) : 16; }();
-  return g_gbwd && !g_gbwd->used && dtype_half(d->dtype) && (d->W <= gb_maxw || d->a_c0 + d->a_c1 <= gb_maxk) &&
-         d->a_mode == 0 && d->res_mode < 0 && !d->stats;
+  return g_gbwd && !g_gbwd->used && dtype_half(d->dtype) && d->W <= gb_maxw && d->a_mode == 0 && d->res_mode < 0 &&
+         !d->stats;
 }
 
 int gn_apply(const void* x0, int c0, const void* x1, int c1, const float* gn, int64_t B, int64_t vpb, int dtype,
