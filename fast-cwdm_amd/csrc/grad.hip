@@ -45,7 +45,7 @@ template <> __device__ __forceinline__ void store8<float>(float* p, const float*
 template <> __device__ __forceinline__ void store8<bf16_t>(bf16_t* p, const float* f) {
   u4 a;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) a[i] = (unsigned)f2bf(f[2 * i]) | ((unsigned)f2bf(f[2 * i + 1]) << 16);
+  for (int i = 0; i < 4; ++i) a[i] = pack2<bf16_t>(f[2 * i], f[2 * i + 1]);   // v_cvt_pk_bf16_f32 (RNE, as f2bf)
   *reinterpret_cast<u4*>(p) = a;
 }
 template <> __device__ __forceinline__ void store8<f16_t>(f16_t* p, const float* f) {
@@ -284,12 +284,35 @@ __global__ void __launch_bounds__(256) gn_bwd_apply_kernel(const T* __restrict__
   constexpr int UNR = MODE == 1 ? 1 : 2;
   for (unsigned v0 = blockIdx.x * (unsigned)nvb + threadIdx.x / ncg; v0 < V; v0 += UNR * vstep) {
     float xv[UNR][8], g[UNR][8], o[UNR][8];
+    if constexpr (sizeof(T) == 2) {
+      // 16-bit: the loads stay packed until the arithmetic (the unpacked copies of x, du
+      // and dx held beside the packed ones took bf16 to 150-168 VGPRs: 3 waves per SIMD)
+      u4 xr[UNR], gr[UNR], orr[UNR];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const unsigned v = v0 + u * vstep < V ? v0 + u * vstep : v0;
-      load8<T>(xb + (size_t)v * xc, xv[u]);
-      load_du<T, MODE>(du, C, c, b, v, d, h, w, g[u]);
-      if (acc) load8<T>(ob + (size_t)v * xc, o[u]);
+      for (int u = 0; u < UNR; ++u) {
+        const unsigned v = v0 + u * vstep < V ? v0 + u * vstep : v0;
+        xr[u] = *reinterpret_cast<const u4*>(xb + (size_t)v * xc);
+        if constexpr (MODE == 0) gr[u] = *reinterpret_cast<const u4*>(du + ((size_t)b * V + v) * C + c);
+        else load_du<T, MODE>(du, C, c, b, v, d, h, w, g[u]);
+        orr[u] = u4{0u, 0u, 0u, 0u};
+        if (acc) orr[u] = *reinterpret_cast<const u4*>(ob + (size_t)v * xc);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          xv[u][2 * i] = lo2f<T>(xr[u][i]); xv[u][2 * i + 1] = hi2f<T>(xr[u][i]);
+          if constexpr (MODE == 0) { g[u][2 * i] = lo2f<T>(gr[u][i]); g[u][2 * i + 1] = hi2f<T>(gr[u][i]); }
+          o[u][2 * i] = lo2f<T>(orr[u][i]); o[u][2 * i + 1] = hi2f<T>(orr[u][i]);
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const unsigned v = v0 + u * vstep < V ? v0 + u * vstep : v0;
+        load8<T>(xb + (size_t)v * xc, xv[u]);
+        load_du<T, MODE>(du, C, c, b, v, d, h, w, g[u]);
+        if (acc) load8<T>(ob + (size_t)v * xc, o[u]);
+      }
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
