@@ -359,10 +359,13 @@ int gn_fin_apply(const GnFinFuse& f, const void* x0, int c0, const void* x1, int
 // reduce (v4 only): only where the conv leaves VALU room -- at 128^3 the
 // epilogue's ~13 VALU + 2 transcendentals per output element cost the
 // MFMA-bound kernel more (+30 %) than the separate reduce pass it saves; at
-// 64^3 / 32^3 it is a net win (same-box kernel traces; env
-// CWDM_GBWD_MAXW, default 64).  Elsewhere the dgrad is an ordinary conv (v5 may take it).
+// 32^3 it is a net win (same-box kernel traces).  At 64^3 it was too
+// against v4's plain dgrad (r03), but the warp-specialised kernel now takes those
+// dgrads faster than the fused v4 instance runs: 12 launches 3096 us fused vs 2547 +
+// 371 us of separate reduces (r06, profiles/r06/w_gbwd_maxw_ab.txt).  Env
+// CWDM_GBWD_MAXW, default 32.  Elsewhere the dgrad is an ordinary conv (v5 may take it).
 bool gbwd_grid_ok(const cwdm_conv3d_desc* d) {
-  static const int gb_maxw = [] { const char* e = std::getenv("CWDM_GBWD_MAXW"); return e ? std::atoi(e) : 64; }();
+  static const int gb_maxw = [] { const char* e = std::getenv("CWDM_GBWD_MAXW"); return e ? std::atoi(e) : 32; }();
   return g_gbwd && !g_gbwd->used && dtype_half(d->dtype) && d->W <= gb_maxw && d->a_mode == 0 && d->res_mode < 0 &&
          !d->stats;
 }
