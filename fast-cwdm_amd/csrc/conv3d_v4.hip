@@ -125,14 +125,6 @@ __global__ void __launch_bounds__(256) gn_fin_apply_kernel(GnFinApplyArgs a) {
   const int cs = first ? a.c0 : a.c1, cl0 = first ? c16 : c16 - a.c0;
   const long long P = first ? a.p0 : a.p1;
   const float2* part = reinterpret_cast<const float2*>(first ? a.s0 : a.s1) + (long long)b * P * cs + cl0;
-  // this thread's first x row is loaded before the statistics round trip (at the small
-  // grids a workgroup's 128 voxel slots cover its block: one row per thread in all)
-  const int h = t & 1, vs = t >> 1;
-  const T* xs = reinterpret_cast<const T*>(first ? a.x0 : a.x1) + (long long)b * a.V * cs + cl0 + 8 * h;
-  T* out = reinterpret_cast<T*>(a.out) + (((long long)b * (C / 16) + j) * a.V) * 16 + 8 * h;
-  const int v0 = vb * a.vblk, v1 = min(a.V, v0 + a.vblk);
-  u32x4 xq = u32x4{0u, 0u, 0u, 0u};
-  if (v0 + vs < v1) xq = *reinterpret_cast<const u32x4*>(xs + (long long)(v0 + vs) * cs);
   __shared__ double r1[256], r2[256];
   __shared__ float tab[32];
   {
@@ -179,18 +171,19 @@ __global__ void __launch_bounds__(256) gn_fin_apply_kernel(GnFinApplyArgs a) {
     }
   }
   __syncthreads();
+  const int h = t & 1, vs = t >> 1;
   float sa[8], sb[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) silu_aff_coef(tab[2 * (8 * h + e)], tab[2 * (8 * h + e) + 1], sa[e], sb[e]);
+  const T* xs = reinterpret_cast<const T*>(first ? a.x0 : a.x1) + (long long)b * a.V * cs + cl0 + 8 * h;
+  T* out = reinterpret_cast<T*>(a.out) + (((long long)b * (C / 16) + j) * a.V) * 16 + 8 * h;
+  const int v0 = vb * a.vblk, v1 = min(a.V, v0 + a.vblk);
   for (int v = v0 + vs; v < v1; v += 128) {
-    u32x4 xn = u32x4{0u, 0u, 0u, 0u};
-    if (v + 128 < v1) xn = *reinterpret_cast<const u32x4*>(xs + (long long)(v + 128) * cs);   // next row in flight
     float f[8];
-    unpack<T>(xq, f);
+    unpack<T>(*reinterpret_cast<const u32x4*>(xs + (long long)v * cs), f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] = silu_aff(f[e], sa[e], sb[e]);
     *reinterpret_cast<u32x4*>(out + (long long)v * 16) = pack<T>(f);
-    xq = xn;
   }
 }
 
