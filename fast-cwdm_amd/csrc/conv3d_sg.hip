@@ -498,14 +498,17 @@ bool sg_skip_eligible(const cwdm_conv3d_desc* d) {
 // K slices of a launch: enough work items for the chip (~256), at least one
 // 32-channel chunk per slice (the 16^3 level has 256 tiles: no split)
 namespace {
-int sg_split_for(const cwdm_conv3d_desc* d, int cin) {
+int sg_split_for(const cwdm_conv3d_desc* d, int cin, bool skip = false) {
   const int64_t parts = sg_geom(d).parts();
   const int64_t tiles = d->B * parts * (d->cout / 16);
   const int nch = cin / 32;
   // work-item target (env CWDM_SG_TARGET, A/B knob; 192 since r04: the 8^3
   // level splits K 4 ways instead of 8, 66.28 -> 66.54 steps/s on one box,
-  // config 5 unchanged -- profiles/r04/g_sg_target_ab.txt)
-  static const int64_t target = [] { const char* e = std::getenv("CWDM_SG_TARGET"); return e ? std::atoll(e) : 192LL; }();
+  // config 5 unchanged -- profiles/r04/g_sg_target_ab.txt); the 1x1 skips' own
+  // (env CWDM_SG_SKIP_TARGET, A/B knob, default the same)
+  static const int64_t target3 = [] { const char* e = std::getenv("CWDM_SG_TARGET"); return e ? std::atoll(e) : 192LL; }();
+  static const int64_t target1 = [] { const char* e = std::getenv("CWDM_SG_SKIP_TARGET"); return e ? std::atoll(e) : target3; }();
+  const int64_t target = skip ? target1 : target3;
   if (tiles >= target || nch < 2) return 1;
   int S = (int)std::min<int64_t>((target + tiles - 1) / tiles, nch);
   const int per = (nch + S - 1) / S;
@@ -520,7 +523,7 @@ int sg_ksplit(const cwdm_conv3d_desc* d) { return sg_eligible(d) ? sg_split_for(
 int64_t ksplit_slice_voxels(const cwdm_conv3d_desc* d) {
   return sg_shape_ok(d) ? sg_geom(d).parts() * 256 : d->D * d->H * d->W;
 }
-int sg_skip_ksplit(const cwdm_conv3d_desc* d) { return sg_skip_eligible(d) ? sg_split_for(d, d->b_c0 + d->b_c1) : 1; }
+int sg_skip_ksplit(const cwdm_conv3d_desc* d) { return sg_skip_eligible(d) ? sg_split_for(d, d->b_c0 + d->b_c1, true) : 1; }
 
 // bytes of the K-split counter block a lone launch keeps behind its slices (0 without a split)
 int64_t sg_sync_bytes(int ksplit) { return ksplit > 1 ? kSgSyncWords * 4 : 0; }
