@@ -47,6 +47,9 @@ WG_CASES = [
     ("head_hw_b2", 2, (8, 8, 32), 64, 0, 8, 0, True, 3, 16),
     ("head_hw_cout3", 1, (4, 12, 16), 64, 0, 3, 0, True, 3, 16),
     ("head_hw_nogn", 1, (8, 4, 16), 64, 0, 8, 0, False, 3, 16),
+    # > 512 bricks (two per workgroup) with an odd count per batch entry: a workgroup's
+    # range straddles the batch boundary (its GroupNorm coefficients reload mid-range)
+    ("head_hw_straddle", 2, (100, 44, 16), 64, 0, 8, 0, True, 3, 16),
     ("skip1x1", 2, (4, 8, 16), 64, 32, 64, 0, False, 1, 64),
     ("tiny_grid", 1, (2, 2, 2), 64, 64, 128, 0, True, 3, 128),
     # 1x1 streaming kernel (wgrad1_kernel): R0-like concat 128 + 64 -> 64 over two
