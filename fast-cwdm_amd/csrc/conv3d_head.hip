@@ -45,7 +45,6 @@ struct HeadParams {
   void* out; int out_f32;   // [B][V][cout]
   cwdm_sampler_args samp;   // SAMP only: the step (out unused)
   int mir_vec;              // SAMP: the mirror's 8 channels are 16-byte vectors
-  int xt_dma;               // SAMP, head2: x_t's 8 channels are 16-byte aligned rows (LDS-DMA prefetch)
   unsigned long long* stamps;   // diagnostics (make STAMPS=1): head2 phase stamps, 64 per workgroup
 };
 
@@ -381,24 +380,7 @@ __global__ void __launch_bounds__(512) head2_kernel(HeadParams p, Head2Geo g) {
     float* tfin = reinterpret_cast<float*>(smem + H2T + wv * 2048);   // finished plane [64 voxels][8]
     // SAMP: the sampler step of the plane in tfin (tile tzp of the column at x0, y0):
     // lane = voxel (line lane >> 4, x lane & 15)
-    // xt_dma: the plane's x_t rows ([64 voxels][8] fp32, 2 KB) go to the first half of this
-    // wave's partial-sum region by LDS-DMA at the start of the tile whose MFMAs precede its
-    // sampler step (the region is free from B_k until the partials are written after the
-    // MFMAs), so the epilogue's x_t fetch is off the chain without holding registers across
-    // the MFMA block (those spilled the resident weights)
-    unsigned char* const xlds = smem + H2P + wv * 4096;
-    auto issue_xt = [&](int b, int x0, int y0, int tzp) {
-      const cwdm_sampler_args& a = p.samp;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int vi = (lane >> 1) + 32 * i;
-        const int64_t vv = ((int64_t)(tzp * 4 + pf) * p.H + y0 + (vi >> 4)) * p.W + x0 + (vi & 15);
-        const float* src = a.x_t + b * a.xt_s[0] + vv * a.xt_s[2] + 4 * (lane & 1);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(xlds + i * 1024), 16, 0, 0);
-      }
-    };
-    auto samp_plane = [&](int b, int x0, int y0, int tzp, const float* xpre) {
+    auto samp_plane = [&](int b, int x0, int y0, int tzp) {
       const cwdm_sampler_args& a = p.samp;
       int64_t t = a.t[b];
       t = t < 0 ? 0 : (t >= a.T ? a.T - 1 : t);
@@ -408,14 +390,9 @@ __global__ void __launch_bounds__(512) head2_kernel(HeadParams p, Head2Geo g) {
       const bool philox = noisy && !a.noise && a.noise_philox;
       const int64_t vv = ((int64_t)(tzp * 4 + pf) * p.H + y0 + (lane >> 4)) * p.W + x0 + (lane & 15);
       float xv[8], nzv[8];
-      if (xpre) {
+      const float* xp = a.x_t + b * a.xt_s[0] + vv * a.xt_s[2];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) xv[q] = xpre[q];
-      } else {
-        const float* xp = a.x_t + b * a.xt_s[0] + vv * a.xt_s[2];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) xv[q] = xp[q * a.xt_s[1]];
-      }
+      for (int q = 0; q < 8; ++q) xv[q] = xp[q * a.xt_s[1]];
       if (noisy && a.noise) {
         const float* np = a.noise + b * a.nz_s[0] + vv * a.nz_s[2];
 #pragma unroll
@@ -468,9 +445,6 @@ __global__ void __launch_bounds__(512) head2_kernel(HeadParams p, Head2Geo g) {
         const int z0 = tz * 4;
         [[maybe_unused]] const int ks = tz - tz0;
         H2_STAMP(1 + 3 * ks, tid == 0 && ks < 8 && u == u0);
-        if constexpr (SAMP) {
-          if (p.xt_dma && tz > tz0) issue_xt(b, x0, y0, tz - 1);
-        }
         // SAMP: the previous tile's sampler step runs after this tile's MFMAs (the
         // MFMA waves wait for the fill there)
         hf32x4 acc[2][4];
@@ -498,19 +472,6 @@ __global__ void __launch_bounds__(512) head2_kernel(HeadParams p, Head2Geo g) {
         H2_STAMP(2 + 3 * ks, tid == 0 && ks < 8 && u == u0);
         // the partner's plane goes to it; X_k: every wave is past its ring reads too
         hf32x4 fin[4];
-        [[maybe_unused]] float xpre[8];
-        if constexpr (SAMP) {
-          if (p.xt_dma && tz > tz0) {
-            // the DMA of this tile's start has landed (the MFMA block lies between); read
-            // before the partials overwrite the region
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const float4 x0v = *reinterpret_cast<const float4*>(xlds + lane * 32);
-            const float4 x1v = *reinterpret_cast<const float4*>(xlds + lane * 32 + 16);
-            xpre[0] = x0v.x; xpre[1] = x0v.y; xpre[2] = x0v.z; xpre[3] = x0v.w;
-            xpre[4] = x1v.x; xpre[5] = x1v.y; xpre[6] = x1v.z; xpre[7] = x1v.w;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          }
-        }
         if (h == 0) {
 #pragma unroll
           for (int m = 0; m < 4; ++m) part_mine[m * 64 + lane] = acc[1][m];
@@ -520,7 +481,7 @@ __global__ void __launch_bounds__(512) head2_kernel(HeadParams p, Head2Geo g) {
         }
         // (the partner read this region before B_k: it may be rewritten any time in tile k)
         if constexpr (SAMP) {
-          if (tz > tz0) samp_plane(b, x0, y0, tz - 1, p.xt_dma ? xpre : nullptr);
+          if (tz > tz0) samp_plane(b, x0, y0, tz - 1);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -561,7 +522,7 @@ __global__ void __launch_bounds__(512) head2_kernel(HeadParams p, Head2Geo g) {
       }
       if constexpr (SAMP) {
         // the column's last tile
-        samp_plane(b, x0, y0, tz1 - 1, nullptr);
+        samp_plane(b, x0, y0, tz1 - 1);
       }
 #ifdef CWDM_CONV_STAMPS
       if (p.stamps && tid == 0 && u == u0) {
@@ -790,10 +751,6 @@ int head_sampler_forward(const cwdm_conv3d_desc* d, const cwdm_sampler_args* a, 
   const int mesz = a->mirror ? dtype_size(a->mirror_dtype) : 0;
   p.mir_vec = a->mirror && a->mr_s[1] == 1 && ((uintptr_t)a->mirror % 16) == 0 && (a->mr_s[0] * mesz) % 16 == 0 &&
               (a->mr_s[2] * mesz) % 16 == 0;
-  // head2's x_t prefetch by LDS-DMA (env CWDM_HEAD_XT_DMA=0: the register loads, A/B knob)
-  static const bool xt_dma_on = [] { const char* e = std::getenv("CWDM_HEAD_XT_DMA"); return !(e && e[0] == '0'); }();
-  p.xt_dma = xt_dma_on && a->x_t && a->xt_s[1] == 1 && ((uintptr_t)a->x_t % 16) == 0 && (a->xt_s[0] * 4) % 16 == 0 &&
-             (a->xt_s[2] * 4) % 16 == 0;
   const long long nblk = (long long)p.B * p.tx * p.ty * p.tz;
   CWDM_REQUIRE(nblk < (1LL << 31), CWDM_E_UNSUPPORTED, "conv3d head: grid too large");
   const bool f32m = a->mirror && a->mirror_dtype == CWDM_F32;
