@@ -96,9 +96,6 @@ __device__ __forceinline__ float dsilu(float z, float du) {
   return du * (s * (1.0f + z * (1.0f - s)));
 }
 
-#ifndef GNB_UNR16
-#define GNB_UNR16 8
-#endif
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) gn_bwd_reduce_kernel(const T* __restrict__ x0, int c0, const T* __restrict__ x1,
                                                            int c1, const T* __restrict__ du,
@@ -125,34 +122,15 @@ __global__ void __launch_bounds__(256) gn_bwd_reduce_kernel(const T* __restrict_
   const int xc = c < c0 ? c0 : c1, xo = c < c0 ? c : c - c0;
   if (slot < nslots) {
     const long long v0 = blk * vpb, v1 = v0 + vpb < V ? v0 + vpb : V;
-    // UNR voxels per trip, all their loads issued before the arithmetic (16-bit, MODE 0:
-    // 8 voxels, the loads kept packed until the arithmetic -- twice the bytes in flight
-    // in the same registers)
-    constexpr int UNR = MODE == 1 ? 1 : (MODE == 0 && sizeof(T) == 2 ? GNB_UNR16 : 4);
+    // UNR voxels per trip, all their loads issued before the arithmetic
+    constexpr int UNR = MODE == 1 ? 1 : 4;
     for (long long vb = v0 + slot; vb < v1; vb += (long long)UNR * nslots) {
       float xv[UNR][8], g[UNR][8];
-      if constexpr (MODE == 0 && sizeof(T) == 2) {
-        u4 xr[UNR], gr[UNR];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-          const long long v = vb + (long long)u * nslots < v1 ? vb + (long long)u * nslots : vb;
-          xr[u] = *reinterpret_cast<const u4*>(xs + ((long long)b * V + v) * xc + xo);
-          gr[u] = *reinterpret_cast<const u4*>(du + ((long long)b * V + v) * C + c);
-        }
-#pragma unroll
-        for (int u = 0; u < UNR; ++u)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            xv[u][2 * i] = lo2f<T>(xr[u][i]); xv[u][2 * i + 1] = hi2f<T>(xr[u][i]);
-            g[u][2 * i] = lo2f<T>(gr[u][i]); g[u][2 * i + 1] = hi2f<T>(gr[u][i]);
-          }
-      } else {
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-          const long long v = vb + (long long)u * nslots < v1 ? vb + (long long)u * nslots : vb;
-          load8<T>(xs + ((long long)b * V + v) * xc + xo, xv[u]);
-          load_du<T, MODE>(du, C, c, b, (unsigned)v, d, h, w, g[u]);
-        }
+      for (int u = 0; u < UNR; ++u) {
+        const long long v = vb + (long long)u * nslots < v1 ? vb + (long long)u * nslots : vb;
+        load8<T>(xs + ((long long)b * V + v) * xc + xo, xv[u]);
+        load_du<T, MODE>(du, C, c, b, (unsigned)v, d, h, w, g[u]);
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
