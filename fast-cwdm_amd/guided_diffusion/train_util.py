@@ -240,7 +240,8 @@ class TrainLoop:
             self._report_finite(*pending)
 
     def forward_backward(self, batch, cond, label=None):
-        for p in self.model.parameters():
+        plist = self.model.param_list() if hasattr(self.model, "param_list") else self.model.parameters()
+        for p in plist:
             p.grad = None
         batch_size = batch["t1n"].shape[0] if self.mode == "i2i" else batch.shape[0]
         t, weights = self.schedule_sampler.sample(batch_size, dist_util.dev())

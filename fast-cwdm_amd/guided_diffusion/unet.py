@@ -158,6 +158,12 @@ class UNetModel(nn.Module):
         order): the optimizer, gradient all-reduce and weight packing run over
         flat ranges; the views share the buffer's version counter."""
         params = list(self.parameters())
+        # the hot paths (forward, packs, backward, zero_grad) read this list: a
+        # traversal of the module tree per call cost ~0.2-0.3 ms of host time,
+        # several per training step, while the GPU waited at the step's start
+        # (parameters are views of the flat buffer, never re-registered after
+        # construction; _apply re-flattens and refreshes it)
+        self._param_list = params
         if not params:
             return
         dev = params[0].device
@@ -181,10 +187,17 @@ class UNetModel(nn.Module):
     def flat_params(self):
         return self._flat
 
+    def param_list(self):
+        """The parameters in registration (state_dict) order, cached."""
+        pl = self.__dict__.get("_param_list")
+        if pl is None:
+            pl = self._param_list = list(self.parameters())
+        return pl
+
     def flat_grad(self):
         """Flat fp32 gradient of the last backward (the buffer the native backward
         wrote when the .grad tensors still alias it, else a concatenation)."""
-        params = list(self.parameters())
+        params = self.param_list()
         g = self._last_grad_flat
         if g is not None and params[0].grad is not None and params[0].grad.data_ptr() == g.data_ptr() and \
                 params[-1].grad.data_ptr() == g[g.numel() - params[-1].numel():].data_ptr():
@@ -242,13 +255,13 @@ class UNetModel(nn.Module):
         # counter (set_data); writers of the flat buffer bump the flat's, in-place
         # ops on a parameter bump that parameter's, raw writers call
         # mark_params_changed -- the key covers all three
-        params = list(self.parameters())
+        params = self.param_list()
         return (self.compute_dtype, self._param_gen, self._flat._version) + \
             tuple((p.data_ptr(), p._version) for p in params)
 
     def packed_weights(self):
         """Packed kernel-layout weights; re-packed whenever a parameter changed."""
-        params = list(self.parameters())
+        params = self.param_list()
         key = self._weights_key()
         if self._packed is None or self._packed_key != key:
             arr = self._src_array(params, key)
@@ -279,7 +292,7 @@ class UNetModel(nn.Module):
 
     def packed_bwd_weights(self):
         """Transposed/flipped dgrad weight layouts for the native backward."""
-        params = list(self.parameters())
+        params = self.param_list()
         key = self._weights_key()
         if self._packed_bwd is None or self._packed_bwd_key != key:
             arr = self._src_array(params, key)
@@ -328,7 +341,7 @@ class UNetModel(nn.Module):
             assert x.device == self.devices[0], f"{x.device=} does not match {self.devices[0]=}"
         B, C, D, H, W = x.shape
         assert C == self.in_channels
-        params = list(self.parameters())
+        params = self.param_list()
         if th.is_grad_enabled() and any(p.requires_grad for p in params):
             return _UNetTrain.apply(self, x, timesteps, *params)
         xin, t = self._prep_inputs(x, timesteps)
@@ -409,7 +422,7 @@ class _UNetTrain(th.autograd.Function):
         # accumulation) the view is returned and autograd handles it as usual
         out = []
         o = 0
-        for p, (_, shape) in zip(model.parameters(), plan.param_specs):
+        for p, (_, shape) in zip(model.param_list(), plan.param_specs):
             n = 1
             for s_ in shape:
                 n *= s_
