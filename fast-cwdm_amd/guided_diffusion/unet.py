@@ -36,6 +36,8 @@ def _register(root, dotted, param):
     mod.register_parameter(parts[-1], param)
 
 
+_NO_PARAM_CACHE = os.environ.get("CWDM_PARAM_CACHE", "1") == "0"
+
 class UNetModel(nn.Module):
     def __init__(
         self,
@@ -188,7 +190,10 @@ class UNetModel(nn.Module):
         return self._flat
 
     def param_list(self):
-        """The parameters in registration (state_dict) order, cached."""
+        """The parameters in registration (state_dict) order, cached (env
+        CWDM_PARAM_CACHE=0: a fresh traversal per call, A/B knob)."""
+        if _NO_PARAM_CACHE:
+            return list(self.parameters())
         pl = self.__dict__.get("_param_list")
         if pl is None:
             pl = self._param_list = list(self.parameters())
