@@ -39,8 +39,6 @@ def _register(root, dotted, param):
 _NO_PARAM_CACHE = os.environ.get("CWDM_PARAM_CACHE", "1") == "0"
 # direct_grads training forward through one anchor input (env CWDM_GRAD_ANCHOR=0: the parameters, A/B knob)
 _ANCHOR_ON = os.environ.get("CWDM_GRAD_ANCHOR", "1") != "0"
-# the backward reuses the forward's weights key (env CWDM_BWD_KEY_REUSE=0: recomputed, A/B knob)
-_BWD_KEY_REUSE = os.environ.get("CWDM_BWD_KEY_REUSE", "1") != "0"
 
 class UNetModel(nn.Module):
     def __init__(
@@ -299,12 +297,10 @@ class UNetModel(nn.Module):
         self._src_ptrs = (ptrs, arr)
         return arr
 
-    def packed_bwd_weights(self, key=None):
-        """Transposed/flipped dgrad weight layouts for the native backward (key:
-        the weights key the caller already computed for these parameters)."""
+    def packed_bwd_weights(self):
+        """Transposed/flipped dgrad weight layouts for the native backward."""
         params = self.param_list()
-        if key is None:
-            key = self._weights_key()
+        key = self._weights_key()
         if self._packed_bwd is None or self._packed_bwd_key != key:
             arr = self._src_array(params, key)
             old = self._packed_bwd if (self._packed_bwd is not None and
@@ -407,18 +403,15 @@ class _UNetTrain(th.autograd.Function):
             plan.workspace_bytes(B, D, H, W)
         ws = th.empty(nbytes, dtype=th.uint8, device=x.device)
         out_nd = th.empty((B, D, H, W, model.out_channels), dtype=th.float32, device=x.device)
-        packed = model.packed_weights()
-        plan.forward(packed, xin, t, out_nd, B, D, H, W, ws=ws)
+        plan.forward(model.packed_weights(), xin, t, out_nd, B, D, H, W, ws=ws)
         ctx.model = model
-        # the backward runs on the weights this forward packed (and their key: the
-        # per-parameter key costs ~0.14 ms of host time at the backward's start)
-        ctx.state = (xin, t, ws, (B, D, H, W), packed, model._packed_key)
+        ctx.state = (xin, t, ws, (B, D, H, W))
         return model._to_ncdhw(out_nd)
 
     @staticmethod
     def backward(ctx, gout):
         model = ctx.model
-        xin, t, ws, (B, D, H, W), packed, key = ctx.state
+        xin, t, ws, (B, D, H, W) = ctx.state
         ctx.state = None
         plan = model.plan
         oc = model.out_channels
@@ -427,9 +420,7 @@ class _UNetTrain(th.autograd.Function):
         ops.copy3(gout.contiguous().float(), (oc * V, V, 1), dout, (V * oc, 1, oc), B, oc, V)
         grads = th.empty(plan.grad_numel, dtype=th.float32, device=xin.device)
         gws = th.empty(plan.grad_workspace_bytes(B, D, H, W), dtype=th.uint8, device=xin.device)
-        if not _BWD_KEY_REUSE or key != model._packed_key:   # (re-packed since the forward: the current weights)
-            packed, key = model.packed_weights(), model._packed_key
-        packed_bwd = model.packed_bwd_weights(key if _BWD_KEY_REUSE else None)
+        packed, packed_bwd = model.packed_weights(), model.packed_bwd_weights()
         hook = model._grad_hook
         nseg = plan.num_segments
         if hook is None:
