@@ -9,10 +9,16 @@ parameters, ``param_groups[0]["lr"]`` (annealed by TrainLoop._anneal_lr) and
 ``state_dict()`` layout are torch.optim.AdamW's, so optimizer checkpoints stay
 interchangeable with the reference's.
 """
+import os
+
 import torch
 
 from ._lib import check, lib
 from .ops import _need_cuda, _stream
+
+
+# env CWDM_PER_PARAM_STEP=1: a fresh step tensor per parameter each step (the old host cost, A/B knob)
+_PER_PARAM_STEP = os.environ.get("CWDM_PER_PARAM_STEP", "0") == "1"
 
 
 class FlatAdamW(torch.optim.Optimizer):
@@ -47,10 +53,14 @@ class FlatAdamW(torch.optim.Optimizer):
         self._bind_state()
 
     def _bind_state(self):
+        # one step tensor shared by every parameter's state (torch keeps one per
+        # parameter: 230 host fill_ calls per step, ~0.5 ms of host time while the
+        # next step waited to launch); state_dict() hands each entry the same value
+        self._step_t = torch.tensor(float(self._step))
         o = 0
         for p in self.param_groups[0]["params"]:
             n = p.numel()
-            self.state[p] = {"step": torch.tensor(float(self._step)),
+            self.state[p] = {"step": self._step_t,
                              "exp_avg": self._m[o:o + n].view_as(p),
                              "exp_avg_sq": self._v[o:o + n].view_as(p)}
             o += n
@@ -77,9 +87,19 @@ class FlatAdamW(torch.optim.Optimizer):
         # see writes to the flat buffer)
         torch.autograd.graph.increment_version(self._flat)
         self._model.mark_params_changed()
-        for st in self.state.values():
-            st["step"].fill_(float(self._step))
+        if _PER_PARAM_STEP:
+            for st in self.state.values():
+                st["step"] = torch.tensor(float(self._step))
+        else:
+            self._step_t.fill_(float(self._step))
         return loss
+
+    def state_dict(self):
+        # per-parameter step tensors in the saved form, as torch.optim.AdamW keeps them
+        # (a shared one loaded into torch's AdamW would be incremented once per parameter)
+        sd = super().state_dict()
+        sd["state"] = {k: {**v, "step": v["step"].clone()} if "step" in v else v for k, v in sd["state"].items()}
+        return sd
 
     def zero_grad(self, set_to_none=True):
         for p in self.param_groups[0]["params"]:

@@ -804,6 +804,29 @@ def test_production_unet_backward_skip_dgrad_row_major_epilogue_bitwise(dtype):
     assert not bad, bad[:8]
 
 
+def test_flat_adamw_state_dict_per_parameter_steps():
+    """FlatAdamW keeps one step tensor for all parameters (one host fill per step);
+    its state_dict hands out a separate step tensor per parameter, as
+    torch.optim.AdamW keeps them, and a reload restores the step count."""
+    from cwdm_hip.optim import FlatAdamW
+    P, x, t, R = _prod_case()
+    model = _product_model(PROD_CFG, 32, P, "bf16")
+    opt = FlatAdamW(model, lr=1e-3, weight_decay=0.01, direct_grads=True)
+    for _ in range(2):
+        opt.zero_grad()
+        out = model(x.to(DEV), t.to(DEV))
+        (out * R.to(DEV)).sum().backward()
+        opt.step()
+    sd = opt.state_dict()
+    steps = [v["step"] for v in sd["state"].values()]
+    assert len(steps) == len(list(model.parameters()))
+    assert len({id(s) for s in steps}) == len(steps)
+    assert all(float(s) == 2.0 for s in steps)
+    opt2 = FlatAdamW(model, lr=1e-3, weight_decay=0.01)
+    opt2.load_state_dict(sd)
+    assert opt2._step == 2 and torch.equal(opt2._m, opt._m) and torch.equal(opt2._v, opt._v)
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
 def test_production_training_two_steps_bitwise_reproducible(dtype):
     """Determinism of the training step: two runs of two steps each (forward with
