@@ -450,10 +450,24 @@ __global__ void __launch_bounds__(256) channel_sum_kernel(const T* __restrict__ 
 // norm/grad_max, train_util.py:370-375 of the reference) from the same pass, as the bit patterns of
 // non-negative floats -- unsigned order = float order, a NaN above +inf, so NaN propagates -- one
 // atomic max per workgroup (exact whatever the order)
+// DEV (the sync-free loss-scaled step): the step count lives on the device (dstep, the
+// steps taken so far) and found_inf (GradScaler's, after unscale_) skips the whole
+// update, as GradScaler.step skips optimizer.step; the bias corrections are the host's
+// double-precision formulas on the device count (adamw_step_inc advances it afterwards)
+template <bool DEV>
 __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long long n,
                                                    float decay, float w1, float b2, float w2, float neg_step,
-                                                   float bc2_sqrt, float eps, unsigned* __restrict__ maxabs) {
+                                                   float bc2_sqrt, float eps, unsigned* __restrict__ maxabs,
+                                                   const double* __restrict__ dstep, const float* __restrict__ found_inf,
+                                                   double lr, double beta1, double beta2) {
+  if constexpr (DEV) {
+    if (found_inf && *found_inf != 0.f) return;
+    const double sd = *dstep + 1.0;
+    const double bc1 = 1.0 - pow(beta1, sd), bc2 = 1.0 - pow(beta2, sd);
+    neg_step = (float)(-(lr / bc1));
+    bc2_sqrt = (float)sqrt(bc2);
+  }
   const long long stride = (long long)gridDim.x * blockDim.x;
   unsigned mp = 0u, mg = 0u;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -483,6 +497,10 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
     atomicMax(maxabs, mp);
     atomicMax(maxabs + 1, mg);
   }
+}
+
+__global__ void adamw_step_inc(double* __restrict__ dstep, const float* __restrict__ found_inf) {
+  if (threadIdx.x == 0 && !(found_inf && *found_inf != 0.f)) *dstep = *dstep + 1.0;
 }
 
 __device__ __forceinline__ float silu_ref(float v) { return v / (1.0f + expf(-v)); }
@@ -909,13 +927,33 @@ int adamw_launch(float* p, const float* g, float* m, float* v, int64_t n, double
   const float bc2s = (float)std::sqrt(bc2);
   long long blocks = ceil_div(n, 256);
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long long)n,
-                     decay, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), neg_step, bc2s, (float)eps,
-                     reinterpret_cast<unsigned*>(maxabs));
+  hipLaunchKernelGGL(adamw_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
+                     (long long)n, decay, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), neg_step, bc2s,
+                     (float)eps, reinterpret_cast<unsigned*>(maxabs), nullptr, nullptr, lr, beta1, beta2);
   CWDM_LAUNCHED();
   return CWDM_OK;
 }
 }  // namespace
+
+extern "C" int cwdm_adamw_device_step(float* p, const float* g, float* m, float* v, int64_t n, double lr,
+                                      double beta1, double beta2, double eps, double weight_decay, double* step,
+                                      const float* found_inf, cwdm_stream_t stream) {
+  CWDM_REQUIRE(p && g && m && v && step, CWDM_E_INVALID, "cwdm_adamw_device_step: null pointer");
+  CWDM_REQUIRE(n >= 0, CWDM_E_INVALID, "cwdm_adamw_device_step: bad size");
+  hipStream_t s = (hipStream_t)stream;
+  if (n > 0) {
+    const float decay = (float)(1.0 - lr * weight_decay);
+    long long blocks = ceil_div(n, 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(adamw_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, (long long)n, decay,
+                       (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), 0.f, 1.f, (float)eps, nullptr, step,
+                       found_inf, lr, beta1, beta2);
+    CWDM_LAUNCHED();
+  }
+  hipLaunchKernelGGL(adamw_step_inc, dim3(1), dim3(64), 0, s, step, found_inf);
+  CWDM_LAUNCHED();
+  return CWDM_OK;
+}
 
 extern "C" int cwdm_adamw(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
                           double beta2, double eps, double weight_decay, int64_t step, cwdm_stream_t stream) {

@@ -172,6 +172,8 @@ _PROTOS = {
                                         vp, i64, vp]),
     "cwdm_adamw": (ctypes.c_int, [vp, vp, vp, vp, i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, ctypes.c_double, i64, vp]),
+    "cwdm_adamw_device_step": (ctypes.c_int, [vp, vp, vp, vp, i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                               ctypes.c_double, ctypes.c_double, vp, vp, vp]),
     "cwdm_adamw_maxabs": (ctypes.c_int, [vp, vp, vp, vp, i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_double, ctypes.c_double, i64, vp, vp]),
     "cwdm_unet_create": (ctypes.c_int, [ctypes.POINTER(UNetConfig), ctypes.POINTER(vp)]),

@@ -46,6 +46,8 @@ class FlatAdamW(torch.optim.Optimizer):
         self._m = torch.zeros_like(flat)
         self._v = torch.zeros_like(flat)
         self._step = 0
+        self._dstep = None   # device step count once a found_inf step ran (sync-free loss scaling)
+        self._fi_keep = None
         # track_maxabs: step() also leaves last_maxabs = [max |p| before the update, max |g|]
         # (a fresh 2-element device tensor per step, cwdm_adamw_maxabs: the same pass)
         self.track_maxabs = False
@@ -66,7 +68,11 @@ class FlatAdamW(torch.optim.Optimizer):
             o += n
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, found_inf=None):
+        """found_inf (device tensor, GradScaler's after unscale_): the sync-free
+        loss-scaled step -- the update is skipped on the device when it is
+        non-zero (GradScaler.step would read it back first and skip the call), and
+        from then on the step count lives on the device (state_dict() reads it)."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -74,6 +80,18 @@ class FlatAdamW(torch.optim.Optimizer):
         g = self._model.flat_grad()
         grp = self.param_groups[0]
         b1, b2 = grp["betas"]
+        if found_inf is not None or self._dstep is not None:
+            if self._dstep is None:
+                self._dstep = torch.tensor(float(self._step), dtype=torch.float64, device=self._flat.device)
+            fi = found_inf.reshape(-1)[:1].float().contiguous() if found_inf is not None else None
+            check(lib().cwdm_adamw_device_step(self._flat.data_ptr(), g.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
+                                               self._flat.numel(), float(grp["lr"]), float(b1), float(b2),
+                                               float(grp["eps"]), float(grp["weight_decay"]), self._dstep.data_ptr(),
+                                               fi.data_ptr() if fi is not None else None, _stream()), "AdamW.step")
+            self._fi_keep = fi   # (alive until the launch has read it)
+            torch.autograd.graph.increment_version(self._flat)
+            self._model.mark_params_changed()
+            return loss
         self._step += 1
         args = (self._flat.data_ptr(), g.data_ptr(), self._m.data_ptr(), self._v.data_ptr(), self._flat.numel(),
                 float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), float(grp["weight_decay"]), self._step)
@@ -97,6 +115,9 @@ class FlatAdamW(torch.optim.Optimizer):
     def state_dict(self):
         # per-parameter step tensors in the saved form, as torch.optim.AdamW keeps them
         # (a shared one loaded into torch's AdamW would be incremented once per parameter)
+        if self._dstep is not None:   # the device count (skipped steps not counted): one read-back here
+            self._step = int(self._dstep.item())
+            self._step_t.fill_(float(self._step))
         sd = super().state_dict()
         sd["state"] = {k: {**v, "step": v["step"].clone()} if "step" in v else v for k, v in sd["state"].items()}
         return sd
@@ -118,4 +139,5 @@ class FlatAdamW(torch.optim.Optimizer):
                 step = int(float(st["step"]))
             o += n
         self._step = step
+        self._dstep = None
         self._bind_state()

@@ -511,6 +511,16 @@ int cwdm_adamw(float* p, const float* g, float* m, float* v, int64_t n, double l
 int cwdm_adamw_maxabs(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
                       double eps, double weight_decay, int64_t step, float* maxabs, cwdm_stream_t stream);
 
+/* cwdm_adamw with the step count on the device (the sync-free loss-scaled step of
+ * TrainLoop's fp16 path): step = device double, the steps taken so far; found_inf
+ * (device float, GradScaler's after unscale_, may be NULL) != 0 skips the whole
+ * update and leaves step unchanged, as GradScaler.step skips optimizer.step;
+ * otherwise the update uses step + 1 for the bias corrections (double precision,
+ * as cwdm_adamw computes them on the host) and step is advanced. */
+int cwdm_adamw_device_step(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
+                           double beta2, double eps, double weight_decay, double* step, const float* found_inf,
+                           cwdm_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * U-Net plan: the whole UNetModel.forward (guided_diffusion/unet.py:754-800)
  * for the run.sh configuration family (no attention, resblock_updown=True,

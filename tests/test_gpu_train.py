@@ -683,6 +683,51 @@ def test_trainloop_runs_and_learns(tmp_path, monkeypatch):
         dist.destroy_process_group()
 
 
+def test_trainloop_fp16_device_scaled_step_matches_gradscaler_step(tmp_path, monkeypatch):
+    """fp16 TrainLoop (dynamic loss scaling): the sync-free step (FlatAdamW skips
+    on GradScaler's device found_inf, the step count on the device) against
+    GradScaler.step (found_inf read back, optimizer.step skipped on the host):
+    the same parameters and moments after a normal step and two overflowing ones
+    (scale forced to 2^60: both skip, the scale halves each time), and the same
+    saved step count."""
+    import numpy as np
+    from guided_diffusion import dist_util, train_util
+    monkeypatch.setenv("CWDM_LOGDIR", str(tmp_path))
+    dist_util.setup_dist()
+    P = ou.random_params(seed=43, **cases.C1_CFG)
+    batch = cases.data.brats_batch(32, seed=6, batch=1)
+    bdev = {k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in batch.items()}
+    res = {}
+    for dev_step in (False, True):
+        model, diffusion = _c1_model_and_diffusion(P, dtype="fp16")
+        loop = train_util.TrainLoop(model=model, diffusion=diffusion, data=[batch], batch_size=1, in_channels=32,
+                                    image_size=64, microbatch=-1, lr=1e-4, ema_rate="0.9999", log_interval=100,
+                                    contr="t1n", save_interval=100, resume_checkpoint="", resume_step=0,
+                                    lr_anneal_steps=0, mode="i2i", diffusion_steps=1000)
+        assert loop.grad_scaler.is_enabled()
+        loop.device_scaled_step = dev_step
+        torch.manual_seed(0)
+        np.random.seed(0)
+        p_after = []
+        for i in range(3):
+            if i == 1:
+                loop.grad_scaler.update(2.0 ** 60)
+            loop.run_step(bdev, {}, info={})
+            p_after.append(model.flat_params.detach().clone())
+        torch.cuda.synchronize()
+        step = float(next(iter(loop.opt.state_dict()["state"].values()))["step"])
+        res[dev_step] = (p_after, loop.opt._m.clone(), loop.opt._v.clone(), step, float(loop.grad_scaler.get_scale()))
+    (pa, ma, va, sa, ka), (pb, mb, vb, sb, kb) = res[False], res[True]
+    assert sa == sb == 1.0, (sa, sb)
+    assert ka == kb == 2.0 ** 58, (ka, kb)
+    assert torch.equal(pa[1], pa[0]) and torch.equal(pb[1], pb[0]) and torch.equal(pb[2], pb[0])
+    for x, y in ((pa[2], pb[2]), (ma, mb), (va, vb)):
+        assert float((x - y).abs().max()) <= 1e-6 * float(x.abs().max().clamp_min(1e-30)), float((x - y).abs().max())
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 # --------------------------------------------------------------------------- production-size backward (config 3)
 PROD_CFG = dict(in_channels=32, model_channels=64, out_channels=8, num_res_blocks=2, channel_mult=(1, 2, 2, 4, 4))
 PROD_GRID = (32, 32, 64)   # W % 32 == 0 at R0 and R1: the DMA-staged kernel runs forward and dgrad
