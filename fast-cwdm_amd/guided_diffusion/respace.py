@@ -5,6 +5,8 @@
 re-uploaded per call (:127-132), and the native sampling loop reads the mapped
 value on the host so no per-step H2D copy or sync remains.
 """
+import os
+
 import numpy as np
 import torch as th
 
@@ -38,6 +40,9 @@ def space_timesteps(num_timesteps, section_counts):
         start_idx += size
     return set(all_steps)
 
+
+# env CWDM_TSMAP_SHARED=0: a device timestep map per wrapper (the old per-step copy, A/B knob)
+_SHARED_TS_MAP = os.environ.get("CWDM_TSMAP_SHARED", "1") != "0"
 
 class SpacedDiffusion(GaussianDiffusion):
     def __init__(self, use_timesteps, **kwargs):
@@ -74,7 +79,12 @@ class SpacedDiffusion(GaussianDiffusion):
     def _wrap_model(self, model):
         if isinstance(model, _WrappedModel):
             return model
-        return _WrappedModel(model, self.timestep_map, self.rescale_timesteps, self.original_num_steps)
+        # the device copy of timestep_map is shared by every wrapper of this diffusion:
+        # training_losses wraps the model on every step, and a fresh th.tensor(list,
+        # device=cuda) per wrapper is a pageable host->device copy that waits for the
+        # whole queue (the config-5 training step spent ~6 ms of host time blocked there)
+        maps = self.__dict__.setdefault("_ts_maps", {}) if _SHARED_TS_MAP else None
+        return _WrappedModel(model, self.timestep_map, self.rescale_timesteps, self.original_num_steps, maps)
 
     def _scale_timesteps(self, t):
         return t  # scaling is done by the wrapped model
@@ -87,12 +97,12 @@ class SpacedDiffusion(GaussianDiffusion):
 
 
 class _WrappedModel:
-    def __init__(self, model, timestep_map, rescale_timesteps, original_num_steps):
+    def __init__(self, model, timestep_map, rescale_timesteps, original_num_steps, maps=None):
         self.model = model
         self.timestep_map = timestep_map
         self.rescale_timesteps = rescale_timesteps
         self.original_num_steps = original_num_steps
-        self._maps = {}
+        self._maps = maps if maps is not None else {}
 
     def parameters(self):
         return self.model.parameters()
